@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node decode tokens/s (+ p50 per-token latency) of the MI355X-native
+pipeline engine on Llama-3-70B Q4_K, PP = number of GPUs (BASELINE.json: "decode tokens/sec (whole
+node) + p50/token, Llama-3-70B PP=8 and 8B PP=1"; reference headline 2-3 tok/s for 70B, PDF p.12).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5                  # PP=1 on one MI355X
+    torchrun --nproc-per-node 8 bench.py --gpus 8 --steps 20 ...     # PP=8, one rank per GPU
+
+Weights are random-init directly in HBM with the exact Llama-3-70B architecture and Q4_K block
+format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
+cost-balanced split with the LM head on the last stage); activations move stage to stage with
+RCCL send/recv over xGMI; M = N micro-batches of `--mb-size` sequences circulate through the
+piped ring.  Weak scaling: per-GPU work is fixed (every stage streams its own weights once per
+micro-batch per round), global batch = N * mb_size sequences.
+The timed region is exactly K decode rounds (every sequence emits one token per round),
+bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_TOK_S = 2.5   # Llama-3-70B, 2-3 tok/s (PDF p.12) -> midpoint
+
+MODELS = {
+    "llama3-70b": dict(name="Llama-3-70B", n_layer=80, d_model=8192, n_head=64, n_head_kv=8, d_ff=28672,
+                       vocab=128256, rope_base=500000.0),
+    "llama3-8b": dict(name="Llama-3-8B", n_layer=32, d_model=4096, n_head=32, n_head_kv=8, d_ff=14336,
+                      vocab=128256, rope_base=500000.0),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="llama3-70b", choices=sorted(MODELS))
+    ap.add_argument("--ftype", default="Q4_K")
+    ap.add_argument("--mb-size", type=int, default=16, help="sequences per micro-batch (<= 16)")
+    ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = #GPUs)")
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus > 1 must be launched with torchrun (one rank per GPU)", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from mipipe.engine import Engine, rccl_unique_id_hex
+
+    n_mb = args.n_mb or world
+    max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
+    cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
+               prefill_chunk=256, graphs=not args.no_graphs, split="cost", seed=1234)
+    if world > 1:
+        ids = [rccl_unique_id_hex() for _ in range(world)] if rank == 0 else None
+        obj = [ids]
+        dist.broadcast_object_list(obj, src=0)
+        cfg.update(mode="mp", world=world, rank=rank, device=local_rank, rccl_ids=obj[0])
+    else:
+        cfg.update(mode="local", stages=1, devices=[local_rank])
+
+    eng = Engine(**cfg)
+    g = torch.Generator().manual_seed(0)
+    prompts = torch.randint(3, MODELS[args.model]["vocab"], (n_mb * args.mb_size, args.prompt_len),
+                            generator=g).tolist()
+    eng.start(prompts)
+    if args.warmup:
+        eng.decode(args.warmup)
+
+    def bracket():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    bracket()
+    t0 = time.perf_counter()
+    st = eng.decode(args.steps)
+    bracket()
+    ms = (time.perf_counter() - t0) * 1e3
+
+    tms = sorted(st.get("token_ms", []))
+    p50 = tms[len(tms) // 2] if tms else 0.0
+    vals = torch.tensor([ms, p50], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
+    ms, p50 = float(vals[0]), float(vals[1])
+    n_tok = args.steps * n_mb * args.mb_size
+    value = n_tok / (ms / 1e3)
+    if rank == 0:
+        m = MODELS[args.model]
+        print(json.dumps({
+            "metric": "decode tokens/sec (whole node) + p50/token",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms / args.steps, 4),
+            "p50_token_ms": round(p50, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_TOK_S, 2) if args.model == "llama3-70b" else None,
+            "dtype": "bf16-class: f16 MFMA on dequantized " + args.ftype + " weights, f32 accumulate",
+            "data": "synthetic prompts, random-init weights (GGUF " + args.ftype + " blocks generated in HBM)",
+            "config": {"model": f"{m['name']} {args.ftype}", "global_batch": n_mb * args.mb_size,
+                       "seq_len": args.prompt_len, "parallelism": f"pp{world}",
+                       "micro_batches": n_mb, "mb_size": args.mb_size, "max_ctx": max_ctx,
+                       "stages": eng.info["stages"]},
+        }), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

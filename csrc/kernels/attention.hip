@@ -1,0 +1,206 @@
+// Paged GQA attention on MFMA (K7): flash-decoding split-K for decode, the same kernel with
+// several query tokens per row group for (chunked) prefill.
+//
+// One workgroup = (row group, kv head, kv split).  A row group is up to 16 MFMA rows
+// rho = tq_i * G + g (tq tokens of ONE sequence x the G query heads sharing kv head `kvh`).
+// Per 32-key chunk a wave computes S^T = K * Q^T with two chains of v_mfma_f32_16x16x32_f16
+// (A = K rows, B = Q^T), with key rows permuted pi(c, R) = 8(R>>2) + 4c + (R&3) so that the
+// exponentiated scores already sit in the lanes/registers of the B operand of the P.V product
+// (O^T = V^T P^T, A = V^T read from the transposed V page) -- no LDS round trip, no shuffles for P.
+// Online softmax in registers; 4 waves interleave chunks and are merged through LDS; splits are
+// merged by attn_combine (LSE merge).  KV pages hold 64 tokens: K [64][Dp], V^T [Dp][64].
+#include "kcommon.h"
+#include "../runtime/kernels_api.h"
+
+namespace mpk {
+using namespace mp;
+
+template <int DP>
+__global__ __launch_bounds__(256) void attn_kernel(const AttnParams p) {
+  constexpr int KK = DP / 32;   // k-steps of QK^T
+  constexpr int DT = DP / 16;   // 16-row d tiles of O^T
+  __shared__ float sm_m[4][16], sm_l[4][16];
+  __shared__ float sm_o[4][16][DP];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q4 = lane >> 4, col = lane & 15;
+  const int grp = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
+  const int G = p.Hq / p.Hkv;
+  const int t0 = grp * p.tq;
+  const int tq_i = col / G, g = col % G;
+  const int t = t0 + tq_i;
+  const bool rvalid = (tq_i < p.tq) && (t < p.M) && (col < G * p.tq);
+  const int tl = min(t0 + p.tq, p.M) - 1;           // last token of the group
+  const int slot = p.slot[t0];
+  const int maxlen = p.kvlen[tl];
+  const int my_len = rvalid ? p.kvlen[t] : 0;
+  const int h = kvh * G + g;
+
+  const int start = z * p.split_len;
+  const int end = min(start + p.split_len, maxlen);
+  const size_t row_id = (size_t)t * p.Hq + h;
+
+  if (start >= end) {
+    // empty split: publish (m=-inf, l=0); combine skips it
+    if (wave == 0 && q4 == 0 && rvalid && p.n_split > 1) {
+      float* ml = p.ml_part + ((size_t)z * p.M * p.Hq + row_id) * 2;
+      ml[0] = -INFINITY; ml[1] = 0.f;
+    }
+    return;
+  }
+
+  // Q^T fragments: lane holds q[t][h][d = 32kk + 8q4 + j]
+  half8_t qf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    half8_t zf = {};
+    qf[kk] = rvalid ? *reinterpret_cast<const half8_t*>(p.q + row_id * DP + 32 * kk + 8 * q4) : zf;
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int32_t* bt = p.block_table + (size_t)slot * p.max_pages;
+  const int nch = (end - start + 31) / 32;
+  const int R = col;
+  const int krow0 = 8 * (R >> 2) + (R & 3);      // pi(c, R) - 4c
+
+  for (int ci = wave; ci < nch; ci += 4) {
+    const int P0 = start + ci * 32;
+    const int page = bt[P0 >> 6];
+    const int in_page = P0 & 63;
+    const f16* kbase = p.k_cache + ((size_t)page * p.Hkv + kvh) * 64 * DP;
+    const f16* vbase = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
+    half8_t kf[2][KK];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        kf[c][kk] = *reinterpret_cast<const half8_t*>(kbase + (size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4);
+    half8_t vf[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      vf[dt] = *reinterpret_cast<const half8_t*>(vbase + (size_t)(16 * dt + col) * 64 + in_page + 8 * q4);
+
+    f32x4 s[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) a = mfma16x16x32(kf[c][kk], qf[kk], a);
+      s[c] = a;
+    }
+    // lane holds scores for row `col`, keys P0 + 8*q4 + 4c + i
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kpos = P0 + 8 * q4 + 4 * c + i;
+        const float v = kpos < my_len ? s[c][i] : -INFINITY;
+        s[c][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+    float pv[2][4];
+    float psum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = (m_new == -INFINITY) ? 0.f : __expf(s[c][i] - m_new);
+        pv[c][i] = e;
+        psum += e;
+      }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    half8_t pf = {(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
+                  (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      f32x4 acc = o[dt] * alpha;
+      o[dt] = mfma16x16x32(vf[dt], pf, acc);
+    }
+  }
+  // per-row totals across the 4 lane groups
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+  if (q4 == 0) { sm_m[wave][col] = m_run; sm_l[wave][col] = l_run; }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[wave][col][16 * dt + 4 * q4 + i] = o[dt][i];
+  __syncthreads();
+
+  // merge the 4 waves: thread handles (row, d) pairs
+  for (int e = threadIdx.x; e < 16 * DP; e += 256) {
+    const int row = e / DP, d = e % DP;
+    const int rt = t0 + row / G;
+    const bool ok = (row / G < p.tq) && (rt < p.M) && (row < G * p.tq);
+    if (!ok) continue;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][row]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (sm_m[w][row] == -INFINITY) continue;
+      const float f = __expf(sm_m[w][row] - M);
+      L += sm_l[w][row] * f;
+      O += sm_o[w][row][d] * f;
+    }
+    const int hh = kvh * G + row % G;
+    const size_t rid = (size_t)rt * p.Hq + hh;
+    if (p.n_split == 1) {
+      if (d < p.hd) p.out[(size_t)rt * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
+    } else {
+      p.o_part[((size_t)z * p.M * p.Hq + rid) * DP + d] = O;
+      if (d == 0) {
+        float* ml = p.ml_part + ((size_t)z * p.M * p.Hq + rid) * 2;
+        ml[0] = M; ml[1] = L;
+      }
+    }
+  }
+}
+
+template <int DP>
+__global__ __launch_bounds__(DP) void attn_combine_kernel(const AttnParams p) {
+  const int rid = blockIdx.x;                // t*Hq + h
+  const int t = rid / p.Hq, h = rid % p.Hq;
+  const int d = threadIdx.x;
+  const size_t stride = (size_t)p.M * p.Hq;
+  float M = -INFINITY;
+  for (int z = 0; z < p.n_split; ++z) M = fmaxf(M, p.ml_part[(z * stride + rid) * 2]);
+  float L = 0.f, O = 0.f;
+  for (int z = 0; z < p.n_split; ++z) {
+    const float mz = p.ml_part[(z * stride + rid) * 2], lz = p.ml_part[(z * stride + rid) * 2 + 1];
+    if (lz == 0.f || mz == -INFINITY) continue;
+    const float f = __expf(mz - M);
+    L += lz * f;
+    O += p.o_part[(z * stride + rid) * DP + d] * f;
+  }
+  if (d < p.hd) p.out[(size_t)t * p.ldo + h * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+void launch_attention(const AttnParams& p, hipStream_t st) {
+  const int ng = (p.M + p.tq - 1) / p.tq;
+  dim3 grid(ng, p.Hkv, p.n_split);
+  if (p.Dp == 128) {
+    hipLaunchKernelGGL(mpk::attn_kernel<128>, grid, dim3(256), 0, st, p);
+    if (p.n_split > 1) hipLaunchKernelGGL(mpk::attn_combine_kernel<128>, dim3(p.M * p.Hq), dim3(128), 0, st, p);
+  } else {
+    hipLaunchKernelGGL(mpk::attn_kernel<64>, grid, dim3(256), 0, st, p);
+    if (p.n_split > 1) hipLaunchKernelGGL(mpk::attn_combine_kernel<64>, dim3(p.M * p.Hq), dim3(64), 0, st, p);
+  }
+}
+
+}  // namespace mp

@@ -1,0 +1,237 @@
+// Memory-bound row kernels: RMSNorm (K2), embedding gather+dequant (K1), RoPE + paged KV append
+// (K5+K6 fused), argmax (K12 greedy), decode-step advance, SwiGLU (K8, unfused fallback).
+// All loads/stores of bf16/f16/f32 rows are vectorised (guide Guideline 13).
+#include "kcommon.h"
+#include "../runtime/kernels_api.h"
+#include "../runtime/qtypes.h"
+
+namespace mpk {
+using namespace mp;
+
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
+                                                      float eps, f16* out, int ldo, float* zero,
+                                                      int64_t zero_n, int M) {
+  __shared__ float red[4];
+  const int row = blockIdx.x;
+  const float* xr = x + (size_t)row * ldx;
+  float ss = 0.f;
+  const int d4 = d & ~3;
+  for (int i = threadIdx.x * 4; i < d4; i += 1024) {
+    float4 v = *reinterpret_cast<const float4*>(xr + i);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (int i = d4 + threadIdx.x; i < d; i += 256) ss += xr[i] * xr[i];
+  ss = block_sum_256(ss, red);
+  const float sc = rsqrtf(ss / (float)d + eps);
+  f16* o = out + (size_t)row * ldo;
+  for (int i = threadIdx.x * 4; i < d4; i += 1024) {
+    float4 v = *reinterpret_cast<const float4*>(xr + i);
+    float4 ww = *reinterpret_cast<const float4*>(w + i);
+    half2_t a = {(f16)(v.x * sc * ww.x), (f16)(v.y * sc * ww.y)};
+    half2_t b = {(f16)(v.z * sc * ww.z), (f16)(v.w * sc * ww.w)};
+    u32x2 pk = {as_u32(a), as_u32(b)};
+    *reinterpret_cast<u32x2*>(o + i) = pk;
+  }
+  for (int i = d4 + threadIdx.x; i < d; i += 256) o[i] = (f16)(xr[i] * sc * w[i]);
+  if (zero) {
+    const int64_t per = (zero_n + M - 1) / M;
+    const int64_t z0 = (int64_t)row * per, z1 = min(zero_n, z0 + per);
+    for (int64_t i = z0 + threadIdx.x; i < z1; i += 256) zero[i] = 0.f;
+  }
+}
+
+// ---------------------------------------------------------------- embedding (raw GGUF rows)
+__device__ float deq_elem(int t, const uint8_t* row, int e) {
+  switch (t) {
+    case T_F32: return reinterpret_cast<const float*>(row)[e];
+    case T_F16: return h2f(reinterpret_cast<const uint16_t*>(row)[e]);
+    case T_BF16: return bf16_to_f32(reinterpret_cast<const uint16_t*>(row)[e]);
+    case T_Q8_0: {
+      const uint8_t* b = row + (e / 32) * 34;
+      return h2f(*reinterpret_cast<const uint16_t*>(b)) * (float)(int8_t)b[2 + e % 32];
+    }
+    case T_Q4_0: {
+      const uint8_t* b = row + (e / 32) * 18;
+      const int l = e % 32;
+      const int q = l < 16 ? (b[2 + l] & 15) : (b[2 + l - 16] >> 4);
+      return h2f(*reinterpret_cast<const uint16_t*>(b)) * (float)(q - 8);
+    }
+    case T_Q4_K: case T_Q5_K: {
+      const int bb = t == T_Q4_K ? 144 : 176;
+      const uint8_t* b = row + (e / 256) * bb;
+      const int w = e % 256, c = w / 64, l = w % 64;
+      const float d = h2f(*reinterpret_cast<const uint16_t*>(b));
+      const float dmin = h2f(*reinterpret_cast<const uint16_t*>(b + 2));
+      int sc, m;
+      scale_min_k4(2 * c + (l >= 32), b + 4, sc, m);
+      const uint8_t* qs = b + (t == T_Q4_K ? 16 : 48);
+      int q = l < 32 ? (qs[32 * c + l] & 15) : (qs[32 * c + l - 32] >> 4);
+      if (t == T_Q5_K) q += ((b[16 + (l & 31)] >> (2 * c + (l >= 32))) & 1) << 4;
+      return d * sc * q - dmin * m;
+    }
+    case T_Q6_K: {
+      const uint8_t* b = row + (e / 256) * 210;
+      const int w = e % 256, n = w / 128, r = w % 128, k = r / 32, l = r % 32;
+      const uint8_t* ql = b + 64 * n;
+      const uint8_t* qh = b + 128 + 32 * n;
+      const int8_t* sc = reinterpret_cast<const int8_t*>(b + 192) + 8 * n;
+      const int lo = (k == 0) ? (ql[l] & 15) : (k == 1) ? (ql[l + 32] & 15) : (k == 2) ? (ql[l] >> 4) : (ql[l + 32] >> 4);
+      const int hi = (qh[l] >> (2 * k)) & 3;
+      const float d = h2f(*reinterpret_cast<const uint16_t*>(b + 208));
+      return d * sc[l / 16 + 2 * k] * (float)((lo | (hi << 4)) - 32);
+    }
+  }
+  return 0.f;
+}
+
+__global__ __launch_bounds__(256) void embed_kernel(int t, const uint8_t* table, int64_t rb, int d,
+                                                    const int32_t* tokens, float* x, int ldx) {
+  const int m = blockIdx.x;
+  const uint8_t* row = table + (int64_t)tokens[m] * rb;
+  for (int e = threadIdx.x; e < d; e += 256) x[(size_t)m * ldx + e] = deq_elem(t, row, e);
+}
+
+// ---------------------------------------------------------------- RoPE (NORM, adjacent pairs) + KV append
+__global__ __launch_bounds__(256) void rope_kv_kernel(const RopeKvParams p) {
+  const int m = blockIdx.x;
+  const int pos = p.pos[m];
+  const int slot = p.slot[m];
+  const int hd2 = p.hd / 2, Dp2 = p.Dp / 2;
+  const float* row = p.qkv + (size_t)m * p.ldqkv;
+  const float2* cs = p.rope_cs + (size_t)pos * hd2;
+  // q: Hq heads
+  for (int i = threadIdx.x; i < p.Hq * Dp2; i += 256) {
+    const int h = i / Dp2, j = i % Dp2;
+    half2_t o = {(f16)0.f, (f16)0.f};
+    if (j < hd2) {
+      const float x0 = row[h * p.hd + 2 * j], x1 = row[h * p.hd + 2 * j + 1];
+      const float2 c = cs[j];
+      o = half2_t{(f16)((x0 * c.x - x1 * c.y) * p.q_scale), (f16)((x0 * c.y + x1 * c.x) * p.q_scale)};
+    }
+    *reinterpret_cast<half2_t*>(p.q_out + ((size_t)m * p.Hq + h) * p.Dp + 2 * j) = o;
+  }
+  const int page = p.block_table[(size_t)slot * p.max_pages + pos / 64];
+  const int idx = pos % 64;
+  const float* kr = row + p.Hq * p.hd;
+  const float* vr = kr + p.Hkv * p.hd;
+  for (int i = threadIdx.x; i < p.Hkv * Dp2; i += 256) {
+    const int h = i / Dp2, j = i % Dp2;
+    half2_t o = {(f16)0.f, (f16)0.f};
+    if (j < hd2) {
+      const float x0 = kr[h * p.hd + 2 * j], x1 = kr[h * p.hd + 2 * j + 1];
+      const float2 c = cs[j];
+      o = half2_t{(f16)(x0 * c.x - x1 * c.y), (f16)(x0 * c.y + x1 * c.x)};
+    }
+    *reinterpret_cast<half2_t*>(p.k_cache + (((size_t)page * p.Hkv + h) * 64 + idx) * p.Dp + 2 * j) = o;
+  }
+  for (int i = threadIdx.x; i < p.Hkv * p.Dp; i += 256) {
+    const int h = i / p.Dp, dd = i % p.Dp;
+    const float v = dd < p.hd ? vr[h * p.hd + dd] : 0.f;
+    p.v_cache[(((size_t)page * p.Hkv + h) * p.Dp + dd) * 64 + idx] = (f16)v;
+  }
+}
+
+// ---------------------------------------------------------------- argmax
+__global__ __launch_bounds__(1024) void argmax_kernel(const float* logits, int ld, int n, int32_t* tok) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const float* r = logits + (size_t)blockIdx.x * ld;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const float v = r[i];
+    if (v > bv) { bv = v; bi = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i)
+      if (sv[i] > bv || (sv[i] == bv && si[i] < bi)) { bv = sv[i]; bi = si[i]; }
+    tok[blockIdx.x] = bi;
+  }
+}
+
+__global__ void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
+  const int i = threadIdx.x;
+  if (i < M) { const int p = pos[i] + 1; pos[i] = p; kvlen[i] = p + 1; }
+  if (i == 0 && step) step[0] += 1;
+}
+
+__global__ __launch_bounds__(256) void swiglu_kernel(const float* gu, int ld, int F, f16* h, int ldh) {
+  const int m = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < F) {
+    const float g = gu[(size_t)m * ld + j], u = gu[(size_t)m * ld + F + j];
+    h[(size_t)m * ldh + j] = (f16)(silu(g) * u);
+  }
+}
+
+__global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* x, int ldx, int n, f16* y, int ldy) {
+  const int m = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < n) y[(size_t)m * ldy + j] = (f16)x[(size_t)m * ldx + j];
+}
+
+__global__ void prefill_meta_kernel(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, int T, int s) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < T) { pos[i] = p0 + i; kvlen[i] = p0 + i + 1; slot[i] = s; }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+void launch_prefill_meta(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, int T, int s, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::prefill_meta_kernel, dim3((T + 255) / 256), dim3(256), 0, st, pos, kvlen, slot, p0, T, s);
+}
+
+void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
+                    float* zero, int64_t zero_n, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M), dim3(256), 0, st, x, ldx, w, d, eps, out, ldo, zero, zero_n, M);
+}
+
+void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,
+                  int ldx, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::embed_kernel, dim3(M), dim3(256), 0, st, t, table, rb, d, tokens, x, ldx);
+}
+
+void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::rope_kv_kernel, dim3(p.M), dim3(256), 0, st, p);
+}
+
+void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::argmax_kernel, dim3(M), dim3(1024), 0, st, logits, ld, n, tokens);
+}
+
+void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::advance_kernel, dim3(1), dim3(64), 0, st, pos, kvlen, M, step);
+}
+
+void launch_swiglu(const float* gu, int ld, int F, int M, f16* h, int ldh, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::swiglu_kernel, dim3((F + 255) / 256, M), dim3(256), 0, st, gu, ld, F, h, ldh);
+}
+
+void launch_f32_to_f16(const float* x, int ldx, int n, int M, f16* y, int ldy, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::f32_to_f16_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, x, ldx, n, y, ldy);
+}
+
+}  // namespace mp

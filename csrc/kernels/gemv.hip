@@ -1,0 +1,149 @@
+// Skinny dequant-GEMM for decode micro-batches (M <= 16 rows of activations).
+//
+//   Y[m][n] (+)= sum_k X[m][k] * W[n][k]      X: f16 [M][ldx], W: T16-packed quantized weights
+//
+// One wavefront owns one 16-row tile of W and a contiguous range of 256-k super-blocks; four
+// waves per workgroup own four adjacent tiles.  Each lane streams its share of the packed tile
+// with 16-B non-temporal loads (double-buffered in registers), dequantizes to f16 in registers
+// (dequant.h) and feeds v_mfma_f32_16x16x32_f16 with A = X (rows m), B = W^T (cols n).  The MFMA
+// is ~14 % busy at HBM speed: the kernel is weight-bandwidth bound for any M <= 16, so a decode
+// micro-batch of 16 sequences costs about the same as one.
+// Split-K over super-blocks (grid.y) with f32 atomics into the destination gives >= 2k waves on
+// the 256 CUs for every Llama shape; residual adds (Wo, Wdown) atomically accumulate straight
+// into the f32 residual stream, and the gate/up projection is packed interleaved (rows 0-7 gate,
+// 8-15 up of the same 8 outputs) so SwiGLU is fused in the epilogue (K8/K9 fusion).
+#include "kcommon.h"
+#include "dequant.h"
+#include "../runtime/kernels_api.h"
+
+namespace mpk {
+
+template <int PT, int EPI>
+__global__ __launch_bounds__(256) void gemv_kernel(const mp::GemvParams p) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= p.ntiles) return;
+  const int sb0 = blockIdx.y * p.sb_per_split;
+  const int sb1 = min(sb0 + p.sb_per_split, p.nsb);
+  if (sb0 >= sb1) return;
+  const int g = lane >> 4, r = lane & 15;
+  const uint8_t* wp = p.W + ((size_t)tile * p.nsb + sb0) * CB;
+  const bool xv = r < p.M;
+  const f16* xp = p.X + (size_t)(xv ? r : 0) * p.ldx + 8 * g;
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  typename D::Raw cur, nxt;
+  D::load(cur, wp, lane);
+  for (int sb = sb0; sb < sb1; ++sb) {
+    if (sb + 1 < sb1) D::load(nxt, wp + CB, lane);
+    half8_t a[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      half8_t z = {};
+      a[t] = xv ? *reinterpret_cast<const half8_t*>(xp + (size_t)sb * 256 + 32 * t) : z;
+    }
+    half8_t b[4];
+    D::template dequant<0>(cur, b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[s], b[s], acc);
+    D::template dequant<1>(cur, b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[4 + s], b[s], acc);
+    cur = nxt;
+    wp += CB;
+  }
+
+  // lane holds C[m = 4g + i][n = 16*tile + r]
+  if constexpr (EPI == mp::EPI_SWIGLU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float other = __shfl_xor(acc[i], 8);
+      const int m = 4 * g + i;
+      if (r < 8 && m < p.M) {
+        const int o = tile * 8 + r;
+        if (o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[i]) * other);
+      }
+    }
+  } else {
+    const int n = tile * 16 + r;
+    if (n < p.n_valid) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 4 * g + i;
+        if (m < p.M) {
+          float* dst = p.Y + (size_t)m * p.ldy + n;
+          if constexpr (EPI == mp::EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i]);
+          else *dst = acc[i];
+        }
+      }
+    }
+  }
+}
+
+// Dense dequantization of a T16-packed matrix back to f16 [N_pad][K_pad] (tests, prefill staging).
+template <int PT>
+__global__ __launch_bounds__(64) void unpack_kernel(const uint8_t* W, int nsb, f16* out, int ldo) {
+  using D = Deq<PT>;
+  const int lane = threadIdx.x;
+  const int tile = blockIdx.x, sb = blockIdx.y;
+  const uint8_t* c = W + ((size_t)tile * nsb + sb) * D::CB;
+  typename D::Raw raw;
+  D::load(raw, c, lane);
+  half8_t b[4];
+  const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 0) D::template dequant<0>(raw, b, lane);
+    else D::template dequant<1>(raw, b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      f16* o = out + (size_t)(tile * 16 + r) * ldo + sb * 256 + 128 * h + 32 * s + 8 * g;
+      *reinterpret_cast<half8_t*>(o) = b[s];
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+template <int PT>
+static void launch_pt(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  dim3 grid((p.ntiles + 3) / 4, nsplit);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE>), grid, dim3(256), 0, st, p); break;
+    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC>), grid, dim3(256), 0, st, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU>), grid, dim3(256), 0, st, p); break;
+  }
+}
+
+void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
+  if (nsplit < 1) nsplit = 1;
+  p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
+  nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
+  switch (ptype) {
+    case P_Q4_K: launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
+    case P_Q5_K: launch_pt<P_Q5_K>(epi, p, nsplit, st); break;
+    case P_Q6_K: launch_pt<P_Q6_K>(epi, p, nsplit, st); break;
+    case P_Q8_0: launch_pt<P_Q8_0>(epi, p, nsplit, st); break;
+    case P_Q4_0: launch_pt<P_Q4_0>(epi, p, nsplit, st); break;
+    case P_F16: launch_pt<P_F16>(epi, p, nsplit, st); break;
+  }
+}
+
+void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, int ldo, hipStream_t st) {
+  dim3 grid(ntiles, nsb);
+  switch (ptype) {
+    case P_Q4_K: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q4_K>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_Q5_K: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q5_K>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_Q6_K: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q6_K>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_Q8_0: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q8_0>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_Q4_0: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q4_0>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_F16: hipLaunchKernelGGL(mpk::unpack_kernel<P_F16>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+  }
+}
+
+}  // namespace mp

@@ -1,0 +1,333 @@
+// C ABI of libmipipe.so (consumed by the python package through ctypes and by the C++ tools).
+// Every entry point catches exceptions, records the message (mp_last_error) and returns an
+// error code / nullptr.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "engine.h"
+#include "gguf.h"
+#include "hip_stage.h"
+#include "json.h"
+#include "kernels_api.h"
+#include "log.h"
+#include "pack.h"
+
+using namespace mp;
+
+static thread_local std::string g_err;
+static thread_local std::string g_str;
+
+#define API_TRY try {
+#define API_CATCH(ret)                 \
+  }                                    \
+  catch (const std::exception& e) {    \
+    g_err = e.what();                  \
+    return ret;                        \
+  }
+
+extern "C" {
+
+const char* mp_last_error() { return g_err.c_str(); }
+int mp_version() { return 1; }
+void mp_log_level(int lvl) { log_set_level(lvl); }
+void mp_log_file(const char* path) { log_set_file(path ? path : ""); }
+
+// ------------------------------------------------------------------ host utilities
+int64_t mp_packed_bytes(int type, int64_t N, int64_t K) {
+  const int pt = pack_type_of(type);
+  if (pt < 0) return -1;
+  return (int64_t)packed_dims(pt, N, K).bytes;
+}
+int mp_pack_type(int type) { return pack_type_of(type); }
+
+int mp_pack_t16(int type, int64_t N, int64_t K, const uint8_t* src, int64_t src_row_bytes, uint8_t* dst,
+                int gateup_interleave) {
+  API_TRY
+  if (gateup_interleave) {
+    // src holds gate rows [0, N/2) then up rows [N/2, N)
+    const int64_t F = N / 2;
+    pack_t16(type, N, K, [&](int64_t n) -> const uint8_t* {
+      bool up;
+      const int64_t r = gateup_src_row(n, &up);
+      if (r >= F) return nullptr;
+      return src + (up ? F + r : r) * src_row_bytes;
+    }, dst);
+  } else {
+    pack_t16(type, N, K, [&](int64_t n) -> const uint8_t* { return src + n * src_row_bytes; }, dst);
+  }
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_dequant_row(int type, const uint8_t* src, float* dst, int64_t K) {
+  API_TRY
+  dequant_row(type, src, dst, K);
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_partition(const double* cost, int L, double first_extra, double last_extra, const double* speed, int S,
+                 int mode, int32_t* out_ranges) {
+  API_TRY
+  std::vector<double> c(cost, cost + L), sp(speed, speed + S);
+  auto r = partition_layers(c, first_extra, last_extra, sp, (SplitMode)mode);
+  for (int s = 0; s < S; ++s) { out_ranges[2 * s] = r[s].layer_begin; out_ranges[2 * s + 1] = r[s].layer_end; }
+  return 0;
+  API_CATCH(-1)
+}
+
+// ------------------------------------------------------------------ GGUF
+void* mp_gguf_open(const char* path) {
+  API_TRY
+  return new GgufFile(path);
+  API_CATCH(nullptr)
+}
+void mp_gguf_close(void* h) { delete static_cast<GgufFile*>(h); }
+
+const char* mp_gguf_json(void* h) {
+  API_TRY
+  auto* f = static_cast<GgufFile*>(h);
+  Json j = Json::object();
+  j["version"] = (int)f->version();
+  Json kv = Json::object();
+  for (auto& it : f->kv()) {
+    const GgufValue& v = it.second;
+    if (v.type == GV_STRING) kv[it.first] = Json(v.s);
+    else if (v.type == GV_ARRAY) {
+      Json a = Json::object();
+      a["array_len"] = (int64_t)(v.elem_type == GV_STRING ? v.strs.size() : v.nums.size());
+      a["elem_type"] = (int)v.elem_type;
+      kv[it.first] = a;
+    } else if (v.type == GV_F32 || v.type == GV_F64) kv[it.first] = Json(v.f);
+    else kv[it.first] = Json((int64_t)v.i);
+  }
+  j["kv"] = kv;
+  Json ts = Json::array();
+  for (auto& t : f->tensors()) {
+    Json o = Json::object();
+    o["name"] = t.name;
+    Json ne = Json::array();
+    for (auto x : t.ne) ne.push(Json((int64_t)x));
+    o["ne"] = ne;
+    o["type"] = t.type;
+    o["offset"] = (int64_t)t.offset;
+    o["nbytes"] = (int64_t)t.nbytes;
+    ts.push(o);
+  }
+  j["tensors"] = ts;
+  g_str = j.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+
+const char* mp_model_config_json(const char* gguf_path) {
+  API_TRY
+  GgufFile f(gguf_path);
+  ModelConfig c = ModelConfig::from_gguf(f);
+  Json j = Json::object();
+  j["n_layer"] = c.n_layer; j["d_model"] = c.d_model; j["n_head"] = c.n_head; j["n_head_kv"] = c.n_head_kv;
+  j["head_dim"] = c.head_dim; j["d_ff"] = c.d_ff; j["vocab"] = c.vocab; j["rope_base"] = (double)c.rope_base;
+  j["eps"] = (double)c.eps; j["n_expert"] = c.n_expert; j["n_expert_used"] = c.n_expert_used;
+  j["rope_freqs"] = c.rope_freqs; j["tied_output"] = c.tied_output;
+  g_str = j.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+
+// ------------------------------------------------------------------ kernel ops (tests)
+int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+               int ldy, void* H, int ldh, int n_valid, int nsplit, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  if (M > 16) {
+    for (int r0 = 0; r0 < M; r0 += 16) {
+      GemvParams q = p;
+      q.M = std::min(16, M - r0);
+      q.X = p.X + (size_t)r0 * ldx;
+      if (q.Y) q.Y = p.Y + (size_t)r0 * ldy;
+      if (q.H) q.H = p.H + (size_t)r0 * ldh;
+      launch_gemv(ptype, epi, q, nsplit, (hipStream_t)stream);
+    }
+  } else {
+    launch_gemv(ptype, epi, p, nsplit, (hipStream_t)stream);
+  }
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_unpack(int ptype, const void* W, int ntiles, int nsb, void* out, int ldo, void* stream) {
+  API_TRY
+  launch_unpack(ptype, (const uint8_t*)W, ntiles, nsb, (f16*)out, ldo, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_rmsnorm(const void* x, int ldx, const void* w, int d, float eps, void* out, int ldo, int M, void* stream) {
+  API_TRY
+  launch_rmsnorm((const float*)x, ldx, (const float*)w, d, eps, (f16*)out, ldo, M, nullptr, 0, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_embed(int type, const void* table, int64_t row_bytes, int d, const void* tokens, int M, void* x, int ldx,
+                void* stream) {
+  API_TRY
+  launch_embed(type, (const uint8_t*)table, row_bytes, d, (const int32_t*)tokens, M, (float*)x, ldx,
+               (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_rope_kv(const void* qkv, int ldqkv, int M, int Hq, int Hkv, int hd, int Dp, const void* pos,
+                  const void* slot, const void* block_table, int max_pages, const void* rope_cs, float q_scale,
+                  void* q_out, void* k_cache, void* v_cache, void* stream) {
+  API_TRY
+  RopeKvParams p{};
+  p.qkv = (const float*)qkv; p.ldqkv = ldqkv; p.M = M; p.Hq = Hq; p.Hkv = Hkv; p.hd = hd; p.Dp = Dp;
+  p.pos = (const int32_t*)pos; p.slot = (const int32_t*)slot; p.block_table = (const int32_t*)block_table;
+  p.max_pages = max_pages; p.rope_cs = (const float2*)rope_cs; p.q_scale = q_scale; p.q_out = (f16*)q_out;
+  p.k_cache = (f16*)k_cache; p.v_cache = (f16*)v_cache;
+  launch_rope_kv(p, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_attention(const void* q, const void* kvlen, const void* slot, const void* block_table, int max_pages,
+                    const void* k_cache, const void* v_cache, int M, int Hq, int Hkv, int hd, int Dp, int tq,
+                    int split_len, int n_split, void* o_part, void* ml_part, void* out, int ldo, void* stream) {
+  API_TRY
+  AttnParams p{};
+  p.q = (const f16*)q; p.kvlen = (const int32_t*)kvlen; p.slot = (const int32_t*)slot;
+  p.block_table = (const int32_t*)block_table; p.max_pages = max_pages; p.k_cache = (const f16*)k_cache;
+  p.v_cache = (const f16*)v_cache; p.M = M; p.Hq = Hq; p.Hkv = Hkv; p.hd = hd; p.Dp = Dp; p.tq = tq;
+  p.split_len = split_len; p.n_split = n_split; p.o_part = (float*)o_part; p.ml_part = (float*)ml_part;
+  p.out = (f16*)out; p.ldo = ldo;
+  launch_attention(p, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_argmax(const void* logits, int ld, int n, int M, void* tokens, void* stream) {
+  API_TRY
+  launch_argmax((const float*)logits, ld, n, M, (int32_t*)tokens, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_sample(const void* logits, int ld, int n, int M, float temp, int top_k, float top_p, float min_p,
+                 uint64_t seed, const void* step, void* tokens, void* stream) {
+  API_TRY
+  SampleParams p{};
+  p.logits = (const float*)logits; p.ld = ld; p.n = n; p.M = M; p.temp = temp; p.top_k = top_k; p.top_p = top_p;
+  p.min_p = min_p; p.seed = seed; p.step = (const int32_t*)step; p.tokens = (int32_t*)tokens;
+  launch_sample(p, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+// ------------------------------------------------------------------ engine
+void* mp_engine_create(const char* json_cfg) {
+  API_TRY
+  return new Engine(Json::parse(json_cfg));
+  API_CATCH(nullptr)
+}
+void mp_engine_destroy(void* h) {
+  try { delete static_cast<Engine*>(h); } catch (...) {}
+}
+const char* mp_engine_info(void* h) {
+  API_TRY
+  g_str = static_cast<Engine*>(h)->info().dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+// Generate for a batch of prompts. prompts: concatenated token ids, lens[n]. out: [n][n_predict]
+// returns JSON stats string
+const char* mp_engine_generate(void* h, const int32_t* prompt_tokens, const int32_t* lens, int n_seq, int n_predict,
+                               int32_t* out_tokens) {
+  API_TRY
+  std::vector<std::vector<int32_t>> prompts;
+  size_t off = 0;
+  for (int i = 0; i < n_seq; ++i) {
+    prompts.emplace_back(prompt_tokens + off, prompt_tokens + off + lens[i]);
+    off += lens[i];
+  }
+  std::vector<std::vector<int32_t>> outs;
+  Json stats = static_cast<Engine*>(h)->generate(prompts, n_predict, &outs);
+  for (int i = 0; i < n_seq; ++i)
+    for (int j = 0; j < n_predict; ++j) out_tokens[(size_t)i * n_predict + j] = j < (int)outs[i].size() ? outs[i][j] : -1;
+  g_str = stats.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+// Benchmark decode loop: n_warmup + n_steps decode steps of every micro-batch after a prefill of
+// prompt_len synthetic tokens. Returns JSON stats.
+const char* mp_engine_bench(void* h, int prompt_len, int n_warmup, int n_steps) {
+  API_TRY
+  g_str = static_cast<Engine*>(h)->bench(prompt_len, n_warmup, n_steps).dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+// fine-grained control (bench.py drives the timed region itself)
+int mp_engine_start(void* h, const int32_t* prompt_tokens, const int32_t* lens, int n_seq) {
+  API_TRY
+  std::vector<std::vector<int32_t>> prompts;
+  size_t off = 0;
+  for (int i = 0; i < n_seq; ++i) {
+    prompts.emplace_back(prompt_tokens + off, prompt_tokens + off + lens[i]);
+    off += lens[i];
+  }
+  static_cast<Engine*>(h)->start(prompts);
+  return 0;
+  API_CATCH(-1)
+}
+const char* mp_engine_decode(void* h, int k) {
+  API_TRY
+  StepStats ss = static_cast<Engine*>(h)->decode_steps(k);
+  Json j = Json::object();
+  j["wall_ms"] = ss.wall_ms;
+  Json a = Json::array();
+  for (double v : ss.token_ms) a.push(Json(v));
+  j["token_ms"] = a;
+  g_str = j.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+// copy generated tokens: out[n_seq][cap]; returns tokens per sequence (min over sequences)
+int mp_engine_tokens(void* h, int32_t* out, int n_seq, int cap) {
+  API_TRY
+  auto t = static_cast<Engine*>(h)->tokens();
+  int n = cap;
+  for (int i = 0; i < n_seq && i < (int)t.size(); ++i) {
+    n = std::min<int>(n, (int)t[i].size());
+    for (int j = 0; j < cap; ++j) out[(size_t)i * cap + j] = j < (int)t[i].size() ? t[i][j] : -1;
+  }
+  return n;
+  API_CATCH(-1)
+}
+// debug: logits of the last decode/prefill of a micro-batch (last stage, rank-local)
+int mp_engine_logits(void* h, int mb, float* out, int rows) {
+  API_TRY
+  return static_cast<Engine*>(h)->copy_logits(mb, out, rows);
+  API_CATCH(-1)
+}
+// multi-process rendezvous helpers: unique id bytes for RCCL
+int mp_rccl_unique_id(uint8_t* out128) {
+  API_TRY
+  return rccl_unique_id(out128);
+  API_CATCH(-1)
+}
+
+}  // extern "C"

@@ -1,0 +1,530 @@
+#include "engine.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <exception>
+#include <numeric>
+#include <stdexcept>
+
+#include "gguf.h"
+#include "log.h"
+#include "qtypes.h"
+
+namespace mp {
+
+namespace {
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+ModelConfig config_from_json(const Json& j) {
+  ModelConfig c;
+  c.name = j.get_str("name", "synthetic");
+  c.n_layer = j.get_int("n_layer", 0);
+  c.d_model = j.get_int("d_model", 0);
+  c.n_head = j.get_int("n_head", 0);
+  c.n_head_kv = j.get_int("n_head_kv", c.n_head);
+  c.d_ff = j.get_int("d_ff", 0);
+  c.vocab = j.get_int("vocab", 32000);
+  c.head_dim = j.get_int("head_dim", c.n_head ? c.d_model / c.n_head : 0);
+  c.rope_base = (float)j.get_num("rope_base", 10000.0);
+  c.eps = (float)j.get_num("eps", 1e-5);
+  c.n_expert = j.get_int("n_expert", 0);
+  c.n_expert_used = j.get_int("n_expert_used", 0);
+  c.n_ctx_train = j.get_int("n_ctx_train", 2048);
+  if (!c.n_layer || !c.d_model || !c.n_head || !c.d_ff) throw std::runtime_error("synthetic config incomplete");
+  return c;
+}
+
+std::vector<uint8_t> unhex(const std::string& s) {
+  std::vector<uint8_t> o(s.size() / 2);
+  for (size_t i = 0; i < o.size(); ++i) o[i] = (uint8_t)std::stoi(s.substr(2 * i, 2), nullptr, 16);
+  return o;
+}
+
+double pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  const double idx = p * (v.size() - 1);
+  const size_t i = (size_t)idx;
+  const double f = idx - i;
+  return i + 1 < v.size() ? v[i] * (1 - f) + v[i + 1] * f : v[i];
+}
+
+// decode-step bytes of one layer / the head (partition cost model: decode is HBM-bound)
+double synth_layer_bytes(const ModelConfig& c, const std::string& ftype, int li) {
+  const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, li, c.n_layer);
+  auto b = [](int ty, double n, double k) { return n * k * block_bytes(ty) / block_elems(ty); };
+  const double d = c.d_model, q = c.q_dim(), kv = c.kv_dim(), f = c.d_ff;
+  return b(t.q, q, d) + b(t.k, kv, d) + b(t.v, kv, d) + b(t.o, d, q) + b(t.gate, f, d) + b(t.up, f, d) +
+         b(t.down, d, f);
+}
+
+}  // namespace
+
+Engine::Engine(const Json& j) : jcfg_(j) {
+  const double t0 = now_ms();
+  if (j.get_bool("verbose", false)) log_set_level(LOG_DEBUG);
+  if (j.has("log_file")) log_set_file(j.get_str("log_file", ""));
+  mode_ = j.get_str("mode", "local");
+  M_ = std::max(1, j.get_int("n_mb", 1));
+  B_ = std::max(1, j.get_int("mb_size", 1));
+  if (B_ > 16) throw std::runtime_error("mb_size > 16 not supported (decode micro-batch is one MFMA row tile)");
+  max_ctx_ = (int)round_up(std::max(64, j.get_int("max_ctx", 2048)), 64);
+  chunk_ = std::max(16, j.get_int("prefill_chunk", 256));
+  const std::string ftype = j.get_str("ftype", "Q4_K_M");
+  const uint64_t seed = (uint64_t)j.get_num("seed", 1234);
+
+  std::vector<double> layer_cost;
+  double head_cost = 0, embd_cost = 0;
+  if (j.has("gguf")) {
+    gguf_.reset(new GgufFile(j.get_str("gguf", "")));
+    cfg_ = ModelConfig::from_gguf(*gguf_);
+    for (int li = 0; li < cfg_.n_layer; ++li) {
+      double bytes = 0;
+      const std::string p = "blk." + std::to_string(li) + ".";
+      for (auto& t : gguf_->tensors())
+        if (t.name.compare(0, p.size(), p) == 0) bytes += (double)t.nbytes;
+      layer_cost.push_back(bytes);
+    }
+    const GgufTensor* out = gguf_->tensor("output.weight");
+    head_cost = (double)(out ? out->nbytes : gguf_->tensor("token_embd.weight")->nbytes);
+  } else if (j.has("synthetic")) {
+    cfg_ = config_from_json(j["synthetic"]);
+    for (int li = 0; li < cfg_.n_layer; ++li) layer_cost.push_back(synth_layer_bytes(cfg_, ftype, li));
+    const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, 0, cfg_.n_layer);
+    head_cost = (double)cfg_.vocab * cfg_.d_model * block_bytes(t.out) / block_elems(t.out);
+  } else {
+    throw std::runtime_error("engine config needs 'gguf' or 'synthetic'");
+  }
+  MP_LOGI("model: %s", cfg_.describe().c_str());
+
+  // ---- partition
+  if (mode_ == "mp") {
+    S_ = j.get_int("world", 1);
+    rank_ = j.get_int("rank", 0);
+  } else {
+    S_ = std::max(1, j.get_int("stages", 1));
+  }
+  std::vector<double> speed(S_, 1.0);
+  if (j.has("device_speed"))
+    for (int s = 0; s < S_ && s < (int)j["device_speed"].arr().size(); ++s) speed[s] = j["device_speed"].arr()[s].num();
+  specs_ = partition_layers(layer_cost, embd_cost, head_cost, speed, parse_split_mode(j.get_str("split", "cost")));
+  std::vector<int> devices(S_);
+  for (int s = 0; s < S_; ++s) devices[s] = s;
+  if (j.has("devices")) {
+    auto& a = j["devices"].arr();
+    for (int s = 0; s < S_; ++s) devices[s] = (int)a[s % a.size()].num();
+  }
+  if (mode_ == "mp") devices[rank_] = j.get_int("device", devices[rank_]);
+  for (int s = 0; s < S_; ++s) specs_[s].device = devices[s];
+  for (auto& sp : specs_)
+    MP_LOGI("partition: stage %d <- layers [%d, %d) (%d layers)%s%s", sp.stage, sp.layer_begin, sp.layer_end,
+            sp.layer_end - sp.layer_begin, sp.first() ? " +embd" : "", sp.last() ? " +head" : "");
+
+  StageOptions so;
+  so.n_mb = M_;
+  so.mb_size = B_;
+  so.max_ctx = max_ctx_;
+  so.prefill_chunk = chunk_;
+  so.use_graphs = j.get_bool("graphs", true);
+  so.attn_split_len = j.get_int("attn_split_len", 256);
+
+  // ---- stages this process owns
+  for (int s = 0; s < S_; ++s) {
+    if (mode_ == "mp" && s != rank_) continue;
+    auto w = std::make_unique<Worker>();
+    w->device = specs_[s].device;
+    HIP_OK(hipSetDevice(w->device));
+    w->stage.reset(new HipStage(cfg_, specs_[s], so));
+    if (gguf_) w->stage->load_gguf(*gguf_);
+    else w->stage->init_synthetic(ftype, seed);
+    w->stage->alloc_runtime();
+    HIP_OK(hipStreamCreateWithFlags(&w->send_st, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&w->recv_st, hipStreamNonBlocking));
+    w->comp_ev.resize(M_); w->sent_ev.resize(M_); w->recv_ev.resize(M_);
+    w->sent_valid.assign(M_, false);
+    for (int mb = 0; mb < M_; ++mb) {
+      HIP_OK(hipEventCreateWithFlags(&w->comp_ev[mb], hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&w->sent_ev[mb], hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&w->recv_ev[mb], hipEventDisableTiming));
+    }
+    workers_.push_back(std::move(w));
+  }
+  build_links(j);
+  for (auto& w : workers_) {
+    HIP_OK(hipSetDevice(w->device));
+    w->stage->capture_graphs();
+  }
+  rounds_cap_ = max_ctx_ + 2;
+  HIP_OK(hipHostMalloc((void**)&out_host_, (size_t)rounds_cap_ * M_ * B_ * 4, hipHostMallocDefault));
+  std::memset(out_host_, 0xff, (size_t)rounds_cap_ * M_ * B_ * 4);
+  load_ms_ = now_ms() - t0;
+  MP_LOGI("engine ready: %d stage(s), %d micro-batch(es) x %d seq, ctx %d, load %.1f ms", S_, M_, B_, max_ctx_,
+          load_ms_);
+}
+
+Engine::~Engine() {
+  try {
+    sync_all();
+  } catch (...) {
+  }
+  for (auto& w : workers_) {
+    (void)hipSetDevice(w->device);
+    for (auto e : w->comp_ev) (void)hipEventDestroy(e);
+    for (auto e : w->sent_ev) (void)hipEventDestroy(e);
+    for (auto e : w->recv_ev) (void)hipEventDestroy(e);
+    for (auto e : w->tok_ev) (void)hipEventDestroy(e);
+    w->stage.reset();
+    (void)hipStreamDestroy(w->send_st);
+    (void)hipStreamDestroy(w->recv_st);
+  }
+  links_.clear();
+  if (out_host_) (void)hipHostFree(out_host_);
+}
+
+bool Engine::owns_last() const {
+  for (auto& w : workers_) if (w->stage->spec().last()) return true;
+  return false;
+}
+bool Engine::owns_first() const {
+  for (auto& w : workers_) if (w->stage->spec().first()) return true;
+  return false;
+}
+
+void Engine::build_links(const Json& j) {
+  if (S_ == 1) return;
+  // link i: stage i -> stage (i+1) % S (link S-1 is the token ring back to stage 0)
+  const size_t act_bytes = (size_t)std::max(chunk_, B_) * cfg_.d_model * 4;
+  if (mode_ == "local") {
+    const std::string kind = j.get_str("link", "local");
+    std::vector<Link*> fwd(S_);
+    for (int i = 0; i < S_; ++i) {
+      const int a = i, b = (i + 1) % S_;
+      if (kind == "rccl") {
+        void *ca, *cb;
+        rccl_make_pair(specs_[a].device, specs_[b].device, &ca, &cb);
+        links_.emplace_back(new RcclLink(ca, 0, specs_[a].device));   // sender end
+        Link* snd = links_.back().get();
+        links_.emplace_back(new RcclLink(cb, 1, specs_[b].device));   // receiver end
+        Link* rcv = links_.back().get();
+        workers_[a]->out = snd;
+        workers_[b]->in = rcv;
+      } else {
+        links_.emplace_back(new LocalLink(specs_[a].device, specs_[b].device, act_bytes, std::max(4, M_ + 2)));
+        workers_[a]->out = links_.back().get();
+        workers_[b]->in = links_.back().get();
+      }
+    }
+    MP_LOGI("links: %d x %s (act %.1f KiB/token, ring %d B/token)", S_, kind.c_str(), cfg_.d_model * 4 / 1024.0, 4);
+  } else {
+    const auto& ids = j["rccl_ids"].arr();
+    if ((int)ids.size() != S_) throw std::runtime_error("mp mode needs one RCCL id per link");
+    const int in_l = (rank_ - 1 + S_) % S_, out_l = rank_;
+    Worker& w = *workers_[0];
+    for (int l : {std::min(in_l, out_l), std::max(in_l, out_l)}) {
+      auto id = unhex(ids[l].str());
+      const bool sender = (l == out_l);
+      void* c = rccl_init_rank(id.data(), sender ? 0 : 1, w.device);
+      links_.emplace_back(new RcclLink(c, sender ? 0 : 1, w.device));
+      if (sender) w.out = links_.back().get();
+      else w.in = links_.back().get();
+    }
+    MP_LOGI("rank %d: RCCL links in=%d out=%d on GPU %d", rank_, in_l, out_l, w.device);
+  }
+}
+
+void Engine::post_ring_recv(Worker& w, int mb) {
+  HipStage& st = *w.stage;
+  HIP_OK(hipEventRecord(w.comp_ev[mb], st.stream()));
+  HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
+  w.in->recv(st.tokens(mb), (size_t)B_ * 4, w.recv_st);
+  HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
+}
+
+void Engine::run_items(Worker& w, const std::vector<Item>& items) {
+  HIP_OK(hipSetDevice(w.device));
+  HipStage& st = *w.stage;
+  hipStream_t cs = st.stream();
+  const bool first = st.spec().first(), last = st.spec().last();
+  const size_t d4 = (size_t)cfg_.d_model * 4;
+  auto recv_into = [&](int mb, void* buf, size_t bytes) {
+    if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(w.recv_st, w.sent_ev[mb], 0));
+    HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
+    HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
+    w.in->recv(buf, bytes, w.recv_st);
+    HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
+    HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
+  };
+  auto send_from = [&](int mb, const void* buf, size_t bytes) {
+    HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
+    HIP_OK(hipStreamWaitEvent(w.send_st, w.comp_ev[mb], 0));
+    w.out->send(buf, bytes, w.send_st);
+    HIP_OK(hipEventRecord(w.sent_ev[mb], w.send_st));
+    w.sent_valid[mb] = true;
+  };
+  for (const Item& it : items) {
+    const int mb = it.mb;
+    switch (it.kind) {
+      case Item::PREFILL: {
+        const size_t bytes = (size_t)it.T * d4;
+        if (!first) recv_into(mb, st.act(mb), bytes);
+        else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
+        const int slot = st.slot_of(mb, it.b);
+        st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_dev() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
+                         it.last_chunk, cs);
+        if (!last) send_from(mb, st.act(mb), bytes);
+        break;
+      }
+      case Item::PREFILL_END: {
+        if (last) HIP_OK(hipMemcpyAsync(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4,
+                                        hipMemcpyDeviceToHost, cs));
+        if (S_ > 1) {
+          if (last) send_from(mb, st.tokens(mb), (size_t)B_ * 4);
+          if (first) post_ring_recv(w, mb);
+        }
+        break;
+      }
+      case Item::DECODE: {
+        if (!first) recv_into(mb, st.act(mb), (size_t)B_ * d4);
+        else if (S_ > 1) HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
+        if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
+        st.decode(mb, cs);
+        if (last) {
+          const size_t ev_i = (size_t)(it.round - rounds_done_) * M_ + mb;
+          if (ev_i < w.tok_ev.size()) HIP_OK(hipEventRecord(w.tok_ev[ev_i], cs));
+          HIP_OK(hipMemcpyAsync(out_host_ + ((size_t)(it.round + 1) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4,
+                                hipMemcpyDeviceToHost, cs));
+        }
+        if (S_ > 1) {
+          if (!last) send_from(mb, st.act(mb), (size_t)B_ * d4);
+          else send_from(mb, st.tokens(mb), (size_t)B_ * 4);
+          if (first) post_ring_recv(w, mb);
+        }
+        break;
+      }
+    }
+  }
+}
+
+void Engine::run_all(const std::vector<Item>& items) {
+  if (workers_.size() == 1) {
+    run_items(*workers_[0], items);
+  } else {
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> errs(workers_.size());
+    for (size_t i = 0; i < workers_.size(); ++i)
+      th.emplace_back([&, i] {
+        try {
+          run_items(*workers_[i], items);
+        } catch (...) {
+          errs[i] = std::current_exception();
+          for (auto& l : links_) l->abort();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  sync_all();
+}
+
+void Engine::sync_all() {
+  for (auto& w : workers_) {
+    HIP_OK(hipSetDevice(w->device));
+    HIP_OK(hipStreamSynchronize(w->stage->stream()));
+    HIP_OK(hipStreamSynchronize(w->send_st));
+    // the first stage keeps ring receives posted for the next round; they complete once the last
+    // stage sends, which it has (every DECODE / PREFILL_END sends), so this does not block forever
+    HIP_OK(hipStreamSynchronize(w->recv_st));
+  }
+}
+
+void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
+  if ((int)prompts.size() > M_ * B_) throw std::runtime_error("more prompts than micro-batch slots");
+  prompts_ = prompts;
+  gen_.assign(prompts.size(), {});
+  rounds_done_ = 0;
+  std::vector<Item> items;
+  for (auto& w : workers_) {
+    HipStage& st = *w->stage;
+    HIP_OK(hipSetDevice(w->device));
+    for (int mb = 0; mb < M_; ++mb) {
+      std::vector<int32_t> pos(B_, 0);
+      for (int b = 0; b < B_; ++b) {
+        const size_t i = (size_t)mb * B_ + b;
+        if (i < prompts.size()) pos[b] = (int)prompts[i].size();
+      }
+      st.set_positions(mb, pos, st.stream());
+    }
+    if (st.spec().first()) {
+      for (size_t i = 0; i < prompts.size(); ++i) {
+        if (prompts[i].empty() || (int)prompts[i].size() >= max_ctx_) throw std::runtime_error("bad prompt length");
+        HIP_OK(hipMemcpy(st.prompt_dev() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4,
+                         hipMemcpyHostToDevice));
+      }
+    }
+  }
+  for (int mb = 0; mb < M_; ++mb) {
+    for (int b = 0; b < B_; ++b) {
+      const size_t i = (size_t)mb * B_ + b;
+      if (i >= prompts.size()) continue;
+      const int n = (int)prompts[i].size();
+      for (int p0 = 0; p0 < n; p0 += chunk_) {
+        Item it{Item::PREFILL};
+        it.mb = mb; it.b = b; it.p0 = p0; it.T = std::min(chunk_, n - p0); it.last_chunk = p0 + it.T >= n;
+        items.push_back(it);
+      }
+    }
+    Item e{Item::PREFILL_END};
+    e.mb = mb;
+    items.push_back(e);
+  }
+  run_all(items);
+  started_ = true;
+  if (owns_last())
+    for (size_t i = 0; i < prompts.size(); ++i) gen_[i].push_back(out_host_[i]);
+}
+
+StepStats Engine::decode_steps(int k) {
+  if (!started_) throw std::runtime_error("decode_steps before start");
+  size_t max_prompt = 0;
+  for (auto& p : prompts_) max_prompt = std::max(max_prompt, p.size());
+  if (rounds_done_ + k + 1 >= rounds_cap_ || (int)max_prompt + rounds_done_ + k + 1 > max_ctx_)
+    throw std::runtime_error("context capacity exhausted (prompt + generated tokens > max_ctx)");
+  for (auto& w : workers_)
+    if (w->stage->spec().last()) {
+      HIP_OK(hipSetDevice(w->device));
+      for (auto e : w->tok_ev) (void)hipEventDestroy(e);
+      w->tok_ev.assign((size_t)k * M_, nullptr);
+      for (auto& e : w->tok_ev) HIP_OK(hipEventCreate(&e));
+    }
+  std::vector<Item> items;
+  for (int r = 0; r < k; ++r)
+    for (int mb = 0; mb < M_; ++mb) {
+      Item it{Item::DECODE};
+      it.mb = mb;
+      it.round = rounds_done_ + r;
+      items.push_back(it);
+    }
+  const double t0 = now_ms();
+  run_all(items);
+  StepStats ss;
+  ss.wall_ms = now_ms() - t0;
+  for (auto& w : workers_)
+    if (w->stage->spec().last()) {
+      for (int r = 1; r < k; ++r)
+        for (int mb = 0; mb < M_; ++mb) {
+          float ms = 0;
+          HIP_OK(hipEventElapsedTime(&ms, w->tok_ev[(size_t)(r - 1) * M_ + mb], w->tok_ev[(size_t)r * M_ + mb]));
+          ss.token_ms.push_back(ms);
+        }
+    }
+  if (owns_last())
+    for (int r = 0; r < k; ++r)
+      for (size_t i = 0; i < prompts_.size(); ++i) {
+        const int32_t t = out_host_[(size_t)(rounds_done_ + r + 1) * M_ * B_ + i];
+        gen_[i].push_back(t);
+        if (on_token) on_token((int)i, t);
+      }
+  rounds_done_ += k;
+  return ss;
+}
+
+std::vector<std::vector<int32_t>> Engine::tokens() const { return gen_; }
+
+Json Engine::generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict,
+                      std::vector<std::vector<int32_t>>* out) {
+  const double t0 = now_ms();
+  start(prompts);
+  const double t1 = now_ms();
+  StepStats ss;
+  if (n_predict > 1) ss = decode_steps(n_predict - 1);
+  const double t2 = now_ms();
+  if (out) *out = gen_;
+  size_t n_prompt = 0;
+  for (auto& p : prompts) n_prompt += p.size();
+  Json j = Json::object();
+  j["prefill_ms"] = t1 - t0;
+  j["decode_ms"] = t2 - t1;
+  j["n_prompt_tokens"] = (int64_t)n_prompt;
+  j["n_decode_tokens"] = (int64_t)(prompts.size() * std::max(0, n_predict - 1));
+  j["prompt_tok_s"] = n_prompt / std::max(1e-9, (t1 - t0) / 1e3);
+  j["decode_tok_s"] = prompts.size() * std::max(0, n_predict - 1) / std::max(1e-9, (t2 - t1) / 1e3);
+  j["p50_ms"] = pct(ss.token_ms, 0.5);
+  j["p90_ms"] = pct(ss.token_ms, 0.9);
+  j["p99_ms"] = pct(ss.token_ms, 0.99);
+  return j;
+}
+
+Json Engine::bench(int prompt_len, int warmup, int steps) {
+  std::vector<std::vector<int32_t>> prompts(M_ * B_);
+  uint32_t h = 12345;
+  for (auto& p : prompts) {
+    p.resize(prompt_len);
+    for (auto& t : p) { h = h * 1664525u + 1013904223u; t = (int32_t)(h % (uint32_t)cfg_.vocab); }
+  }
+  const double t0 = now_ms();
+  start(prompts);
+  const double t1 = now_ms();
+  if (warmup > 0) decode_steps(warmup);
+  StepStats ss = decode_steps(steps);
+  Json j = Json::object();
+  const double toks = (double)steps * M_ * B_;
+  j["decode_tok_s"] = toks / (ss.wall_ms / 1e3);
+  j["wall_ms"] = ss.wall_ms;
+  j["ms_per_round"] = ss.wall_ms / std::max(1, steps);
+  j["p50_ms"] = pct(ss.token_ms, 0.5);
+  j["p90_ms"] = pct(ss.token_ms, 0.9);
+  j["p99_ms"] = pct(ss.token_ms, 0.99);
+  j["prefill_ms"] = t1 - t0;
+  j["prompt_tok_s"] = (double)prompt_len * M_ * B_ / ((t1 - t0) / 1e3);
+  return j;
+}
+
+int Engine::copy_logits(int mb, float* out, int rows) {
+  (void)mb;
+  for (auto& w : workers_)
+    if (w->stage->spec().last()) {
+      HIP_OK(hipSetDevice(w->device));
+      HIP_OK(hipStreamSynchronize(w->stage->stream()));
+      HIP_OK(hipMemcpy2D(out, (size_t)cfg_.vocab * 4, w->stage->logits(), (size_t)w->stage->logits_ld() * 4,
+                         (size_t)cfg_.vocab * 4, rows, hipMemcpyDeviceToHost));
+      return 0;
+    }
+  return -1;
+}
+
+Json Engine::info() const {
+  Json j = Json::object();
+  j["n_stages"] = S_;
+  j["n_mb"] = M_;
+  j["mb_size"] = B_;
+  j["max_ctx"] = max_ctx_;
+  j["mode"] = mode_;
+  j["load_ms"] = load_ms_;
+  Json st = Json::array();
+  for (auto& s : specs_) {
+    Json o = Json::object();
+    o["stage"] = s.stage;
+    o["layer_begin"] = s.layer_begin;
+    o["layer_end"] = s.layer_end;
+    o["device"] = s.device;
+    st.push(o);
+  }
+  j["stages"] = st;
+  Json m = Json::object();
+  m["n_layer"] = cfg_.n_layer; m["d_model"] = cfg_.d_model; m["vocab"] = cfg_.vocab;
+  m["n_head"] = cfg_.n_head; m["n_head_kv"] = cfg_.n_head_kv; m["d_ff"] = cfg_.d_ff;
+  j["model"] = m;
+  size_t wb = 0, kb = 0;
+  for (auto& w : workers_) { wb += w->stage->weight_bytes(); kb += w->stage->kv_bytes(); }
+  j["weight_bytes_local"] = (int64_t)wb;
+  j["kv_bytes_local"] = (int64_t)kb;
+  return j;
+}
+
+}  // namespace mp

@@ -1,0 +1,113 @@
+// Engine = model + partition + stage workers + links + the micro-batched piped-ring scheduler.
+//
+// This replaces, MI355X-first, what the reference assembles from `llama-cli --rpc ... -ngl 99`
+// (orchestrator/src/main.rs:35-57): llama.cpp's backend scheduler runs the layer splits of the two
+// rpc-servers strictly one after the other (E7).  Here every stage owns a GPU and
+// runs concurrently: M micro-batches circulate through the S stages (activations forward,
+// sampled token ids from the last stage back to the first: the PDF's "piped-ring", D1), each
+// stage overlaps its sends/receives (dedicated comm streams, events) with the compute of the
+// other micro-batches.
+//
+// Modes (config "mode"):
+//   "local" : all stages in this process, one host thread each; devices from "devices" (may
+//             repeat a device for single-GPU PP emulation); links "local" (D2D) or "rccl".
+//   "mp"    : one stage per process (torch.distributed / torchrun launch): config carries
+//             "world", "rank" and the RCCL unique ids of the links this rank participates in.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hip_stage.h"
+#include "json.h"
+#include "model.h"
+#include "transport.h"
+
+namespace mp {
+
+class GgufFile;
+
+struct Item {
+  enum Kind { PREFILL, PREFILL_END, DECODE } kind;
+  int mb = 0, b = 0, p0 = 0, T = 0;
+  bool last_chunk = false;
+  int round = 0;
+};
+
+struct StepStats {
+  std::vector<double> token_ms;   // inter-token latency samples (per micro-batch per round)
+  double wall_ms = 0;
+};
+
+class Engine {
+ public:
+  explicit Engine(const Json& cfg);
+  ~Engine();
+
+  Json info() const;
+  const ModelConfig& model() const { return cfg_; }
+  int n_stages() const { return S_; }
+  int n_mb() const { return M_; }
+  int mb_size() const { return B_; }
+  bool owns_last() const;
+  bool owns_first() const;
+
+  // assign prompts to slots (sequence i -> mb i / B, row i % B), prefill them, produce token 0
+  void start(const std::vector<std::vector<int32_t>>& prompts);
+  // run k decode rounds (every micro-batch once per round); blocks until the GPU work is done
+  StepStats decode_steps(int k);
+  // generated tokens so far per sequence (valid where the last stage lives)
+  std::vector<std::vector<int32_t>> tokens() const;
+
+  Json generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict,
+                std::vector<std::vector<int32_t>>* out);
+  Json bench(int prompt_len, int warmup, int steps);
+  int copy_logits(int mb, float* out, int rows);
+
+  // streaming hook: called on the host (from the worker of the last stage) after each round
+  // with (sequence index, token) pairs
+  std::function<void(int seq, int32_t tok)> on_token;
+
+ private:
+  struct Worker {
+    std::unique_ptr<HipStage> stage;
+    Link* in = nullptr;    // activations from s-1 (or ring tokens from S-1 for s = 0)
+    Link* out = nullptr;   // activations to s+1 (or ring tokens to 0 for s = S-1)
+    hipStream_t send_st = nullptr, recv_st = nullptr;
+    std::vector<hipEvent_t> comp_ev, sent_ev, recv_ev;
+    std::vector<bool> sent_valid;
+    std::vector<hipEvent_t> tok_ev;   // last stage: per (round, mb) timing events
+    int device = 0;
+  };
+
+  void build_links(const Json& cfg);
+  void run_items(Worker& w, const std::vector<Item>& items);
+  void run_all(const std::vector<Item>& items);
+  void post_ring_recv(Worker& w, int mb);
+  void sync_all();
+
+  Json jcfg_;
+  ModelConfig cfg_;
+  std::vector<StageSpec> specs_;
+  int S_ = 1, M_ = 1, B_ = 1;
+  int max_ctx_ = 2048, chunk_ = 256;
+  std::string mode_ = "local";
+  int rank_ = 0;
+  std::vector<std::unique_ptr<Worker>> workers_;   // owned stages (all in local mode)
+  std::vector<std::unique_ptr<Link>> links_;
+  std::unique_ptr<GgufFile> gguf_;
+  // sequences
+  std::vector<std::vector<int32_t>> prompts_;
+  std::vector<std::vector<int32_t>> gen_;          // generated tokens per sequence
+  int32_t* out_host_ = nullptr;                    // pinned [rounds_cap][M*B]
+  int rounds_cap_ = 0, rounds_done_ = 0;
+  bool started_ = false;
+  double load_ms_ = 0;
+};
+
+}  // namespace mp

@@ -1,0 +1,456 @@
+#include "hip_stage.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "gguf.h"
+#include "log.h"
+#include "pack.h"
+
+namespace mp {
+
+void launch_prefill_meta(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, int T, int s, hipStream_t st);
+
+SyntheticTypes SyntheticTypes::from_ftype(const std::string& ftype_in, int layer, int n_layer) {
+  std::string f = ftype_in;
+  for (auto& c : f) c = (char)toupper(c);
+  SyntheticTypes t;
+  auto all = [&](int ty) { t.embd = t.q = t.k = t.v = t.o = t.gate = t.up = t.down = t.out = ty; };
+  auto more_bits = [&](int i, int n) { return i < n / 8 || i >= 7 * n / 8 || (i - n / 8) % 3 == 2; };
+  if (f == "F16") all(T_F16);
+  else if (f == "BF16") all(T_BF16);
+  else if (f == "F32") all(T_F32);
+  else if (f == "Q8_0") all(T_Q8_0);
+  else if (f == "Q6_K") all(T_Q6_K);
+  else if (f == "Q5_K" || f == "Q5_K_M") { all(T_Q5_K); t.out = T_Q6_K; }
+  else if (f == "Q4_0") all(T_Q4_0);
+  else if (f == "Q4_K" || f == "Q4_K_S") { all(T_Q4_K); t.out = T_Q6_K; }
+  else if (f == "Q4_K_M") {
+    all(T_Q4_K);
+    t.out = T_Q6_K;
+    if (more_bits(layer, n_layer)) { t.v = T_Q6_K; t.down = T_Q6_K; }
+  } else throw std::runtime_error("unknown synthetic ftype " + ftype_in);
+  if (f == "Q5_K_M" && more_bits(layer, n_layer)) { t.v = T_Q6_K; t.down = T_Q6_K; }
+  return t;
+}
+
+HipStage::HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOptions& opt)
+    : cfg_(cfg), spec_(spec), opt_(opt) {
+  HIP_OK(hipSetDevice(spec_.device));
+  HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (opt_.max_ctx % 64) opt_.max_ctx = (int)round_up(opt_.max_ctx, 64);
+  if (opt_.prefill_chunk < 1) opt_.prefill_chunk = 1;
+  layers_.resize(spec_.layer_end - spec_.layer_begin);
+  Dp_ = cfg_.padded_head_dim();
+  Kd_ = (int)round_up(cfg_.d_model, 256);
+  Ko_ = (int)round_up(cfg_.q_dim(), 256);
+  Kff_ = (int)round_up(cfg_.d_ff, 256);
+  qkv_n_ = cfg_.q_dim() + 2 * cfg_.kv_dim();
+}
+
+HipStage::~HipStage() {
+  hipSetDevice(spec_.device);
+  destroy_graphs();
+  for (void* p : allocs_) hipFree(p);
+  if (pf_host_) hipHostFree(pf_host_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+void* HipStage::dmalloc(size_t bytes) {
+  void* p = nullptr;
+  HIP_OK(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+  allocs_.push_back(p);
+  return p;
+}
+
+float* HipStage::upload_f32(const float* h, size_t n) {
+  float* d = (float*)dmalloc(n * sizeof(float));
+  HIP_OK(hipMemcpy(d, h, n * sizeof(float), hipMemcpyHostToDevice));
+  weight_bytes_ += n * sizeof(float);
+  return d;
+}
+
+PackedMat HipStage::upload_packed(int t, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row) {
+  PackedMat m;
+  m.ptype = pack_type_of(t);
+  if (m.ptype < 0) throw std::runtime_error(std::string("unsupported weight type ") + type_name(t));
+  m.dims = packed_dims(m.ptype, N, K);
+  std::vector<uint8_t> host(m.dims.bytes);
+  pack_t16(t, N, K, row, host.data());
+  m.d = (uint8_t*)dmalloc(m.dims.bytes);
+  HIP_OK(hipMemcpy(m.d, host.data(), m.dims.bytes, hipMemcpyHostToDevice));
+  weight_bytes_ += m.dims.bytes;
+  return m;
+}
+
+PackedMat HipStage::alloc_packed_random(int t, int64_t N, int64_t K, uint64_t seed) {
+  PackedMat m;
+  m.ptype = pack_type_of(t);
+  m.dims = packed_dims(m.ptype, N, K);
+  m.d = (uint8_t*)dmalloc(m.dims.bytes);
+  launch_init_packed(m.d, m.dims.bytes, m.ptype, 1.0f / std::sqrt((float)K), seed, stream_);
+  weight_bytes_ += m.dims.bytes;
+  return m;
+}
+
+static std::vector<float> tensor_f32(const GgufTensor& t) {
+  std::vector<float> v(t.nelem());
+  const int64_t K = t.ne[0];
+  const size_t rb = row_bytes(t.type, K);
+  for (int64_t r = 0; r < t.nelem() / K; ++r) dequant_row(t.type, t.data + r * rb, v.data() + r * K, K);
+  return v;
+}
+
+void HipStage::load_gguf(const GgufFile& f) {
+  HIP_OK(hipSetDevice(spec_.device));
+  auto need = [&](const std::string& n) -> const GgufTensor& {
+    const GgufTensor* t = f.tensor(n);
+    if (!t) throw std::runtime_error("missing tensor " + n);
+    return *t;
+  };
+  auto rows_of = [](const GgufTensor& t) {
+    const size_t rb = row_bytes(t.type, t.ne[0]);
+    return [&t, rb](int64_t n) -> const uint8_t* { return t.data + n * rb; };
+  };
+  auto pack_mat = [&](const GgufTensor& t) { return upload_packed(t.type, t.ne[1], t.ne[0], rows_of(t)); };
+
+  for (int li = spec_.layer_begin; li < spec_.layer_end; ++li) {
+    LayerW& L = layers_[li - spec_.layer_begin];
+    const std::string p = "blk." + std::to_string(li) + ".";
+    {
+      auto v = tensor_f32(need(p + "attn_norm.weight"));
+      L.attn_norm = upload_f32(v.data(), v.size());
+      auto w = tensor_f32(need(p + "ffn_norm.weight"));
+      L.ffn_norm = upload_f32(w.data(), w.size());
+    }
+    const GgufTensor& tq = need(p + "attn_q.weight");
+    const GgufTensor& tk = need(p + "attn_k.weight");
+    const GgufTensor& tv = need(p + "attn_v.weight");
+    // merge same-type q/k/v into one launch (tile-major layout concatenates)
+    const GgufTensor* qkv[3] = {&tq, &tk, &tv};
+    int off = 0;
+    for (int i = 0; i < 3;) {
+      int j = i + 1;
+      while (j < 3 && pack_type_of(qkv[j]->type) == pack_type_of(qkv[i]->type) && qkv[j - 1]->ne[1] % 16 == 0 &&
+             qkv[j]->type == qkv[i]->type)
+        ++j;
+      int64_t N = 0;
+      std::vector<std::pair<const GgufTensor*, int64_t>> parts;
+      for (int k = i; k < j; ++k) { parts.push_back({qkv[k], N}); N += qkv[k]->ne[1]; }
+      auto rowfn = [&parts](int64_t n) -> const uint8_t* {
+        for (auto it = parts.rbegin(); it != parts.rend(); ++it)
+          if (n >= it->second) {
+            const GgufTensor* t = it->first;
+            return t->data + (n - it->second) * row_bytes(t->type, t->ne[0]);
+          }
+        return nullptr;
+      };
+      MatSeg s;
+      s.m = upload_packed(qkv[i]->type, N, qkv[i]->ne[0], rowfn);
+      s.y_off = off;
+      off += (int)N;
+      L.qkv.push_back(s);
+      i = j;
+    }
+    L.wo = pack_mat(need(p + "attn_output.weight"));
+    if (cfg_.n_expert) {
+      throw std::runtime_error("MoE weights: use load path with experts (not yet wired)");
+    }
+    const GgufTensor& tg = need(p + "ffn_gate.weight");
+    const GgufTensor& tu = need(p + "ffn_up.weight");
+    if (tg.type == tu.type && cfg_.d_ff % 8 == 0) {
+      L.fused_gateup = true;
+      const size_t rb = row_bytes(tg.type, tg.ne[0]);
+      const int64_t F = tg.ne[1];
+      L.gateup = upload_packed(tg.type, 2 * F, tg.ne[0], [&](int64_t n) -> const uint8_t* {
+        bool up;
+        const int64_t r = gateup_src_row(n, &up);
+        if (r >= F) return nullptr;
+        return (up ? tu.data : tg.data) + r * rb;
+      });
+    } else {
+      L.fused_gateup = false;
+      L.gate = pack_mat(tg);
+      L.up = pack_mat(tu);
+    }
+    L.down = pack_mat(need(p + "ffn_down.weight"));
+  }
+  const GgufTensor& te = need("token_embd.weight");
+  if (spec_.first()) {
+    embd_type_ = te.type;
+    embd_row_bytes_ = row_bytes(te.type, te.ne[0]);
+    embd_raw_ = (uint8_t*)dmalloc(te.nbytes);
+    HIP_OK(hipMemcpy(embd_raw_, te.data, te.nbytes, hipMemcpyHostToDevice));
+    weight_bytes_ += te.nbytes;
+  }
+  if (spec_.last()) {
+    auto v = tensor_f32(need("output_norm.weight"));
+    out_norm_ = upload_f32(v.data(), v.size());
+    const GgufTensor* to = f.tensor("output.weight");
+    out_ = pack_mat(to ? *to : te);
+  }
+  rope_ff_.clear();
+  if (const GgufTensor* rf = f.tensor("rope_freqs.weight")) rope_ff_ = tensor_f32(*rf);
+  HIP_OK(hipDeviceSynchronize());
+}
+
+void HipStage::init_synthetic(const std::string& ftype, uint64_t seed) {
+  HIP_OK(hipSetDevice(spec_.device));
+  const int d = cfg_.d_model, qd = cfg_.q_dim(), kvd = cfg_.kv_dim(), F = cfg_.d_ff;
+  std::vector<float> ones(std::max(d, 1), 1.0f);
+  for (int li = spec_.layer_begin; li < spec_.layer_end; ++li) {
+    LayerW& L = layers_[li - spec_.layer_begin];
+    const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, li, cfg_.n_layer);
+    const uint64_t s = seed * 1000003ULL + (uint64_t)li * 97;
+    L.attn_norm = upload_f32(ones.data(), d);
+    L.ffn_norm = upload_f32(ones.data(), d);
+    int off = 0;
+    if (t.q == t.k && t.k == t.v) {
+      L.qkv.push_back({alloc_packed_random(t.q, qd + 2 * kvd, d, s + 1), 0});
+    } else if (t.q == t.k) {
+      L.qkv.push_back({alloc_packed_random(t.q, qd + kvd, d, s + 1), 0});
+      L.qkv.push_back({alloc_packed_random(t.v, kvd, d, s + 2), qd + kvd});
+    } else {
+      L.qkv.push_back({alloc_packed_random(t.q, qd, d, s + 1), off});
+      L.qkv.push_back({alloc_packed_random(t.k, kvd, d, s + 2), qd});
+      L.qkv.push_back({alloc_packed_random(t.v, kvd, d, s + 3), qd + kvd});
+    }
+    L.wo = alloc_packed_random(t.o, d, qd, s + 4);
+    if (cfg_.n_expert) throw std::runtime_error("synthetic MoE not wired yet");
+    L.fused_gateup = true;
+    L.gateup = alloc_packed_random(t.gate, 2 * F, d, s + 5);
+    L.down = alloc_packed_random(t.down, d, F, s + 6);
+  }
+  const SyntheticTypes t0 = SyntheticTypes::from_ftype(ftype, 0, cfg_.n_layer);
+  if (spec_.first()) {
+    embd_type_ = t0.embd;
+    embd_row_bytes_ = row_bytes(embd_type_, d);
+    const size_t nb = embd_row_bytes_ * (size_t)cfg_.vocab;
+    embd_raw_ = (uint8_t*)dmalloc(nb);
+    launch_init_raw(embd_raw_, (int64_t)(nb / block_bytes(embd_type_)), embd_type_, 1.0f, seed ^ 0xE3BD, stream_);
+    weight_bytes_ += nb;
+  }
+  if (spec_.last()) {
+    out_norm_ = upload_f32(ones.data(), d);
+    out_ = alloc_packed_random(t0.out, cfg_.vocab, d, seed ^ 0x0F7);
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+void HipStage::alloc_runtime() {
+  HIP_OK(hipSetDevice(spec_.device));
+  const int B = opt_.mb_size, NM = opt_.n_mb;
+  const int d = cfg_.d_model, Hq = cfg_.n_head, Hkv = cfg_.n_head_kv;
+  scratch_rows_ = std::max(B, opt_.prefill_chunk);
+  act_rows_ = scratch_rows_;
+  auto zalloc = [&](size_t bytes) {
+    void* p = dmalloc(bytes);
+    HIP_OK(hipMemset(p, 0, bytes));
+    return p;
+  };
+  xn_ = (f16*)zalloc((size_t)scratch_rows_ * Kd_ * 2);
+  attn_ = (f16*)zalloc((size_t)scratch_rows_ * Ko_ * 2);
+  h_ = (f16*)zalloc((size_t)scratch_rows_ * Kff_ * 2);
+  qkv_ = (float*)zalloc((size_t)scratch_rows_ * qkv_n_ * 4);
+  q_ = (f16*)zalloc((size_t)scratch_rows_ * Hq * Dp_ * 2);
+  bool any_unfused = false;
+  for (auto& L : layers_) any_unfused |= !L.fused_gateup;
+  if (any_unfused) gu_ = (float*)zalloc((size_t)scratch_rows_ * 2 * cfg_.d_ff * 4);
+  if (spec_.last()) {
+    logits_ld_ = (int)round_up(cfg_.vocab, 16);
+    logits_ = (float*)zalloc((size_t)B * logits_ld_ * 4);
+  }
+  const int split = std::max(128, (int)round_up(opt_.attn_split_len, 128));
+  opt_.attn_split_len = split;
+  n_split_ = (int)((opt_.max_ctx + split - 1) / split);
+  if (n_split_ > 1) {
+    o_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * Dp_ * 4);
+    ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
+  }
+  // KV cache: static paging, every slot owns max_ctx/64 pages
+  const int n_slots = NM * B;
+  max_pages_ = opt_.max_ctx / 64;
+  const int64_t n_pages = (int64_t)n_slots * max_pages_;
+  const size_t per = (size_t)n_pages * Hkv * 64 * Dp_ * 2;
+  for (size_t i = 0; i < layers_.size(); ++i) {
+    kc_.push_back((f16*)zalloc(per));
+    vc_.push_back((f16*)zalloc(per));
+    kv_bytes_ += 2 * per;
+  }
+  std::vector<int32_t> bt((size_t)n_slots * max_pages_);
+  for (size_t i = 0; i < bt.size(); ++i) bt[i] = (int32_t)i;
+  block_table_ = (int32_t*)dmalloc(bt.size() * 4);
+  HIP_OK(hipMemcpy(block_table_, bt.data(), bt.size() * 4, hipMemcpyHostToDevice));
+  // RoPE table (NORM mode), Llama-3.1 frequency factors if present
+  const int hd2 = cfg_.head_dim / 2;
+  std::vector<float2> cs((size_t)opt_.max_ctx * hd2);
+  for (int i = 0; i < hd2; ++i) {
+    double inv = std::pow((double)cfg_.rope_base, -2.0 * i / cfg_.head_dim);
+    if (!rope_ff_.empty()) inv /= rope_ff_[i];
+    for (int p = 0; p < opt_.max_ctx; ++p) {
+      const double a = p * inv;
+      cs[(size_t)p * hd2 + i] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+  }
+  rope_cs_ = (float2*)dmalloc(cs.size() * sizeof(float2));
+  HIP_OK(hipMemcpy(rope_cs_, cs.data(), cs.size() * sizeof(float2), hipMemcpyHostToDevice));
+  // per micro-batch I/O
+  for (int mb = 0; mb < NM; ++mb) {
+    act_.push_back((float*)zalloc((size_t)act_rows_ * d * 4));
+    tok_.push_back((int32_t*)zalloc(std::max(B, 16) * 4));
+    pos_.push_back((int32_t*)zalloc(std::max(B, 16) * 4));
+    kvlen_.push_back((int32_t*)zalloc(std::max(B, 16) * 4));
+    std::vector<int32_t> sl(std::max(B, 16), 0);
+    for (int b = 0; b < B; ++b) sl[b] = slot_of(mb, b);
+    int32_t* sd = (int32_t*)dmalloc(sl.size() * 4);
+    HIP_OK(hipMemcpy(sd, sl.data(), sl.size() * 4, hipMemcpyHostToDevice));
+    slot_.push_back(sd);
+  }
+  step_ = (int32_t*)zalloc(16);
+  pf_pos_ = (int32_t*)zalloc((size_t)opt_.prefill_chunk * 4);
+  pf_kvlen_ = (int32_t*)zalloc((size_t)opt_.prefill_chunk * 4);
+  pf_slot_ = (int32_t*)zalloc((size_t)opt_.prefill_chunk * 4);
+  prompt_dev_ = (int32_t*)zalloc((size_t)n_slots * opt_.max_ctx * 4);
+  HIP_OK(hipDeviceSynchronize());
+  MP_LOGI("stage %d: layers %d-%d offloaded to GPU %d (%s), weights %.2f GiB, KV %.2f GiB (%d slots x %d ctx)",
+          spec_.stage, spec_.layer_begin, spec_.layer_end - 1, spec_.device,
+          spec_.first() && spec_.last() ? "embd+head" : spec_.first() ? "embd" : spec_.last() ? "head" : "mid",
+          weight_bytes_ / 1073741824.0, kv_bytes_ / 1073741824.0, n_slots, opt_.max_ctx);
+}
+
+void HipStage::set_positions(int mb, const std::vector<int32_t>& pos, hipStream_t st) {
+  std::vector<int32_t> p(std::max(opt_.mb_size, 16), 0), k(std::max(opt_.mb_size, 16), 1);
+  for (size_t i = 0; i < pos.size() && i < p.size(); ++i) { p[i] = pos[i]; k[i] = pos[i] + 1; }
+  HIP_OK(hipMemcpyAsync(pos_[mb], p.data(), p.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(kvlen_[mb], k.data(), k.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_OK(hipStreamSynchronize(st));
+}
+
+void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
+                    int n_valid, bool allow_split, hipStream_t st) {
+  for (int r0 = 0; r0 < M; r0 += 16) {
+    GemvParams p{};
+    p.W = m.d;
+    p.X = X + (size_t)r0 * ldx;
+    p.ldx = ldx;
+    p.M = std::min(16, M - r0);
+    p.Y = Y ? Y + (size_t)r0 * ldy : nullptr;
+    p.ldy = ldy;
+    p.H = H ? H + (size_t)r0 * ldh : nullptr;
+    p.ldh = ldh;
+    p.ntiles = (int)m.dims.ntiles;
+    p.nsb = (int)m.dims.nsb;
+    p.n_valid = n_valid;
+    int nsplit = 1;
+    if (allow_split && epi == EPI_ATOMIC) {
+      nsplit = (int)std::min<int64_t>((2048 + p.ntiles - 1) / p.ntiles, std::max<int64_t>(1, p.nsb / 2));
+      nsplit = std::max(1, nsplit);
+    }
+    launch_gemv(m.ptype, epi, p, nsplit, st);
+  }
+}
+
+void HipStage::layer_forward(int li, int M, int mb, float* x, const int32_t* pos, const int32_t* kvlen,
+                             const int32_t* slot, int tq, bool decode, hipStream_t st) {
+  (void)mb;
+  const LayerW& L = layers_[li];
+  const int d = cfg_.d_model;
+  launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st);
+  for (const MatSeg& s : L.qkv)
+    gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
+  RopeKvParams rp{};
+  rp.qkv = qkv_; rp.ldqkv = qkv_n_; rp.M = M; rp.Hq = cfg_.n_head; rp.Hkv = cfg_.n_head_kv;
+  rp.hd = cfg_.head_dim; rp.Dp = Dp_; rp.pos = pos; rp.slot = slot; rp.block_table = block_table_;
+  rp.max_pages = max_pages_; rp.rope_cs = rope_cs_; rp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
+  rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li];
+  launch_rope_kv(rp, st);
+  AttnParams ap{};
+  ap.q = q_; ap.kvlen = kvlen; ap.slot = slot; ap.block_table = block_table_; ap.max_pages = max_pages_;
+  ap.k_cache = kc_[li]; ap.v_cache = vc_[li]; ap.M = M; ap.Hq = cfg_.n_head; ap.Hkv = cfg_.n_head_kv;
+  ap.hd = cfg_.head_dim; ap.Dp = Dp_; ap.max_kv = opt_.max_ctx; ap.out = attn_; ap.ldo = Ko_;
+  if (decode) {
+    ap.tq = 1;
+    ap.split_len = opt_.attn_split_len;
+    ap.n_split = n_split_;
+    ap.o_part = o_part_; ap.ml_part = ml_part_;
+  } else {
+    const int G = cfg_.n_head / cfg_.n_head_kv;
+    ap.tq = std::max(1, 16 / G);
+    ap.split_len = (int)round_up(opt_.max_ctx, 128);
+    ap.n_split = 1;
+  }
+  launch_attention(ap, st);
+  gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
+  launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+  if (L.fused_gateup) {
+    gemv(L.gateup, EPI_SWIGLU, xn_, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st);
+  } else {
+    const int F = cfg_.d_ff;
+    gemv(L.gate, EPI_STORE, xn_, Kd_, M, gu_, 2 * F, nullptr, 0, F, false, st);
+    gemv(L.up, EPI_STORE, xn_, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st);
+    launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
+  }
+  gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
+}
+
+void HipStage::head(int M, const float* x, int32_t* tok_out, hipStream_t st) {
+  const int d = cfg_.d_model;
+  launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+  gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
+  launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st);
+}
+
+void HipStage::prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk,
+                             hipStream_t st) {
+  if (T > opt_.prefill_chunk) throw std::runtime_error("prefill chunk too large");
+  if (p0 + T > opt_.max_ctx) throw std::runtime_error("prompt exceeds context");
+  const int sl = slot_of(mb, b);
+  launch_prefill_meta(pf_pos_, pf_kvlen_, pf_slot_, p0, T, sl, st);
+  float* x = act_[mb];
+  if (spec_.first()) launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tokens_dev, T, x,
+                                  cfg_.d_model, st);
+  for (size_t li = 0; li < layers_.size(); ++li)
+    layer_forward((int)li, T, mb, x, pf_pos_, pf_kvlen_, pf_slot_, 0, false, st);
+  if (spec_.last() && last_chunk) head(1, x + (size_t)(T - 1) * cfg_.d_model, tok_[mb] + b, st);
+}
+
+void HipStage::decode_eager(int mb, hipStream_t st) {
+  const int B = opt_.mb_size;
+  float* x = act_[mb];
+  if (spec_.first())
+    launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tok_[mb], B, x, cfg_.d_model, st);
+  for (size_t li = 0; li < layers_.size(); ++li)
+    layer_forward((int)li, B, mb, x, pos_[mb], kvlen_[mb], slot_[mb], 1, true, st);
+  if (spec_.last()) head(B, x, tok_[mb], st);
+  launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
+}
+
+void HipStage::capture_graphs() {
+  HIP_OK(hipSetDevice(spec_.device));
+  destroy_graphs();
+  if (!opt_.use_graphs) return;
+  for (int mb = 0; mb < opt_.n_mb; ++mb) {
+    hipGraph_t g;
+    HIP_OK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
+    decode_eager(mb, stream_);
+    HIP_OK(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t ex;
+    HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(g));
+    graphs_.push_back(ex);
+  }
+}
+
+void HipStage::destroy_graphs() {
+  for (auto g : graphs_) hipGraphExecDestroy(g);
+  graphs_.clear();
+}
+
+void HipStage::decode(int mb, hipStream_t st) {
+  if (!graphs_.empty()) HIP_OK(hipGraphLaunch(graphs_[mb], st));
+  else decode_eager(mb, st);
+}
+
+}  // namespace mp

@@ -1,0 +1,178 @@
+// HipStage: one pipeline stage on one MI355X = a contiguous layer range, its packed weights in
+// HBM, its share of the paged KV cache, per-micro-batch I/O buffers and one captured hipGraph per
+// micro-batch for the decode step (E5/E6/E9 of SURVEY.md §2.2, MI355X-native).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels_api.h"
+#include "model.h"
+#include "qtypes.h"
+
+namespace mp {
+
+class GgufFile;
+
+#define HIP_OK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                                   " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+struct StageOptions {
+  int n_mb = 1;             // micro-batches in flight
+  int mb_size = 1;          // sequences per micro-batch
+  int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
+  int prefill_chunk = 256;  // max tokens per prefill chunk
+  bool use_graphs = true;
+  int attn_split_len = 256; // decode flash-decoding split length (multiple of 128)
+};
+
+// ggml types of the 2-D weights when initialising a synthetic model on device
+struct SyntheticTypes {
+  int embd = T_Q4_K, q = T_Q4_K, k = T_Q4_K, v = T_Q4_K, o = T_Q4_K, gate = T_Q4_K, up = T_Q4_K,
+      down = T_Q4_K, out = T_Q6_K;
+  static SyntheticTypes from_ftype(const std::string& ftype, int layer, int n_layer);
+};
+
+struct PackedMat {
+  uint8_t* d = nullptr;
+  int ptype = -1;
+  PackedDims dims{};
+  size_t bytes() const { return dims.bytes; }
+};
+
+struct MatSeg {  // one launch of a (possibly merged) projection
+  PackedMat m;
+  int y_off = 0;  // output column offset
+};
+
+struct ExpertW {  // MoE layer weights (Mixtral); experts stored back to back
+  uint8_t* gateup = nullptr; int gu_ptype = -1; PackedDims gu_dims{}; size_t gu_stride = 0;
+  uint8_t* down = nullptr; int dn_ptype = -1; PackedDims dn_dims{}; size_t dn_stride = 0;
+  float* router = nullptr;    // [E][d] f32
+  uint8_t* router_packed = nullptr; PackedMat router_m;
+};
+
+struct LayerW {
+  float* attn_norm = nullptr;
+  float* ffn_norm = nullptr;
+  std::vector<MatSeg> qkv;
+  PackedMat wo;
+  bool fused_gateup = true;
+  PackedMat gateup;           // interleaved (fused SwiGLU)
+  PackedMat gate, up;         // unfused fallback
+  PackedMat down;
+  bool moe = false;
+  ExpertW ex;
+};
+
+class HipStage {
+ public:
+  HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOptions& opt);
+  ~HipStage();
+
+  void load_gguf(const GgufFile& f);
+  void init_synthetic(const std::string& ftype, uint64_t seed);
+  void alloc_runtime();   // KV cache, buffers, rope tables (after weights)
+
+  const StageSpec& spec() const { return spec_; }
+  const ModelConfig& cfg() const { return cfg_; }
+  hipStream_t stream() const { return stream_; }
+  int device() const { return spec_.device; }
+
+  // --- per micro-batch buffers (device) ---
+  float* act(int mb) { return act_[mb]; }          // [act_rows][d] f32 residual in/out
+  int32_t* tokens(int mb) { return tok_[mb]; }     // [mb_size] (first: input, last: output)
+  size_t act_bytes(int rows) const { return (size_t)rows * cfg_.d_model * sizeof(float); }
+  int act_rows() const { return act_rows_; }
+
+  // --- sequence state ---
+  // set positions for micro-batch mb (host values) before decode; kvlen = pos + 1
+  void set_positions(int mb, const std::vector<int32_t>& pos, hipStream_t st);
+  int slot_of(int mb, int b) const { return mb * opt_.mb_size + b; }
+
+  // Prefill T tokens of sequence (mb, b) starting at position p0.  First stage: tokens_dev holds
+  // the T token ids (device); otherwise act(mb) holds the incoming activations.  On the last
+  // stage and `last_chunk`, the greedy next token is written to tokens(mb)[b].
+  void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk, hipStream_t st);
+
+  // One decode step for micro-batch mb (graph replay if captured).
+  void decode(int mb, hipStream_t st);
+  void capture_graphs();
+  void destroy_graphs();
+
+  // host prompt staging (pinned) for the first stage
+  int32_t* prompt_dev() { return prompt_dev_; }
+  int prompt_cap() const { return opt_.prefill_chunk; }
+
+  size_t weight_bytes() const { return weight_bytes_; }
+  size_t kv_bytes() const { return kv_bytes_; }
+  float* logits() { return logits_; }
+  int logits_ld() const { return logits_ld_; }
+
+  // reference decode body (no graph), exposed for tests
+  void decode_eager(int mb, hipStream_t st);
+
+ private:
+  void layer_forward(int li, int M, int mb, float* x, const int32_t* pos, const int32_t* kvlen,
+                     const int32_t* slot, int tq, bool decode, hipStream_t st);
+  void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
+            int n_valid, bool allow_split, hipStream_t st);
+  void head(int M, const float* x, int32_t* tok_out, hipStream_t st);
+  PackedMat upload_packed(int ggml_type, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row);
+  PackedMat alloc_packed_random(int ggml_type, int64_t N, int64_t K, uint64_t seed);
+  float* upload_f32(const float* h, size_t n);
+  void* dmalloc(size_t bytes);
+
+  ModelConfig cfg_;
+  StageSpec spec_;
+  StageOptions opt_;
+  hipStream_t stream_ = nullptr;
+  std::vector<void*> allocs_;
+  size_t weight_bytes_ = 0, kv_bytes_ = 0;
+
+  // weights
+  std::vector<LayerW> layers_;
+  uint8_t* embd_raw_ = nullptr; int embd_type_ = 0; size_t embd_row_bytes_ = 0;
+  float* out_norm_ = nullptr;
+  PackedMat out_;
+
+  // dims
+  int Kd_ = 0, Ko_ = 0, Kff_ = 0, qkv_n_ = 0, Dp_ = 0;
+  int act_rows_ = 0, scratch_rows_ = 0;
+
+  // scratch (shared by micro-batches: compute is serial on the stage's stream)
+  f16* xn_ = nullptr; float* qkv_ = nullptr; f16* q_ = nullptr; f16* attn_ = nullptr; f16* h_ = nullptr;
+  float* gu_ = nullptr;   // unfused gate|up f32
+  float* logits_ = nullptr; int logits_ld_ = 0;
+  float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
+  // MoE scratch
+  float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
+  float* moe_w_ = nullptr; int32_t* moe_eid_ = nullptr; f16* moe_h_ = nullptr;
+  // KV
+  std::vector<f16*> kc_, vc_;
+  int32_t* block_table_ = nullptr; int max_pages_ = 0;
+  float2* rope_cs_ = nullptr;
+  std::vector<float> rope_ff_;
+  // per-mb I/O
+  std::vector<float*> act_;
+  std::vector<int32_t*> tok_, pos_, kvlen_, slot_;
+  int32_t* step_ = nullptr;
+  // prefill metadata
+  int32_t* pf_pos_ = nullptr; int32_t* pf_kvlen_ = nullptr; int32_t* pf_slot_ = nullptr;
+  int32_t* pf_host_ = nullptr;   // pinned staging
+  int32_t* prompt_dev_ = nullptr;
+  // graphs
+  std::vector<hipGraphExec_t> graphs_;
+};
+
+// device random init (init.hip)
+void launch_init_packed(uint8_t* W, size_t nbytes, int pt, float scale, uint64_t seed, hipStream_t st);
+void launch_init_raw(uint8_t* W, int64_t nblocks, int t, float scale, uint64_t seed, hipStream_t st);
+
+}  // namespace mp

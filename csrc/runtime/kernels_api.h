@@ -1,0 +1,123 @@
+// Host-visible launch API of the mipipe HIP kernels (implemented in csrc/kernels/*.hip).
+// Every launcher is asynchronous on the given stream and graph-capturable (no allocation,
+// no synchronisation inside).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+
+namespace mp {
+
+enum Epilogue : int { EPI_STORE = 0, EPI_ATOMIC = 1, EPI_SWIGLU = 2 };
+
+struct GemvParams {
+  const uint8_t* W;      // T16-packed weights
+  const f16* X;          // activations [M][ldx] (K_pad columns, zero tail)
+  int ldx;
+  int M;                 // rows of X (<= 16 for gemv)
+  float* Y;              // EPI_STORE / EPI_ATOMIC destination [M][ldy]
+  int ldy;
+  f16* H;                // EPI_SWIGLU destination [M][ldh]
+  int ldh;
+  int ntiles, nsb, sb_per_split;
+  int n_valid;           // valid output columns
+};
+
+void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
+void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, int ldo, hipStream_t st);
+
+// Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.
+void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
+
+// x f32 [M][ldx] -> out f16 [M][ldo] = rmsnorm(x) * w ; also zero `zero_n` floats at `zero`
+void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo,
+                    int M, float* zero, int64_t zero_n, hipStream_t st);
+// same but f32 output (final norm before LM head may use f16 as well)
+
+// embedding gather + dequant of raw GGUF rows -> x f32 [M][ldx]
+void launch_embed(int ggml_type, const uint8_t* table, int64_t row_bytes, int d, const int32_t* tokens,
+                  int M, float* x, int ldx, hipStream_t st);
+
+struct RopeKvParams {
+  const float* qkv;      // [M][ldqkv]: q (Hq*hd) | k (Hkv*hd) | v (Hkv*hd)
+  int ldqkv;
+  int M, Hq, Hkv, hd, Dp;  // Dp: padded head dim (64 or 128)
+  const int32_t* pos;    // [M]
+  const int32_t* slot;   // [M] sequence slot of each token
+  const int32_t* block_table;  // [n_slots][max_pages]
+  int max_pages;
+  const float2* rope_cs; // [max_pos][hd/2] (cos, sin)
+  float q_scale;         // 1/sqrt(hd)
+  f16* q_out;            // [M][Hq][Dp]
+  f16* k_cache;          // pages: [n_pages][Hkv][64][Dp]
+  f16* v_cache;          // pages: [n_pages][Hkv][Dp][64] (transposed)
+};
+void launch_rope_kv(const RopeKvParams& p, hipStream_t st);
+
+struct AttnParams {
+  const f16* q;          // [M][Hq][Dp]
+  const int32_t* kvlen;  // [M]: keys visible to token row (pos + 1)
+  const int32_t* slot;   // [M]
+  const int32_t* block_table;
+  int max_pages;
+  const f16* k_cache;
+  const f16* v_cache;
+  int M, Hq, Hkv, hd, Dp;
+  int tq;                // tokens per row group (same slot, consecutive); 1 for decode
+  int split_len;         // positions per split (multiple of 128)
+  int n_split;
+  int max_kv;            // upper bound of kvlen (grid sizing)
+  float* o_part;         // [n_split][M*Hq][Dp] partial (unnormalised) outputs
+  float* ml_part;        // [n_split][M*Hq][2] (running max, running sum)
+  f16* out;              // [M][ldo] with head h at columns h*hd..
+  int ldo;
+};
+void launch_attention(const AttnParams& p, hipStream_t st);
+
+// greedy sampling: tokens[m] = argmax logits[m][:n]
+void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st);
+// temperature / top-k / top-p / min-p sampling with a counter-based RNG
+struct SampleParams {
+  const float* logits; int ld; int n; int M;
+  float temp; int top_k; float top_p; float min_p;
+  uint64_t seed; const int32_t* step;  // step counter (device) for RNG stream
+  int32_t* tokens;
+};
+void launch_sample(const SampleParams& p, hipStream_t st);
+
+// pos[i] += 1, kvlen[i] = pos[i] + 1 for i < M (graph-resident decode step advance)
+void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st);
+
+// standalone SwiGLU: h[m][j] = silu(g[m][j]) * u[m][j]   (g,u f32; h f16)
+void launch_swiglu(const float* gu, int ld, int F, int M, f16* h, int ldh, hipStream_t st);
+// f32 -> f16 row conversion (used when an activation feeds a GEMM directly)
+void launch_f32_to_f16(const float* x, int ldx, int n, int M, f16* y, int ldy, hipStream_t st);
+
+// MoE
+struct MoeRouteParams {
+  const float* logits;   // [M][E] router logits
+  int M, E, k;
+  int32_t* counts;       // [E]
+  int32_t* lists;        // [E][M] token-slot ids (token*k + j)
+  float* weights;        // [M*k]
+  int32_t* expert_of;    // [M*k]
+};
+void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
+struct MoeGemvParams {
+  const uint8_t* W;      // [E] packed matrices, each `estride` bytes
+  size_t estride;
+  int ntiles, nsb;
+  const f16* X; int ldx; int x_per_slot;  // x row = x_per_slot ? slot : slot / k
+  int k;
+  const int32_t* counts; const int32_t* lists;
+  int max_tok;           // max tokens per expert handled (<=16 per launch chunk)
+  int E;
+  f16* H; int ldh;       // SWIGLU out per slot [M*k][ldh]
+  float* Y; int ldy;     // down out: atomic add weight*y into Y[token]
+  const float* weights;
+  int n_valid;
+};
+void launch_moe_gemv(int ptype, int epi, const MoeGemvParams& p, hipStream_t st);
+
+}  // namespace mp

@@ -1,0 +1,270 @@
+#include "transport.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include <rccl/rccl.h>
+
+#include "hip_stage.h"  // HIP_OK
+
+namespace mp {
+
+#define NCCL_OK(x)                                                                              \
+  do {                                                                                          \
+    ncclResult_t r_ = (x);                                                                      \
+    if (r_ != ncclSuccess) throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_)); \
+  } while (0)
+
+// ---------------------------------------------------------------- LocalLink
+LocalLink::LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_slots)
+    : src_dev_(src_device), dst_dev_(dst_device), slot_bytes_(slot_bytes) {
+  int cur = 0;
+  HIP_OK(hipGetDevice(&cur));
+  if (src_dev_ != dst_dev_) {
+    hipSetDevice(src_dev_);
+    hipDeviceEnablePeerAccess(dst_dev_, 0);
+    hipGetLastError();
+    hipSetDevice(dst_dev_);
+    hipDeviceEnablePeerAccess(src_dev_, 0);
+    hipGetLastError();
+  }
+  slots_.resize(n_slots);
+  ready_.resize(n_slots);
+  freed_.resize(n_slots);
+  freed_valid_.assign(n_slots, false);
+  HIP_OK(hipSetDevice(dst_dev_));
+  for (int i = 0; i < n_slots; ++i) {
+    HIP_OK(hipMalloc(&slots_[i], slot_bytes_));
+    HIP_OK(hipEventCreateWithFlags(&freed_[i], hipEventDisableTiming));
+    free_.push_back(i);
+  }
+  HIP_OK(hipSetDevice(src_dev_));
+  for (int i = 0; i < n_slots; ++i) HIP_OK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming));
+  HIP_OK(hipSetDevice(cur));
+}
+
+LocalLink::~LocalLink() {
+  for (size_t i = 0; i < slots_.size(); ++i) {
+    hipFree(slots_[i]);
+    hipEventDestroy(ready_[i]);
+    hipEventDestroy(freed_[i]);
+  }
+}
+
+void LocalLink::abort() {
+  std::lock_guard<std::mutex> l(mu_);
+  aborted_ = true;
+  cv_.notify_all();
+}
+
+void LocalLink::send(const void* buf, size_t bytes, hipStream_t st) {
+  if (bytes > slot_bytes_) throw std::runtime_error("LocalLink: message larger than slot");
+  int slot;
+  bool wait_freed;
+  {
+    std::unique_lock<std::mutex> l(mu_);
+    if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !free_.empty(); }))
+      throw std::runtime_error("LocalLink: send timed out (peer stalled)");
+    if (aborted_) throw std::runtime_error("LocalLink: aborted");
+    slot = free_.front();
+    free_.pop_front();
+    wait_freed = freed_valid_[slot];
+  }
+  if (wait_freed) HIP_OK(hipStreamWaitEvent(st, freed_[slot], 0));
+  HIP_OK(hipMemcpyAsync(slots_[slot], buf, bytes, hipMemcpyDefault, st));
+  HIP_OK(hipEventRecord(ready_[slot], st));
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    q_.push_back({slot, bytes});
+    bytes_sent += bytes;
+    ++msgs_sent;
+  }
+  cv_.notify_all();
+}
+
+void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
+  Msg m;
+  {
+    std::unique_lock<std::mutex> l(mu_);
+    if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !q_.empty(); }))
+      throw std::runtime_error("LocalLink: recv timed out (peer stalled)");
+    if (aborted_) throw std::runtime_error("LocalLink: aborted");
+    m = q_.front();
+    q_.pop_front();
+  }
+  if (m.bytes != bytes) throw std::runtime_error("LocalLink: message size mismatch");
+  HIP_OK(hipStreamWaitEvent(st, ready_[m.slot], 0));
+  HIP_OK(hipMemcpyAsync(buf, slots_[m.slot], bytes, hipMemcpyDefault, st));
+  HIP_OK(hipEventRecord(freed_[m.slot], st));
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    freed_valid_[m.slot] = true;
+    free_.push_back(m.slot);
+  }
+  cv_.notify_all();
+}
+
+// ---------------------------------------------------------------- RCCL
+RcclLink::RcclLink(void* comm, int my_rank, int device) : comm_(comm), rank_(my_rank), dev_(device) {}
+RcclLink::~RcclLink() {
+  if (comm_) ncclCommDestroy((ncclComm_t)comm_);
+}
+void RcclLink::abort() {
+  if (comm_) { ncclCommAbort((ncclComm_t)comm_); comm_ = nullptr; }
+}
+void RcclLink::send(const void* buf, size_t bytes, hipStream_t st) {
+  if (rank_ != 0) throw std::runtime_error("RcclLink: receiver end cannot send");
+  NCCL_OK(ncclSend(buf, bytes, ncclUint8, 1, (ncclComm_t)comm_, st));
+  bytes_sent += bytes;
+  ++msgs_sent;
+}
+void RcclLink::recv(void* buf, size_t bytes, hipStream_t st) {
+  if (rank_ != 1) throw std::runtime_error("RcclLink: sender end cannot recv");
+  NCCL_OK(ncclRecv(buf, bytes, ncclUint8, 0, (ncclComm_t)comm_, st));
+}
+
+void rccl_make_pair(int dev_a, int dev_b, void** comm_a, void** comm_b) {
+  ncclComm_t comms[2];
+  int devs[2] = {dev_a, dev_b};
+  NCCL_OK(ncclCommInitAll(comms, 2, devs));
+  *comm_a = comms[0];
+  *comm_b = comms[1];
+}
+
+void* rccl_init_rank(const uint8_t* id128, int rank, int device) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  std::memcpy(&id, id128, 128);
+  HIP_OK(hipSetDevice(device));
+  ncclComm_t c;
+  NCCL_OK(ncclCommInitRank(&c, 2, id, rank));
+  return c;
+}
+
+int rccl_unique_id(uint8_t* out128) {
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, 128);
+  return 0;
+}
+
+// ---------------------------------------------------------------- TCP
+static void full_write(int fd, const void* p, size_t n) {
+  const char* c = (const char*)p;
+  while (n) {
+    ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (w <= 0) throw std::runtime_error("TcpLink: send failed");
+    c += w;
+    n -= (size_t)w;
+  }
+}
+static void full_read(int fd, void* p, size_t n) {
+  char* c = (char*)p;
+  while (n) {
+    ssize_t r = ::recv(fd, c, n, 0);
+    if (r <= 0) throw std::runtime_error("TcpLink: peer closed");
+    c += r;
+    n -= (size_t)r;
+  }
+}
+static void tune(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  int buf = 16 << 20;   // PDF p.4-5 sysctl advice, applied per socket
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof(buf));
+  setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof(buf));
+}
+
+std::unique_ptr<TcpLink> TcpLink::make_sender(const std::string& host, int port, double timeout_s) {
+  auto l = std::unique_ptr<TcpLink>(new TcpLink());
+  const auto t0 = std::chrono::steady_clock::now();
+  while (true) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) == 0 && res) {
+      int fd = socket(res->ai_family, res->ai_socktype, 0);
+      if (fd >= 0 && connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+        freeaddrinfo(res);
+        tune(fd);
+        l->fd_ = fd;
+        return l;
+      }
+      if (fd >= 0) ::close(fd);
+      freeaddrinfo(res);
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      throw std::runtime_error("TcpLink: connect timeout to " + host + ":" + std::to_string(port));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+}
+
+std::unique_ptr<TcpLink> TcpLink::make_receiver(int port, double timeout_s) {
+  auto l = std::unique_ptr<TcpLink>(new TcpLink());
+  int ls = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_ANY);
+  a.sin_port = htons((uint16_t)port);
+  if (bind(ls, (sockaddr*)&a, sizeof(a)) != 0 || listen(ls, 1) != 0) {
+    ::close(ls);
+    throw std::runtime_error("TcpLink: cannot listen on port " + std::to_string(port));
+  }
+  timeval tv{(long)timeout_s, 0};
+  setsockopt(ls, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  int fd = accept(ls, nullptr, nullptr);
+  ::close(ls);
+  if (fd < 0) throw std::runtime_error("TcpLink: accept timeout");
+  tune(fd);
+  l->fd_ = fd;
+  return l;
+}
+
+TcpLink::~TcpLink() {
+  if (fd_ >= 0) ::close(fd_);
+}
+void TcpLink::abort() {
+  if (fd_ >= 0) { shutdown(fd_, SHUT_RDWR); }
+}
+
+void TcpLink::send(const void* buf, size_t bytes, hipStream_t st) {
+  const void* src = buf;
+  if (st) {
+    staging_.resize(bytes);
+    HIP_OK(hipMemcpyAsync(staging_.data(), buf, bytes, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    src = staging_.data();
+  }
+  const uint64_t n = bytes;
+  full_write(fd_, &n, 8);
+  full_write(fd_, src, bytes);
+  bytes_sent += bytes;
+  ++msgs_sent;
+}
+
+void TcpLink::recv(void* buf, size_t bytes, hipStream_t st) {
+  uint64_t n = 0;
+  full_read(fd_, &n, 8);
+  if (n != bytes) throw std::runtime_error("TcpLink: message size mismatch");
+  if (st) {
+    staging_.resize(bytes);
+    full_read(fd_, staging_.data(), bytes);
+    HIP_OK(hipMemcpyAsync(buf, staging_.data(), bytes, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+  } else {
+    full_read(fd_, buf, bytes);
+  }
+}
+
+}  // namespace mp

@@ -1,0 +1,99 @@
+// Stage-to-stage transports (E8 of SURVEY.md §2.2): the reference ships activations between
+// llama.cpp rpc-servers through the client over TCP (ggml-rpc, `main.rs:47-48`).  Here a Link is
+// one DIRECTION between two stages; every op is stream-ordered (enqueued, not blocking the GPU
+// of the caller), so comm overlaps the compute of other micro-batches.
+//   - RcclLink:  ncclSend/ncclRecv on a 2-rank communicator per link (xGMI peer-to-peer).
+//   - LocalLink: same-process hand-off through a ring of device slots + HIP events (1-GPU
+//                emulation of PP=S, or in-process multi-GPU without RCCL).
+//   - TcpLink:   host sockets (cross-host parity with the reference's worker-over-TCP mode).
+// One communicator per direction and one stream per side make every link FIFO-consistent, so
+// the piped ring (activations forward, sampled tokens last -> first) is deadlock-free.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace mp {
+
+class Link {
+ public:
+  virtual ~Link() = default;
+  // host pointers allowed when stream == nullptr (CPU stages)
+  virtual void send(const void* buf, size_t bytes, hipStream_t st) = 0;
+  virtual void recv(void* buf, size_t bytes, hipStream_t st) = 0;
+  virtual const char* kind() const = 0;
+  virtual void abort() {}
+  uint64_t bytes_sent = 0, msgs_sent = 0;
+};
+
+// ---------------------------------------------------------------- LocalLink
+class LocalLink : public Link {
+ public:
+  // slots live on `dst_device`; both sides may be on the same device.
+  LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_slots);
+  ~LocalLink() override;
+  void send(const void* buf, size_t bytes, hipStream_t st) override;
+  void recv(void* buf, size_t bytes, hipStream_t st) override;
+  const char* kind() const override { return "local"; }
+  void abort() override;
+
+ private:
+  struct Msg { int slot; size_t bytes; };
+  int src_dev_, dst_dev_;
+  size_t slot_bytes_;
+  std::vector<void*> slots_;
+  std::vector<hipEvent_t> ready_, freed_;   // per slot
+  std::vector<bool> freed_valid_;
+  std::deque<int> free_;
+  std::deque<Msg> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool aborted_ = false;
+};
+
+// ---------------------------------------------------------------- RcclLink
+struct RcclComm;  // opaque (ncclComm_t)
+class RcclLink : public Link {
+ public:
+  // rank 0 = sender, rank 1 = receiver of this direction
+  RcclLink(void* nccl_comm, int my_rank, int device);
+  ~RcclLink() override;
+  void send(const void* buf, size_t bytes, hipStream_t st) override;
+  void recv(void* buf, size_t bytes, hipStream_t st) override;
+  const char* kind() const override { return "rccl"; }
+  void abort() override;
+
+ private:
+  void* comm_;
+  int rank_, dev_;
+};
+
+// creates the two ends of a link between devices a -> b inside one process (ncclCommInitAll)
+void rccl_make_pair(int dev_a, int dev_b, void** comm_a, void** comm_b);
+// multi-process: init this rank's end from a 128-byte unique id (rank 0 = sender)
+void* rccl_init_rank(const uint8_t* id128, int rank, int device);
+int rccl_unique_id(uint8_t* out128);
+
+// ---------------------------------------------------------------- TcpLink
+class TcpLink : public Link {
+ public:
+  // sender connects to host:port; receiver listens on port (accepts one connection)
+  static std::unique_ptr<TcpLink> make_sender(const std::string& host, int port, double timeout_s = 60);
+  static std::unique_ptr<TcpLink> make_receiver(int port, double timeout_s = 60);
+  ~TcpLink() override;
+  void send(const void* buf, size_t bytes, hipStream_t st) override;
+  void recv(void* buf, size_t bytes, hipStream_t st) override;
+  const char* kind() const override { return "tcp"; }
+  void abort() override;
+
+ private:
+  int fd_ = -1;
+  std::vector<char> staging_;
+};
+
+}  // namespace mp

@@ -1,0 +1,87 @@
+"""Python front-end of the native pipeline engine (csrc/runtime/engine.cpp).
+
+    eng = Engine(gguf="model.gguf", stages=2, n_mb=2, mb_size=4, max_ctx=2048)
+    out, stats = eng.generate([[1, 15, 27], [1, 99]], n_predict=32)
+
+Config keys mirror the C++ Engine (see engine.h): gguf | synthetic+ftype, mode ("local" or "mp"),
+stages, devices, link ("local" | "rccl"), n_mb, mb_size, max_ctx, prefill_chunk, split
+("even" | "mem" | "cost"), graphs, attn_split_len, verbose, log_file.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+
+import numpy as np
+
+from . import _native as N
+
+
+class Engine:
+    def __init__(self, **cfg):
+        self.cfg = dict(cfg)
+        L = N.lib()
+        h = L.mp_engine_create(N.cstr(json.dumps(self.cfg)))
+        if not h:
+            N.check(None, "engine create")
+        self._h = ctypes.c_void_p(h)
+        self.info = N.jcall(L.mp_engine_info, self._h, what="engine info")
+        self.n_seq_cap = self.info["n_mb"] * self.info["mb_size"]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().mp_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def _flat(prompts):
+        lens = np.asarray([len(p) for p in prompts], np.int32)
+        flat = np.asarray([t for p in prompts for t in p], np.int32)
+        return flat, lens
+
+    def generate(self, prompts, n_predict: int):
+        flat, lens = self._flat(prompts)
+        out = np.full((len(prompts), n_predict), -1, np.int32)
+        stats = N.jcall(N.lib().mp_engine_generate, self._h, flat.ctypes.data, lens.ctypes.data, len(prompts),
+                        n_predict, out.ctypes.data, what="generate")
+        return out.tolist(), stats
+
+    def start(self, prompts):
+        flat, lens = self._flat(prompts)
+        self._n_seq = len(prompts)
+        N.check(N.lib().mp_engine_start(self._h, flat.ctypes.data, lens.ctypes.data, len(prompts)), "start")
+
+    def decode(self, k: int):
+        return N.jcall(N.lib().mp_engine_decode, self._h, k, what="decode")
+
+    def tokens(self, cap: int = 4096):
+        out = np.full((self._n_seq, cap), -1, np.int32)
+        n = N.check(N.lib().mp_engine_tokens(self._h, out.ctypes.data, self._n_seq, cap), "tokens")
+        return out[:, :n].tolist()
+
+    def bench(self, prompt_len: int, warmup: int, steps: int):
+        return N.jcall(N.lib().mp_engine_bench, self._h, prompt_len, warmup, steps, what="bench")
+
+    def logits(self, rows: int = 1, vocab: int | None = None):
+        vocab = vocab or self.info["model"]["vocab"]
+        out = np.zeros((rows, vocab), np.float32)
+        N.check(N.lib().mp_engine_logits(self._h, 0, out.ctypes.data, rows), "logits")
+        return out
+
+
+def rccl_unique_id_hex() -> str:
+    buf = (ctypes.c_uint8 * 128)()
+    N.check(N.lib().mp_rccl_unique_id(buf), "rccl unique id")
+    return bytes(buf).hex()

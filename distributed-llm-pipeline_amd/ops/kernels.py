@@ -1,0 +1,142 @@
+"""Thin torch wrappers over the HIP kernels (used by the T1 kernel tests and tools).
+
+Every op launches the hand-written gfx950 kernel on torch's current HIP stream.  There is no
+PyTorch fallback: if `libmipipe.so` is missing the import of the library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..utils import quants as Q
+
+EPI_STORE, EPI_ATOMIC, EPI_SWIGLU = 0, 1, 2
+P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0 = 0, 1, 2, 3, 4, 5
+
+
+def _ptr(t: torch.Tensor | None):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def pack_type(ggml_type: int) -> int:
+    return N.lib().mp_pack_type(ggml_type)
+
+
+def packed_dims(ggml_type: int, n: int, k: int):
+    n_pad = (n + 15) // 16 * 16
+    k_pad = (k + 255) // 256 * 256
+    return n_pad, k_pad, n_pad // 16, k_pad // 256
+
+
+def pack_t16(raw: np.ndarray, ggml_type: int, n: int, k: int, gateup: bool = False) -> np.ndarray:
+    """Pack a GGUF-native [n][k] tensor (bytes) into the T16 device layout (host, C++ packer)."""
+    raw = np.ascontiguousarray(raw, dtype=np.uint8)
+    nbytes = N.lib().mp_packed_bytes(ggml_type, n, k)
+    out = np.empty(nbytes, np.uint8)
+    rb = Q.row_bytes(ggml_type, k)
+    N.check(N.lib().mp_pack_t16(ggml_type, n, k, raw.ctypes.data, rb, out.ctypes.data, int(gateup)), "pack_t16")
+    return out
+
+
+class PackedWeight:
+    """A T16-packed weight resident on the GPU."""
+
+    def __init__(self, raw: np.ndarray, ggml_type: int, n: int, k: int, device="cuda", gateup=False):
+        self.ggml_type, self.n, self.k = ggml_type, n, k
+        self.ptype = pack_type(ggml_type)
+        self.n_pad, self.k_pad, self.ntiles, self.nsb = packed_dims(ggml_type, n, k)
+        self.host = pack_t16(raw, ggml_type, n, k, gateup)
+        self.dev = torch.from_numpy(self.host).to(device)
+
+    def unpack(self) -> torch.Tensor:
+        out = torch.zeros(self.n_pad, self.k_pad, dtype=torch.float16, device=self.dev.device)
+        N.check(N.lib().mp_op_unpack(self.ptype, _ptr(self.dev), self.ntiles, self.nsb, _ptr(out), self.k_pad,
+                                     _stream()), "unpack")
+        return out[: self.n, : self.k]
+
+
+def gemv(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor | None = None,
+         nsplit: int = 1, n_valid: int | None = None) -> torch.Tensor:
+    """x: f16 [M][K_pad] (zero tail). Returns f32 [M][n] (STORE/ATOMIC) or f16 [M][n/2] (SWIGLU)."""
+    assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
+    M = x.shape[0]
+    if epi == EPI_SWIGLU:
+        F = w.n // 2
+        h = torch.zeros(M, F, dtype=torch.float16, device=x.device) if y is None else y
+        N.check(N.lib().mp_op_gemv(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, None, 0,
+                                   _ptr(h), h.stride(0), F if n_valid is None else n_valid, 1, _stream()), "gemv")
+        return h
+    if y is None:
+        y = torch.zeros(M, w.n, dtype=torch.float32, device=x.device)
+    N.check(N.lib().mp_op_gemv(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
+                               y.stride(0), None, 0, w.n if n_valid is None else n_valid, nsplit, _stream()),
+            "gemv")
+    return y
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, k_pad: int | None = None) -> torch.Tensor:
+    M, d = x.shape
+    k_pad = k_pad or (d + 255) // 256 * 256
+    out = torch.zeros(M, k_pad, dtype=torch.float16, device=x.device)
+    N.check(N.lib().mp_op_rmsnorm(_ptr(x), x.stride(0), _ptr(w), d, eps, _ptr(out), k_pad, M, _stream()), "rmsnorm")
+    return out
+
+
+def embed(raw_table: torch.Tensor, ggml_type: int, d: int, tokens: torch.Tensor) -> torch.Tensor:
+    M = tokens.numel()
+    x = torch.empty(M, d, dtype=torch.float32, device=tokens.device)
+    rb = Q.row_bytes(ggml_type, d)
+    N.check(N.lib().mp_op_embed(ggml_type, _ptr(raw_table), rb, d, _ptr(tokens), M, _ptr(x), d, _stream()), "embed")
+    return x
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    M, n = logits.shape
+    out = torch.empty(M, dtype=torch.int32, device=logits.device)
+    N.check(N.lib().mp_op_argmax(_ptr(logits), logits.stride(0), n, M, _ptr(out), _stream()), "argmax")
+    return out
+
+
+def sample(logits: torch.Tensor, temp: float, top_k: int = 0, top_p: float = 1.0, min_p: float = 0.0,
+           seed: int = 0, step: torch.Tensor | None = None) -> torch.Tensor:
+    M, n = logits.shape
+    out = torch.empty(M, dtype=torch.int32, device=logits.device)
+    N.check(N.lib().mp_op_sample(_ptr(logits), logits.stride(0), n, M, temp, top_k, top_p, min_p, seed, _ptr(step),
+                                 _ptr(out), _stream()), "sample")
+    return out
+
+
+def rope_cs_table(max_pos: int, hd: int, base: float, freq_factors=None) -> torch.Tensor:
+    inv = base ** (-np.arange(0, hd, 2, dtype=np.float64) / hd)
+    if freq_factors is not None:
+        inv = inv / np.asarray(freq_factors, np.float64)
+    ang = np.outer(np.arange(max_pos, dtype=np.float64), inv)
+    cs = np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)   # [pos][hd/2][2]
+    return torch.from_numpy(cs)
+
+
+def rope_kv(qkv, pos, slot, block_table, rope_cs, Hq, Hkv, hd, Dp, q_scale, k_cache, v_cache):
+    M = qkv.shape[0]
+    q_out = torch.zeros(M, Hq, Dp, dtype=torch.float16, device=qkv.device)
+    N.check(N.lib().mp_op_rope_kv(_ptr(qkv), qkv.stride(0), M, Hq, Hkv, hd, Dp, _ptr(pos), _ptr(slot),
+                                  _ptr(block_table), block_table.shape[1], _ptr(rope_cs), q_scale, _ptr(q_out),
+                                  _ptr(k_cache), _ptr(v_cache), _stream()), "rope_kv")
+    return q_out
+
+
+def attention(q, kvlen, slot, block_table, k_cache, v_cache, Hkv, hd, tq=1, split_len=256, n_split=1):
+    M, Hq, Dp = q.shape
+    out = torch.zeros(M, Hq * hd, dtype=torch.float16, device=q.device)
+    o_part = torch.zeros(max(n_split, 1), M * Hq, Dp, dtype=torch.float32, device=q.device)
+    ml_part = torch.zeros(max(n_split, 1), M * Hq, 2, dtype=torch.float32, device=q.device)
+    N.check(N.lib().mp_op_attention(_ptr(q), _ptr(kvlen), _ptr(slot), _ptr(block_table), block_table.shape[1],
+                                    _ptr(k_cache), _ptr(v_cache), M, Hq, Hkv, hd, Dp, tq, split_len, n_split,
+                                    _ptr(o_part), _ptr(ml_part), _ptr(out), out.stride(0), _stream()), "attention")
+    return out

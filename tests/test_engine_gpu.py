@@ -1,0 +1,91 @@
+"""T2/T3 model-level tests on one MI355X: engine vs the pure-torch fp32 oracle, hipGraph vs eager,
+pipeline emulation (PP=2/3 stages on one GPU with LocalLink) vs PP=1, micro-batch invariance."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import make_model
+
+pytestmark = pytest.mark.gpu
+
+
+def nmse(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(((a - b) ** 2).sum() / ((b ** 2).sum() + 1e-30))
+
+
+@pytest.mark.parametrize("name,ftype", [("stories15m", "F32"), ("tiny-gqa", "Q8_0"), ("tiny-gqa", "Q4_K_M"),
+                                        ("tiny-l3", "Q6_K"), ("tiny-gqa", "Q5_K_M"), ("tiny-gqa", "BF16")])
+def test_engine_matches_reference(cuda, native, model_dir, name, ftype):
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, name, ftype)
+    ref = RefLlama.from_gguf(path)
+    rng = np.random.default_rng(0)
+    prompt = [int(t) for t in rng.integers(3, cfg.vocab, 37)]
+    with Engine(gguf=path, max_ctx=256, prefill_chunk=16, graphs=True) as eng:
+        eng.start([prompt])
+        lg = eng.logits()[0]
+        ref.reset()
+        rl = ref.forward(prompt, 0)[-1].numpy()
+        assert nmse(lg, rl) < 2e-4, nmse(lg, rl)
+        pos = len(prompt)
+        for step in range(6):
+            tok = eng.tokens()[0][-1]
+            rtop = np.sort(rl)[-2:]
+            if rl.argmax() != tok:   # allowed only on a near-tie
+                assert rl.max() - rl[tok] < 1e-2 * (abs(rtop).max() + 1), (step, tok, rl.argmax())
+            eng.decode(1)
+            lg = eng.logits()[0]
+            rl = ref.forward([tok], pos)[-1].numpy()
+            pos += 1
+            assert nmse(lg, rl) < 2e-4, (step, nmse(lg, rl))
+
+
+def test_graph_equals_eager(cuda, native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    prompts = [[5, 6, 7, 8, 9], [100, 200, 300]]
+    outs = []
+    for graphs in (False, True):
+        with Engine(gguf=path, max_ctx=256, n_mb=1, mb_size=2, graphs=graphs) as eng:
+            out, _ = eng.generate(prompts, 12)
+            outs.append(out)
+    assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("stages", [2, 3])
+def test_pipeline_emulation_matches_pp1(cuda, native, model_dir, stages):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(1)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 40, 3, 17)]
+    with Engine(gguf=path, max_ctx=256, n_mb=2, mb_size=2, prefill_chunk=16) as eng:
+        ref_out, _ = eng.generate(prompts, 10)
+    with Engine(gguf=path, max_ctx=256, n_mb=2, mb_size=2, prefill_chunk=16, stages=stages,
+                devices=[0] * stages, link="local", split="even") as eng:
+        assert len(eng.info["stages"]) == stages
+        out, st = eng.generate(prompts, 10)
+    assert out == ref_out
+
+
+def test_microbatch_invariance(cuda, native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts = [[11, 12, 13], [400, 5, 6, 7, 8, 9, 10], [42]]
+    singles = []
+    with Engine(gguf=path, max_ctx=128) as eng:
+        for p in prompts:
+            o, _ = eng.generate([p], 8)
+            singles.append(o[0])
+    with Engine(gguf=path, max_ctx=128, n_mb=2, mb_size=2) as eng:
+        o, _ = eng.generate(prompts, 8)
+    assert o == singles
+
+
+def test_synthetic_engine_runs(cuda, native):
+    from mipipe.engine import Engine
+    syn = dict(n_layer=2, d_model=1024, n_head=8, n_head_kv=2, d_ff=2816, vocab=4096)
+    with Engine(synthetic=syn, ftype="Q4_K_M", max_ctx=256, n_mb=2, mb_size=4) as eng:
+        r = eng.bench(prompt_len=32, warmup=2, steps=8)
+    assert r["decode_tok_s"] > 0 and r["p50_ms"] > 0
