@@ -14,6 +14,7 @@
 #include "kernels_api.h"
 #include "log.h"
 #include "pack.h"
+#include "tokenizer.h"
 
 using namespace mp;
 
@@ -236,6 +237,54 @@ int mp_op_sample(const void* logits, int ld, int n, int M, float temp, int top_k
   HIP_OK(hipGetLastError());
   return 0;
   API_CATCH(-1)
+}
+
+// ------------------------------------------------------------------ tokenizer
+void* mp_tok_open(const char* gguf_path) {
+  API_TRY
+  GgufFile f(gguf_path);
+  return new Tokenizer(Tokenizer::from_gguf(f));
+  API_CATCH(nullptr)
+}
+void mp_tok_close(void* h) { delete static_cast<Tokenizer*>(h); }
+int mp_tok_encode(void* h, const char* text, int add_bos, int parse_special, int32_t* out, int cap) {
+  API_TRY
+  auto ids = static_cast<Tokenizer*>(h)->encode(text, add_bos != 0, parse_special != 0);
+  const int n = (int)ids.size();
+  for (int i = 0; i < n && i < cap; ++i) out[i] = ids[i];
+  return n;
+  API_CATCH(-1)
+}
+int mp_tok_piece(void* h, int32_t id, char* buf, int cap) {
+  API_TRY
+  const std::string s = static_cast<Tokenizer*>(h)->piece(id);
+  const int n = (int)s.size();
+  if (n <= cap) std::memcpy(buf, s.data(), n);
+  return n;
+  API_CATCH(-1)
+}
+int mp_tok_decode(void* h, const int32_t* ids, int n, char* buf, int cap) {
+  API_TRY
+  const std::string s = static_cast<Tokenizer*>(h)->decode(std::vector<int32_t>(ids, ids + n));
+  const int len = (int)s.size();
+  if (len <= cap) std::memcpy(buf, s.data(), len);
+  return len;
+  API_CATCH(-1)
+}
+int mp_tok_info(void* h, int32_t* out) {  // vocab, bos, eos, eot
+  API_TRY
+  auto* t = static_cast<Tokenizer*>(h);
+  out[0] = t->n_vocab(); out[1] = t->bos(); out[2] = t->eos(); out[3] = t->eot();
+  return 0;
+  API_CATCH(-1)
+}
+// pre-tokenizer split (tests): returns pieces joined by '\x1f'
+const char* mp_tok_pretokenize(const char* text) {
+  API_TRY
+  g_str.clear();
+  for (auto& p : Tokenizer::llama3_pretokenize(text)) { g_str += p; g_str += '\x1f'; }
+  return g_str.c_str();
+  API_CATCH(nullptr)
 }
 
 // ------------------------------------------------------------------ engine
