@@ -18,65 +18,88 @@
 
 namespace mpk {
 
-template <int PT, int EPI>
-__global__ __launch_bounds__(256) void gemv_kernel(const mp::GemvParams p) {
+template <int PT, int EPI, int WPB, int TPW, int NSLOT>
+__global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) {
+  // TPW tiles per wave share every x fragment (x traffic / weight traffic = 3.5 / TPW at M = 16);
+  // NSLOT super-blocks per tile are kept in flight in a compile-time indexed register ring.
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x * 4 + wave;
-  if (tile >= p.ntiles) return;
+  const int tile0 = (blockIdx.x * WPB + wave) * TPW;
+  if (tile0 >= p.ntiles) return;
   const int sb0 = blockIdx.y * p.sb_per_split;
   const int sb1 = min(sb0 + p.sb_per_split, p.nsb);
   if (sb0 >= sb1) return;
   const int g = lane >> 4, r = lane & 15;
-  const uint8_t* wp = p.W + ((size_t)tile * p.nsb + sb0) * CB;
-  const bool xv = r < p.M;
-  const f16* xp = p.X + (size_t)(xv ? r : 0) * p.ldx + 8 * g;
+  const uint8_t* wt[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) wt[t] = p.W + (size_t)min(tile0 + t, p.ntiles - 1) * p.nsb * CB;
+  // rows m >= M read row M-1 (clamped address, no exec masking); their outputs are never stored
+  const f16* xp = p.X + (size_t)min(r, p.M - 1) * p.ldx + 8 * g;
 
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  typename D::Raw cur, nxt;
-  D::load(cur, wp, lane);
-  for (int sb = sb0; sb < sb1; ++sb) {
-    if (sb + 1 < sb1) D::load(nxt, wp + CB, lane);
-    half8_t a[8];
+  f32x4 acc[TPW];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      half8_t z = {};
-      a[t] = xv ? *reinterpret_cast<const half8_t*>(xp + (size_t)sb * 256 + 32 * t) : z;
+  for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int last = sb1 - 1;
+  typename D::Raw ring[NSLOT][TPW];
+#pragma unroll
+  for (int sl = 0; sl < NSLOT; ++sl)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)min(sb0 + sl, last) * CB, lane);
+
+  for (int sb = sb0; sb < sb1; sb += NSLOT) {
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) {
+      const int cur = sb + sl;
+      if (cur < sb1) {
+        half8_t a[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          half8_t b[4];
+          D::template dequant<0>(ring[sl][t], b, lane);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(a[s], b[s], acc[t]);
+          D::template dequant<1>(ring[sl][t], b, lane);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(a[4 + s], b[s], acc[t]);
+        }
+        if (cur + NSLOT < sb1) {
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)(cur + NSLOT) * CB, lane);
+        }
+      }
     }
-    half8_t b[4];
-    D::template dequant<0>(cur, b, lane);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[s], b[s], acc);
-    D::template dequant<1>(cur, b, lane);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[4 + s], b[s], acc);
-    cur = nxt;
-    wp += CB;
   }
 
   // lane holds C[m = 4g + i][n = 16*tile + r]
-  if constexpr (EPI == mp::EPI_SWIGLU) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float other = __shfl_xor(acc[i], 8);
-      const int m = 4 * g + i;
-      if (r < 8 && m < p.M) {
-        const int o = tile * 8 + r;
-        if (o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[i]) * other);
-      }
-    }
-  } else {
-    const int n = tile * 16 + r;
-    if (n < p.n_valid) {
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = tile0 + t;
+    if (tile >= p.ntiles) break;
+    if constexpr (EPI == mp::EPI_SWIGLU) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        const float other = __shfl_xor(acc[t][i], 8);
         const int m = 4 * g + i;
-        if (m < p.M) {
-          float* dst = p.Y + (size_t)m * p.ldy + n;
-          if constexpr (EPI == mp::EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i]);
-          else *dst = acc[i];
+        if (r < 8 && m < p.M) {
+          const int o = tile * 8 + r;
+          if (o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[t][i]) * other);
+        }
+      }
+    } else {
+      const int n = tile * 16 + r;
+      if (n < p.n_valid) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 4 * g + i;
+          if (m < p.M) {
+            float* dst = p.Y + (size_t)m * p.ldy + n;
+            if constexpr (EPI == mp::EPI_ATOMIC) unsafeAtomicAdd(dst, acc[t][i]);
+            else *dst = acc[t][i];
+          }
         }
       }
     }
@@ -110,15 +133,46 @@ __global__ __launch_bounds__(64) void unpack_kernel(const uint8_t* W, int nsb, f
 
 namespace mp {
 
-template <int PT>
-static void launch_pt(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
-  dim3 grid((p.ntiles + 3) / 4, nsplit);
+static int g_wpb = 1;   // waves per workgroup (tuning knob, MP_GEMV_WPB)
+static int g_tpw = 0;   // tiles per wave: 0 = auto (1 for M <= 4, else 2)
+
+template <int PT, int WPB, int TPW, int NSLOT>
+static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  const int waves = (p.ntiles + TPW - 1) / TPW;
+  dim3 grid((waves + WPB - 1) / WPB, nsplit);
+  dim3 block(WPB * 64);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE>), grid, dim3(256), 0, st, p); break;
-    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC>), grid, dim3(256), 0, st, p); break;
-    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU>), grid, dim3(256), 0, st, p); break;
+    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
   }
 }
+
+// Tiles per wave: with M > 4 the x fragments (16 rows x 32 k per MFMA) cost more L1/L2 traffic
+// than the weights themselves (3.5x at M = 16); sharing them across tiles pays.  Measured on
+// MI355X (tools/gemv_bench.py, 70B shapes): M = 16 gate/up 115 -> 67 us with 4 tiles per wave.
+int gemv_tiles_per_wave(int M, int epi) {
+  if (g_tpw) return g_tpw;
+  if (M <= 4) return 1;
+  return epi == EPI_ATOMIC ? 2 : 4;
+}
+
+template <int PT>
+static void launch_pt(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  const int tpw = gemv_tiles_per_wave(p.M, epi);
+  if (tpw == 1) {
+    if (g_wpb == 2) launch_cfg<PT, 2, 1, 4>(epi, p, nsplit, st);
+    else launch_cfg<PT, 1, 1, 4>(epi, p, nsplit, st);
+  } else if (tpw == 2) {
+    if (g_wpb == 2) launch_cfg<PT, 2, 2, 2>(epi, p, nsplit, st);
+    else launch_cfg<PT, 1, 2, 2>(epi, p, nsplit, st);
+  } else {
+    launch_cfg<PT, 1, 4, 2>(epi, p, nsplit, st);
+  }
+}
+
+void set_gemv_wpb(int w) { g_wpb = (w == 1 || w == 2) ? w : 1; }
+void set_gemv_tpw(int t) { g_tpw = (t == 1 || t == 2 || t == 4) ? t : 0; }
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   if (nsplit < 1) nsplit = 1;

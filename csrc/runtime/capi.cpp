@@ -162,6 +162,17 @@ int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const voi
   API_CATCH(-1)
 }
 
+void mp_set_gemv_wpb(int w) { set_gemv_wpb(w); }
+void mp_set_gemv_tpw(int t) { set_gemv_tpw(t); }
+
+int mp_init_packed(void* W, size_t nbytes, int ptype, float scale, uint64_t seed, void* stream) {
+  API_TRY
+  launch_init_packed((uint8_t*)W, nbytes, ptype, scale, seed, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_unpack(int ptype, const void* W, int ntiles, int nsb, void* out, int ldo, void* stream) {
   API_TRY
   launch_unpack(ptype, (const uint8_t*)W, ntiles, nsb, (f16*)out, ldo, (hipStream_t)stream);

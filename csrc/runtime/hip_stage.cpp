@@ -343,11 +343,7 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     p.ntiles = (int)m.dims.ntiles;
     p.nsb = (int)m.dims.nsb;
     p.n_valid = n_valid;
-    int nsplit = 1;
-    if (allow_split && epi == EPI_ATOMIC) {
-      nsplit = (int)std::min<int64_t>((2048 + p.ntiles - 1) / p.ntiles, std::max<int64_t>(1, p.nsb / 2));
-      nsplit = std::max(1, nsplit);
-    }
+    const int nsplit = allow_split ? gemv_auto_split(p.ntiles, p.nsb, p.M, epi) : 1;
     launch_gemv(m.ptype, epi, p, nsplit, st);
   }
 }

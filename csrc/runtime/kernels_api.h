@@ -25,6 +25,17 @@ struct GemvParams {
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
+void set_gemv_wpb(int waves_per_block);   // 1 or 2 (tuning knob)
+void set_gemv_tpw(int tiles_per_wave);    // 0 = auto, 1, 2, 4 (tuning knob)
+int gemv_tiles_per_wave(int M, int epi);
+// split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)
+inline int gemv_auto_split(int ntiles, int nsb, int M, int epi, int target_waves = 2048) {
+  if (epi != EPI_ATOMIC) return 1;
+  const int waves = (ntiles + gemv_tiles_per_wave(M, epi) - 1) / gemv_tiles_per_wave(M, epi);
+  int s = (target_waves + waves - 1) / waves;
+  const int smax = nsb / 4 > 1 ? nsb / 4 : 1;
+  return s < 1 ? 1 : (s > smax ? smax : s);
+}
 void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, int ldo, hipStream_t st);
 
 // Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.

@@ -68,6 +68,10 @@ _SIGS = {
     "mp_engine_tokens": ([c_void_p, c_void_p, c_int, c_int], c_int),
     "mp_engine_logits": ([c_void_p, c_int, c_void_p, c_int], c_int),
     "mp_rccl_unique_id": ([c_void_p], c_int),
+    "mp_set_gemv_wpb": ([c_int], None),
+    "mp_set_gemv_tpw": ([c_int], None),
+    "mp_init_packed": ([c_void_p, ctypes.c_size_t, c_int, c_float, ctypes.c_uint64, c_void_p], c_int),
+    "mp_tok_pretokenize": ([c_char_p], c_char_p),
 }
 
 
