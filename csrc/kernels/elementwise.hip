@@ -25,31 +25,47 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, int ldx, c
                                                       int64_t zero_n, int M) {
   __shared__ float red[4];
   const int row = blockIdx.x;
-  const float* xr = x + (size_t)row * ldx;
-  float ss = 0.f;
-  const int d4 = d & ~3;
-  for (int i = threadIdx.x * 4; i < d4; i += 1024) {
-    float4 v = *reinterpret_cast<const float4*>(xr + i);
-    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  if (zero) {   // every block clears a 4096-float slice of the split-K accumulator (float4 stores)
+    const int64_t z0 = (int64_t)blockIdx.x * 4096, z1 = min(zero_n, z0 + 4096);
+    for (int64_t i = z0 + threadIdx.x * 4; i < z1; i += 1024) {
+      if (i + 4 <= z1) *reinterpret_cast<float4*>(zero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      else for (int64_t k = i; k < z1; ++k) zero[k] = 0.f;
+    }
   }
-  for (int i = d4 + threadIdx.x; i < d; i += 256) ss += xr[i] * xr[i];
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * ldx;
+  f16* o = out + (size_t)row * ldo;
+  const int d4 = d & ~3;
+  if (d4 == d && d <= 8 * 1024) {
+    // single pass: the row (<= 8192 floats) stays in registers between the sum and the scale
+    float4 v[8];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = (threadIdx.x + 256 * k) * 4;
+      v[k] = i < d ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    }
+    ss = block_sum_256(ss, red);
+    const float sc = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = (threadIdx.x + 256 * k) * 4;
+      if (i < d) {
+        const float4 ww = *reinterpret_cast<const float4*>(w + i);
+        half2_t a = {(f16)(v[k].x * sc * ww.x), (f16)(v[k].y * sc * ww.y)};
+        half2_t b = {(f16)(v[k].z * sc * ww.z), (f16)(v[k].w * sc * ww.w)};
+        u32x2 pk = {as_u32(a), as_u32(b)};
+        *reinterpret_cast<u32x2*>(o + i) = pk;
+      }
+    }
+    return;
+  }
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < d; i += 256) ss += xr[i] * xr[i];
   ss = block_sum_256(ss, red);
   const float sc = rsqrtf(ss / (float)d + eps);
-  f16* o = out + (size_t)row * ldo;
-  for (int i = threadIdx.x * 4; i < d4; i += 1024) {
-    float4 v = *reinterpret_cast<const float4*>(xr + i);
-    float4 ww = *reinterpret_cast<const float4*>(w + i);
-    half2_t a = {(f16)(v.x * sc * ww.x), (f16)(v.y * sc * ww.y)};
-    half2_t b = {(f16)(v.z * sc * ww.z), (f16)(v.w * sc * ww.w)};
-    u32x2 pk = {as_u32(a), as_u32(b)};
-    *reinterpret_cast<u32x2*>(o + i) = pk;
-  }
-  for (int i = d4 + threadIdx.x; i < d; i += 256) o[i] = (f16)(xr[i] * sc * w[i]);
-  if (zero) {
-    const int64_t per = (zero_n + M - 1) / M;
-    const int64_t z0 = (int64_t)row * per, z1 = min(zero_n, z0 + per);
-    for (int64_t i = z0 + threadIdx.x; i < z1; i += 256) zero[i] = 0.f;
-  }
+  for (int i = threadIdx.x; i < d; i += 256) o[i] = (f16)(xr[i] * sc * w[i]);
 }
 
 // ---------------------------------------------------------------- embedding (raw GGUF rows)
@@ -105,41 +121,39 @@ __global__ __launch_bounds__(256) void embed_kernel(int t, const uint8_t* table,
 
 // ---------------------------------------------------------------- RoPE (NORM, adjacent pairs) + KV append
 __global__ __launch_bounds__(256) void rope_kv_kernel(const RopeKvParams p) {
+  // grid (M tokens, head groups of 4 over [q heads | k heads | v heads]); one thread per pair
   const int m = blockIdx.x;
   const int pos = p.pos[m];
-  const int slot = p.slot[m];
   const int hd2 = p.hd / 2, Dp2 = p.Dp / 2;
   const float* row = p.qkv + (size_t)m * p.ldqkv;
   const float2* cs = p.rope_cs + (size_t)pos * hd2;
-  // q: Hq heads
-  for (int i = threadIdx.x; i < p.Hq * Dp2; i += 256) {
-    const int h = i / Dp2, j = i % Dp2;
-    half2_t o = {(f16)0.f, (f16)0.f};
-    if (j < hd2) {
-      const float x0 = row[h * p.hd + 2 * j], x1 = row[h * p.hd + 2 * j + 1];
-      const float2 c = cs[j];
-      o = half2_t{(f16)((x0 * c.x - x1 * c.y) * p.q_scale), (f16)((x0 * c.y + x1 * c.x) * p.q_scale)};
-    }
-    *reinterpret_cast<half2_t*>(p.q_out + ((size_t)m * p.Hq + h) * p.Dp + 2 * j) = o;
-  }
-  const int page = p.block_table[(size_t)slot * p.max_pages + pos / 64];
+  const int page = p.block_table[(size_t)p.slot[m] * p.max_pages + pos / 64];
   const int idx = pos % 64;
-  const float* kr = row + p.Hq * p.hd;
-  const float* vr = kr + p.Hkv * p.hd;
-  for (int i = threadIdx.x; i < p.Hkv * Dp2; i += 256) {
-    const int h = i / Dp2, j = i % Dp2;
-    half2_t o = {(f16)0.f, (f16)0.f};
-    if (j < hd2) {
-      const float x0 = kr[h * p.hd + 2 * j], x1 = kr[h * p.hd + 2 * j + 1];
-      const float2 c = cs[j];
-      o = half2_t{(f16)(x0 * c.x - x1 * c.y), (f16)(x0 * c.y + x1 * c.x)};
+  const int nh = p.Hq + 2 * p.Hkv;
+  for (int e = threadIdx.x; e < 4 * Dp2; e += 256) {
+    const int hg = blockIdx.y * 4 + e / Dp2, j = e % Dp2;
+    if (hg >= nh) break;
+    if (hg < p.Hq + p.Hkv) {                       // q or k head: rotate adjacent pair j
+      const bool isq = hg < p.Hq;
+      const int h = isq ? hg : hg - p.Hq;
+      half2_t o = {(f16)0.f, (f16)0.f};
+      if (j < hd2) {
+        const float* src = row + (isq ? 0 : p.Hq * p.hd) + h * p.hd + 2 * j;
+        const float x0 = src[0], x1 = src[1];
+        const float2 c = cs[j];
+        const float sc = isq ? p.q_scale : 1.f;
+        o = half2_t{(f16)((x0 * c.x - x1 * c.y) * sc), (f16)((x0 * c.y + x1 * c.x) * sc)};
+      }
+      if (isq) *reinterpret_cast<half2_t*>(p.q_out + ((size_t)m * p.Hq + h) * p.Dp + 2 * j) = o;
+      else *reinterpret_cast<half2_t*>(p.k_cache + (((size_t)page * p.Hkv + h) * 64 + idx) * p.Dp + 2 * j) = o;
+    } else {                                        // v head: transposed page layout [Dp][64]
+      const int h = hg - p.Hq - p.Hkv;
+      const float* vr = row + (p.Hq + p.Hkv) * p.hd + h * p.hd;
+      f16* vd = p.v_cache + (((size_t)page * p.Hkv + h) * p.Dp) * 64 + idx;
+      const int d0 = 2 * j;
+      vd[(size_t)d0 * 64] = (f16)(d0 < p.hd ? vr[d0] : 0.f);
+      vd[(size_t)(d0 + 1) * 64] = (f16)(d0 + 1 < p.hd ? vr[d0 + 1] : 0.f);
     }
-    *reinterpret_cast<half2_t*>(p.k_cache + (((size_t)page * p.Hkv + h) * 64 + idx) * p.Dp + 2 * j) = o;
-  }
-  for (int i = threadIdx.x; i < p.Hkv * p.Dp; i += 256) {
-    const int h = i / p.Dp, dd = i % p.Dp;
-    const float v = dd < p.hd ? vr[h * p.hd + dd] : 0.f;
-    p.v_cache[(((size_t)page * p.Hkv + h) * p.Dp + dd) * 64 + idx] = (f16)v;
   }
 }
 
@@ -206,7 +220,9 @@ void launch_prefill_meta(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, in
 
 void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
                     float* zero, int64_t zero_n, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M), dim3(256), 0, st, x, ldx, w, d, eps, out, ldo, zero, zero_n, M);
+  const int zb = zero ? (int)((zero_n + 4095) / 4096) : 0;
+  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(256), 0, st, x, ldx, w, d, eps, out, ldo, zero,
+                     zero_n, M);
 }
 
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,
@@ -215,7 +231,7 @@ void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t*
 }
 
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::rope_kv_kernel, dim3(p.M), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(mpk::rope_kv_kernel, dim3(p.M, (p.Hq + 2 * p.Hkv + 3) / 4), dim3(256), 0, st, p);
 }
 
 void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st) {

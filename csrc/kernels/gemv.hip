@@ -53,6 +53,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
     for (int sl = 0; sl < NSLOT; ++sl) {
       const int cur = sb + sl;
       if (cur < sb1) {
+        if constexpr (EPI == 3) {   // bandwidth probe: consume the raw words, no dequant / MFMA
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&ring[sl][t]);
+            uint32_t h = 0;
+#pragma unroll
+            for (int i = 0; i < (int)(sizeof(typename D::Raw) / 4); ++i) h ^= w[i];
+            acc[t][0] += __uint_as_float(h & 0x3FFFFFFFu);
+          }
+          if (cur + NSLOT < sb1) {
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)(cur + NSLOT) * CB, lane);
+          }
+          continue;
+        }
         half8_t a[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
@@ -145,6 +160,7 @@ static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st)
     case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
     case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
     case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
   }
 }
 
@@ -152,9 +168,9 @@ static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st)
 // than the weights themselves (3.5x at M = 16); sharing them across tiles pays.  Measured on
 // MI355X (tools/gemv_bench.py, 70B shapes): M = 16 gate/up 115 -> 67 us with 4 tiles per wave.
 int gemv_tiles_per_wave(int M, int epi) {
+  (void)epi;
   if (g_tpw) return g_tpw;
-  if (M <= 4) return 1;
-  return epi == EPI_ATOMIC ? 2 : 4;
+  return M <= 4 ? 1 : 4;
 }
 
 template <int PT>

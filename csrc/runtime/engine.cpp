@@ -131,7 +131,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.max_ctx = max_ctx_;
   so.prefill_chunk = chunk_;
   so.use_graphs = j.get_bool("graphs", true);
-  so.attn_split_len = j.get_int("attn_split_len", 256);
+  so.attn_split_len = j.get_int("attn_split_len", 128);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {

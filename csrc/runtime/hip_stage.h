@@ -29,7 +29,7 @@ struct StageOptions {
   int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
   int prefill_chunk = 256;  // max tokens per prefill chunk
   bool use_graphs = true;
-  int attn_split_len = 256; // decode flash-decoding split length (multiple of 128)
+  int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
 };
 
 // ggml types of the 2-D weights when initialising a synthetic model on device

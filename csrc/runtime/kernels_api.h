@@ -29,9 +29,13 @@ void set_gemv_wpb(int waves_per_block);   // 1 or 2 (tuning knob)
 void set_gemv_tpw(int tiles_per_wave);    // 0 = auto, 1, 2, 4 (tuning knob)
 int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)
-inline int gemv_auto_split(int ntiles, int nsb, int M, int epi, int target_waves = 2048) {
+// Cold-weight sweep on MI355X (tools/gemv_bench.py, 70B shapes): ~4096 tile-waves per launch
+// (e.g. Wo M=16: 4 tiles/wave x 8 splits = 14 us vs 20 us at 1 tile x 2 splits).
+inline int gemv_auto_split(int ntiles, int nsb, int M, int epi) {
   if (epi != EPI_ATOMIC) return 1;
-  const int waves = (ntiles + gemv_tiles_per_wave(M, epi) - 1) / gemv_tiles_per_wave(M, epi);
+  const int tpw = gemv_tiles_per_wave(M, epi);
+  const int target_waves = 4096 / tpw;
+  const int waves = (ntiles + tpw - 1) / tpw;
   int s = (target_waves + waves - 1) / waves;
   const int smax = nsb / 4 > 1 ? nsb / 4 : 1;
   return s < 1 ? 1 : (s > smax ? smax : s);

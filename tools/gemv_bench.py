@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the dequant-GEMV kernel on the Llama-3-70B / 8B decode shapes.
-Reports achieved weight-stream bandwidth (GB/s) per (shape, type, M, waves-per-block)."""
+
+Weights are COLD like in a real decode step: the timed loop cycles through enough copies of the
+matrix (>= 1.5 GB) that the 256 MiB Infinity Cache cannot serve them (a single re-streamed matrix
+that fits the MALL reads up to 40 % faster than HBM allows).  Reports weight GB/s per
+(shape, type, M, tiles-per-wave, split)."""
 import argparse, ctypes, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -12,25 +16,29 @@ SHAPES = {  # name: (N, K, epi)
     "70b.qkv": (10240, 8192, EPI_ATOMIC), "70b.o": (8192, 8192, EPI_ATOMIC),
     "70b.gateup": (57344, 8192, EPI_SWIGLU), "70b.down": (8192, 28672, EPI_ATOMIC),
     "70b.head": (128256, 8192, EPI_STORE),
-    "8b.qkv": (6144, 4096, EPI_ATOMIC), "8b.gateup": (28672, 4096, EPI_SWIGLU), "8b.down": (4096, 14336, EPI_ATOMIC),
+    "8b.qkv": (6144, 4096, EPI_ATOMIC), "8b.o": (4096, 4096, EPI_ATOMIC),
+    "8b.gateup": (28672, 4096, EPI_SWIGLU), "8b.down": (4096, 14336, EPI_ATOMIC),
 }
 TYPES = {"Q4_K": Q.Q4_K, "Q6_K": Q.Q6_K, "Q8_0": Q.Q8_0, "Q5_K": Q.Q5_K, "F16": Q.F16}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="70b.qkv,70b.o,70b.gateup,70b.down,70b.head")
     ap.add_argument("--types", default="Q4_K")
     ap.add_argument("--M", default="1,16")
-    ap.add_argument("--wpb", default="1")
     ap.add_argument("--tpw", default="1,2,4")
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--splits", default="auto")
+    ap.add_argument("--iters", type=int, default=24)
     ap.add_argument("--target", type=int, default=2048)
+    ap.add_argument("--probe", action="store_true", help="bandwidth probe: same loads, no dequant/MFMA")
     a = ap.parse_args()
     L = N.lib()
-    L.mp_set_gemv_wpb.argtypes = [ctypes.c_int]
-    res = []
+    st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for sname in a.shapes.split(","):
         n, k, epi = SHAPES[sname]
+        if a.probe:
+            epi = 3
         for tname in a.types.split(","):
             qt = TYPES[tname]
             if sname.endswith("head") and tname == "Q4_K":
@@ -38,37 +46,46 @@ def main():
             pt = pack_type(qt)
             n_pad, k_pad, ntiles, nsb = packed_dims(qt, n, k)
             nbytes = L.mp_packed_bytes(qt, n, k)
-            W = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-            L.mp_init_packed(ctypes.c_void_p(W.data_ptr()), nbytes, pt, 1.0 / k ** 0.5, 7,
-                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            copies = max(2, min(24, (1536 << 20) // nbytes + 1))
+            Ws = []
+            for c in range(copies):
+                W = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+                L.mp_init_packed(ctypes.c_void_p(W.data_ptr()), nbytes, pt, 1.0 / k ** 0.5, 7 + c, st())
+                Ws.append(W)
             for M in [int(x) for x in a.M.split(",")]:
                 X = torch.randn(M, k_pad, device="cuda").half()
                 Y = torch.zeros(M, n, device="cuda")
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
-                nsplit = 1
-                for wpb, tpw in [(int(w), int(t)) for w in a.wpb.split(",") for t in a.tpw.split(",")]:
+                for tpw in [int(t) for t in a.tpw.split(",")]:
                     L.mp_set_gemv_tpw(tpw)
-                    if epi == EPI_ATOMIC:
-                        waves = (ntiles + tpw - 1) // tpw
-                        nsplit = max(1, min((a.target + waves - 1) // waves, max(1, nsb // 4)))
-                    L.mp_set_gemv_wpb(wpb)
-                    def run():
-                        N.check(L.mp_op_gemv(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
-                                             ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()), n,
-                                             ctypes.c_void_p(H.data_ptr()), n // 2, n if epi != EPI_SWIGLU else n // 2,
-                                             nsplit, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "gemv")
-                    for _ in range(3): run()
-                    torch.cuda.synchronize()
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    for _ in range(a.iters): run()
-                    e1.record(); torch.cuda.synchronize()
-                    us = e0.elapsed_time(e1) * 1e3 / a.iters
-                    r = dict(shape=sname, type=tname, M=M, wpb=wpb, tpw=tpw, nsplit=nsplit, us=round(us, 2),
-                             GBps=round(nbytes / us / 1e3, 1))
-                    res.append(r)
-                    print(json.dumps(r), flush=True)
-    return res
+                    waves = (ntiles + tpw - 1) // tpw
+                    if epi != EPI_ATOMIC:
+                        splits = [1]
+                    elif a.splits == "auto":
+                        splits = [max(1, min((a.target + waves - 1) // waves, max(1, nsb // 4)))]
+                    else:
+                        splits = [int(s) for s in a.splits.split(",")]
+                    for nsplit in splits:
+                        def run(W):
+                            N.check(L.mp_op_gemv(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
+                                                 ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
+                                                 n, ctypes.c_void_p(H.data_ptr()), n // 2,
+                                                 n if epi != EPI_SWIGLU else n // 2, nsplit, st()), "gemv")
+                        for W in Ws[:2]:
+                            run(W)
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for i in range(a.iters):
+                            run(Ws[i % copies])
+                        e1.record()
+                        torch.cuda.synchronize()
+                        us = e0.elapsed_time(e1) * 1e3 / a.iters
+                        print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
+                                              GBps=round(nbytes / us / 1e3, 1))), flush=True)
+            del Ws
+            torch.cuda.empty_cache()
+
 
 if __name__ == "__main__":
     main()
