@@ -1,0 +1,140 @@
+// Mixture-of-experts FFN (Mixtral): device-side top-k routing and a grouped
+// dequant-GEMV over the routed experts.  Everything stays on the GPU (graph-capturable): the
+// router writes per-expert token lists, the expert kernels read the counts and exit early for
+// idle experts, so a decode step streams only the weights of the experts actually selected.
+#include "kcommon.h"
+#include "dequant.h"
+#include "../runtime/kernels_api.h"
+
+namespace mpk {
+using namespace mp;
+
+// one block: softmax over E router logits per token, top-k, renormalise, bucket by expert
+__global__ __launch_bounds__(256) void moe_route_kernel(const MoeRouteParams p) {
+  for (int e = threadIdx.x; e < p.E; e += blockDim.x) p.counts[e] = 0;
+  __syncthreads();
+  for (int t = threadIdx.x; t < p.M; t += blockDim.x) {
+    const float* lg = p.logits + (size_t)t * p.ld;
+    float mx = -INFINITY;
+    for (int e = 0; e < p.E; ++e) mx = fmaxf(mx, lg[e]);
+    float sum = 0.f;
+    for (int e = 0; e < p.E; ++e) sum += __expf(lg[e] - mx);
+    unsigned long long taken = 0;
+    float wsel[8];
+    int esel[8];
+    float wsum = 0.f;
+    for (int j = 0; j < p.k; ++j) {
+      int best = -1;
+      float bv = -INFINITY;
+      for (int e = 0; e < p.E; ++e)
+        if (!((taken >> e) & 1ull) && lg[e] > bv) { bv = lg[e]; best = e; }
+      taken |= 1ull << best;
+      esel[j] = best;
+      wsel[j] = __expf(bv - mx) / sum;
+      wsum += wsel[j];
+    }
+    for (int j = 0; j < p.k; ++j) {
+      const int slot = t * p.k + j;
+      p.weights[slot] = wsel[j] / wsum;
+      const int pos = atomicAdd(&p.counts[esel[j]], 1);
+      p.lists[(size_t)esel[j] * p.list_cap + pos] = slot;
+    }
+  }
+}
+
+// Grouped skinny GEMV: grid (tiles, splits, experts).  Rows = the slots routed to expert e,
+// processed 16 at a time (one MFMA row tile); weights of expert e at W + e * estride.
+template <int PT, int EPI>
+__global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB;
+  constexpr int NSLOT = 4;
+  const int e = blockIdx.z;
+  const int count = p.counts[e];
+  if (count == 0) return;
+  const int lane = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int sb0 = blockIdx.y * p.sb_per_split;
+  const int sb1 = min(sb0 + p.sb_per_split, p.nsb);
+  if (sb0 >= sb1) return;
+  const int g = lane >> 4, r = lane & 15;
+  const uint8_t* wt = p.W + (size_t)e * p.estride + (size_t)tile * p.nsb * CB;
+  const int32_t* list = p.lists + (size_t)e * p.list_cap;
+  const int last = sb1 - 1;
+  for (int r0 = 0; r0 < count; r0 += 16) {
+    const int rows = min(16, count - r0);
+    const int slot_r = list[r0 + min(r, rows - 1)];
+    const int xrow = p.x_per_slot ? slot_r : slot_r / p.k;
+    const f16* xp = p.X + (size_t)xrow * p.ldx + 8 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    typename D::Raw ring[NSLOT];
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) D::load(ring[sl], wt + (size_t)min(sb0 + sl, last) * CB, lane);
+    for (int sb = sb0; sb < sb1; sb += NSLOT) {
+#pragma unroll
+      for (int sl = 0; sl < NSLOT; ++sl) {
+        const int cur = sb + sl;
+        if (cur < sb1) {
+          half8_t a[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+          half8_t b[4];
+          D::template dequant<0>(ring[sl], b, lane);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[s], b[s], acc);
+          D::template dequant<1>(ring[sl], b, lane);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[4 + s], b[s], acc);
+          if (cur + NSLOT < sb1) D::load(ring[sl], wt + (size_t)(cur + NSLOT) * CB, lane);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 4 * g + i;
+      if (EPI == EPI_SWIGLU) {
+        const float other = __shfl_xor(acc[i], 8);
+        if (r < 8 && m < rows) {
+          const int o = tile * 8 + r;
+          const int slot = list[r0 + m];
+          if (o < p.n_valid) p.H[(size_t)slot * p.ldh + o] = (f16)(silu(acc[i]) * other);
+        }
+      } else if (m < rows) {
+        const int n = tile * 16 + r;
+        const int slot = list[r0 + m];
+        if (n < p.n_valid) unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[i]);
+      }
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+void launch_moe_route(const MoeRouteParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::moe_route_kernel, dim3(1), dim3(256), 0, st, p);
+}
+
+template <int PT>
+static void moe_launch_pt(int epi, const MoeGemvParams& p, int nsplit, hipStream_t st) {
+  dim3 grid(p.ntiles, nsplit, p.E);
+  if (epi == EPI_SWIGLU) hipLaunchKernelGGL((mpk::moe_gemv_kernel<PT, EPI_SWIGLU>), grid, dim3(64), 0, st, p);
+  else hipLaunchKernelGGL((mpk::moe_gemv_kernel<PT, EPI_ATOMIC>), grid, dim3(64), 0, st, p);
+}
+
+void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st) {
+  if (nsplit < 1 || epi == EPI_SWIGLU) nsplit = 1;
+  p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
+  nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
+  switch (ptype) {
+    case P_Q4_K: moe_launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
+    case P_Q5_K: moe_launch_pt<P_Q5_K>(epi, p, nsplit, st); break;
+    case P_Q6_K: moe_launch_pt<P_Q6_K>(epi, p, nsplit, st); break;
+    case P_Q8_0: moe_launch_pt<P_Q8_0>(epi, p, nsplit, st); break;
+    case P_Q4_0: moe_launch_pt<P_Q4_0>(epi, p, nsplit, st); break;
+    case P_F16: moe_launch_pt<P_F16>(epi, p, nsplit, st); break;
+  }
+}
+
+}  // namespace mp

@@ -8,6 +8,7 @@
 #include <numeric>
 #include <stdexcept>
 
+#include "cpu_stage.h"
 #include "gguf.h"
 #include "log.h"
 #include "qtypes.h"
@@ -59,8 +60,8 @@ double synth_layer_bytes(const ModelConfig& c, const std::string& ftype, int li)
   const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, li, c.n_layer);
   auto b = [](int ty, double n, double k) { return n * k * block_bytes(ty) / block_elems(ty); };
   const double d = c.d_model, q = c.q_dim(), kv = c.kv_dim(), f = c.d_ff;
-  return b(t.q, q, d) + b(t.k, kv, d) + b(t.v, kv, d) + b(t.o, d, q) + b(t.gate, f, d) + b(t.up, f, d) +
-         b(t.down, d, f);
+  const double ffn = b(t.gate, f, d) + b(t.up, f, d) + b(t.down, d, f);
+  return b(t.q, q, d) + b(t.k, kv, d) + b(t.v, kv, d) + b(t.o, d, q) + ffn * std::max(1, c.n_expert);
 }
 
 }  // namespace
@@ -70,6 +71,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   if (j.get_bool("verbose", false)) log_set_level(LOG_DEBUG);
   if (j.has("log_file")) log_set_file(j.get_str("log_file", ""));
   mode_ = j.get_str("mode", "local");
+  cpu_ = j.get_str("backend", "hip") == "cpu";
   M_ = std::max(1, j.get_int("n_mb", 1));
   B_ = std::max(1, j.get_int("mb_size", 1));
   if (B_ > 16) throw std::runtime_error("mb_size > 16 not supported (decode micro-batch is one MFMA row tile)");
@@ -132,17 +134,29 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.prefill_chunk = chunk_;
   so.use_graphs = j.get_bool("graphs", true);
   so.attn_split_len = j.get_int("attn_split_len", 128);
+  so.threads = j.get_int("threads", 0);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {
     if (mode_ == "mp" && s != rank_) continue;
     auto w = std::make_unique<Worker>();
     w->device = specs_[s].device;
-    HIP_OK(hipSetDevice(w->device));
-    w->stage.reset(new HipStage(cfg_, specs_[s], so));
+    if (cpu_) {
+      w->stage.reset(new CpuStage(cfg_, specs_[s], so));
+    } else {
+      HIP_OK(hipSetDevice(w->device));
+      w->stage.reset(new HipStage(cfg_, specs_[s], so));
+    }
     if (gguf_) w->stage->load_gguf(*gguf_);
     else w->stage->init_synthetic(ftype, seed);
     w->stage->alloc_runtime();
+    w->stage->set_sampling((float)j.get_num("temp", 0.0), j.get_int("top_k", 0), (float)j.get_num("top_p", 1.0),
+                           (float)j.get_num("min_p", 0.0), seed);
+    if (cpu_) {
+      w->ring_pending.assign(M_, false);
+      workers_.push_back(std::move(w));
+      continue;
+    }
     HIP_OK(hipStreamCreateWithFlags(&w->send_st, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&w->recv_st, hipStreamNonBlocking));
     w->comp_ev.resize(M_); w->sent_ev.resize(M_); w->recv_ev.resize(M_);
@@ -155,12 +169,17 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     workers_.push_back(std::move(w));
   }
   build_links(j);
-  for (auto& w : workers_) {
-    HIP_OK(hipSetDevice(w->device));
-    w->stage->capture_graphs();
-  }
   rounds_cap_ = max_ctx_ + 2;
-  HIP_OK(hipHostMalloc((void**)&out_host_, (size_t)rounds_cap_ * M_ * B_ * 4, hipHostMallocDefault));
+  if (cpu_) {
+    out_vec_.resize((size_t)rounds_cap_ * M_ * B_);
+    out_host_ = out_vec_.data();
+  } else {
+    for (auto& w : workers_) {
+      HIP_OK(hipSetDevice(w->device));
+      w->stage->capture_graphs();
+    }
+    HIP_OK(hipHostMalloc((void**)&out_host_, (size_t)rounds_cap_ * M_ * B_ * 4, hipHostMallocDefault));
+  }
   std::memset(out_host_, 0xff, (size_t)rounds_cap_ * M_ * B_ * 4);
   load_ms_ = now_ms() - t0;
   MP_LOGI("engine ready: %d stage(s), %d micro-batch(es) x %d seq, ctx %d, load %.1f ms", S_, M_, B_, max_ctx_,
@@ -173,6 +192,10 @@ Engine::~Engine() {
   } catch (...) {
   }
   for (auto& w : workers_) {
+    if (cpu_) {
+      w->stage.reset();
+      continue;
+    }
     (void)hipSetDevice(w->device);
     for (auto e : w->comp_ev) (void)hipEventDestroy(e);
     for (auto e : w->sent_ev) (void)hipEventDestroy(e);
@@ -183,7 +206,7 @@ Engine::~Engine() {
     (void)hipStreamDestroy(w->recv_st);
   }
   links_.clear();
-  if (out_host_) (void)hipHostFree(out_host_);
+  if (out_host_ && !cpu_) (void)hipHostFree(out_host_);
 }
 
 bool Engine::owns_last() const {
@@ -200,11 +223,14 @@ void Engine::build_links(const Json& j) {
   // link i: stage i -> stage (i+1) % S (link S-1 is the token ring back to stage 0)
   const size_t act_bytes = (size_t)std::max(chunk_, B_) * cfg_.d_model * 4;
   if (mode_ == "local") {
-    const std::string kind = j.get_str("link", "local");
-    std::vector<Link*> fwd(S_);
+    const std::string kind = cpu_ ? "host" : j.get_str("link", "local");
     for (int i = 0; i < S_; ++i) {
       const int a = i, b = (i + 1) % S_;
-      if (kind == "rccl") {
+      if (cpu_) {
+        links_.emplace_back(new HostLink(std::max(4, M_ + 2)));
+        workers_[a]->out = links_.back().get();
+        workers_[b]->in = links_.back().get();
+      } else if (kind == "rccl") {
         void *ca, *cb;
         rccl_make_pair(specs_[a].device, specs_[b].device, &ca, &cb);
         links_.emplace_back(new RcclLink(ca, 0, specs_[a].device));   // sender end
@@ -220,6 +246,41 @@ void Engine::build_links(const Json& j) {
       }
     }
     MP_LOGI("links: %d x %s (act %.1f KiB/token, ring %d B/token)", S_, kind.c_str(), cfg_.d_model * 4 / 1024.0, 4);
+  } else if (cpu_ || j.get_str("link", "rccl") == "tcp") {
+    // one TCP connection per link: receiver of link l (rank l+1) listens on base_port + l,
+    // sender (rank l) connects to hosts[l+1].  Accept runs on a helper thread so the ring cannot
+    // deadlock on connection order.
+    const int base = j.get_int("base_port", 29600);
+    std::vector<std::string> hosts(S_, "127.0.0.1");
+    if (j.has("hosts"))
+      for (int r = 0; r < S_ && r < (int)j["hosts"].arr().size(); ++r) hosts[r] = j["hosts"].arr()[r].str();
+    const double to = j.get_num("connect_timeout", 120.0);
+    const int in_l = (rank_ - 1 + S_) % S_, out_l = rank_;
+    Worker& w = *workers_[0];
+    std::unique_ptr<TcpLink> rx;
+    std::exception_ptr err;
+    std::thread acc([&] {
+      try {
+        rx = TcpLink::make_receiver(base + in_l, to);
+      } catch (...) {
+        err = std::current_exception();
+      }
+    });
+    std::unique_ptr<TcpLink> tx;
+    try {
+      tx = TcpLink::make_sender(hosts[(rank_ + 1) % S_], base + out_l, to);
+    } catch (...) {
+      acc.join();
+      throw;
+    }
+    acc.join();
+    if (err) std::rethrow_exception(err);
+    w.in = rx.get();
+    w.out = tx.get();
+    links_.emplace_back(std::move(rx));
+    links_.emplace_back(std::move(tx));
+    MP_LOGI("rank %d: TCP links in=%d (port %d) out=%d -> %s:%d", rank_, in_l, base + in_l, out_l,
+            hosts[(rank_ + 1) % S_].c_str(), base + out_l);
   } else {
     const auto& ids = j["rccl_ids"].arr();
     if ((int)ids.size() != S_) throw std::runtime_error("mp mode needs one RCCL id per link");
@@ -238,16 +299,71 @@ void Engine::build_links(const Json& j) {
 }
 
 void Engine::post_ring_recv(Worker& w, int mb) {
-  HipStage& st = *w.stage;
+  Stage& st = *w.stage;
   HIP_OK(hipEventRecord(w.comp_ev[mb], st.stream()));
   HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
   w.in->recv(st.tokens(mb), (size_t)B_ * 4, w.recv_st);
   HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
 }
 
+// CPU stages: the same item schedule, blocking host transfers.  The first stage receives the
+// ring token of micro-batch mb lazily (right before its next DECODE) and drains the ring at the
+// end of the item list, like the GPU path's posted ring receives.
+void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
+  Stage& st = *w.stage;
+  const bool first = st.spec().first(), last = st.spec().last();
+  const size_t d4 = (size_t)cfg_.d_model * 4;
+  for (const Item& it : items) {
+    const int mb = it.mb;
+    switch (it.kind) {
+      case Item::PREFILL: {
+        if (!first) w.in->recv(st.act(mb), (size_t)it.T * d4, nullptr);
+        st.prefill_chunk(mb, it.b, it.p0, it.T,
+                         first ? st.prompt_buf() + (size_t)(mb * B_ + it.b) * max_ctx_ + it.p0 : nullptr,
+                         it.last_chunk, nullptr);
+        if (!last) w.out->send(st.act(mb), (size_t)it.T * d4, nullptr);
+        break;
+      }
+      case Item::PREFILL_END: {
+        if (last) std::memcpy(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4);
+        if (S_ > 1) {
+          if (last) w.out->send(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          if (first) w.ring_pending[mb] = true;
+        }
+        break;
+      }
+      case Item::DECODE: {
+        if (!first) w.in->recv(st.act(mb), (size_t)B_ * d4, nullptr);
+        else if (w.ring_pending[mb]) {
+          w.in->recv(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          w.ring_pending[mb] = false;
+        }
+        st.decode(mb, nullptr);
+        if (last) {
+          w.tok_t.push_back(now_ms());
+          std::memcpy(out_host_ + ((size_t)(it.round + 1) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4);
+        }
+        if (S_ > 1) {
+          if (!last) w.out->send(st.act(mb), (size_t)B_ * d4, nullptr);
+          else w.out->send(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          if (first) w.ring_pending[mb] = true;
+        }
+        break;
+      }
+    }
+  }
+  if (first && S_ > 1)
+    for (int mb = 0; mb < M_; ++mb)
+      if (w.ring_pending[mb]) {
+        w.in->recv(st.tokens(mb), (size_t)B_ * 4, nullptr);
+        w.ring_pending[mb] = false;
+      }
+}
+
 void Engine::run_items(Worker& w, const std::vector<Item>& items) {
+  if (cpu_) return run_items_cpu(w, items);
   HIP_OK(hipSetDevice(w.device));
-  HipStage& st = *w.stage;
+  Stage& st = *w.stage;
   hipStream_t cs = st.stream();
   const bool first = st.spec().first(), last = st.spec().last();
   const size_t d4 = (size_t)cfg_.d_model * 4;
@@ -273,8 +389,8 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         const size_t bytes = (size_t)it.T * d4;
         if (!first) recv_into(mb, st.act(mb), bytes);
         else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
-        const int slot = st.slot_of(mb, it.b);
-        st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_dev() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
+        const int slot = mb * B_ + it.b;
+        st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_buf() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
                          it.last_chunk, cs);
         if (!last) send_from(mb, st.act(mb), bytes);
         break;
@@ -333,6 +449,7 @@ void Engine::run_all(const std::vector<Item>& items) {
 }
 
 void Engine::sync_all() {
+  if (cpu_) return;
   for (auto& w : workers_) {
     HIP_OK(hipSetDevice(w->device));
     HIP_OK(hipStreamSynchronize(w->stage->stream()));
@@ -350,21 +467,22 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   rounds_done_ = 0;
   std::vector<Item> items;
   for (auto& w : workers_) {
-    HipStage& st = *w->stage;
-    HIP_OK(hipSetDevice(w->device));
+    Stage& st = *w->stage;
+    if (!cpu_) HIP_OK(hipSetDevice(w->device));
     for (int mb = 0; mb < M_; ++mb) {
       std::vector<int32_t> pos(B_, 0);
       for (int b = 0; b < B_; ++b) {
         const size_t i = (size_t)mb * B_ + b;
         if (i < prompts.size()) pos[b] = (int)prompts[i].size();
       }
-      st.set_positions(mb, pos, st.stream());
+      st.set_positions(mb, pos);
     }
     if (st.spec().first()) {
       for (size_t i = 0; i < prompts.size(); ++i) {
         if (prompts[i].empty() || (int)prompts[i].size() >= max_ctx_) throw std::runtime_error("bad prompt length");
-        HIP_OK(hipMemcpy(st.prompt_dev() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4,
-                         hipMemcpyHostToDevice));
+        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4);
+        else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4,
+                              hipMemcpyHostToDevice));
       }
     }
   }
@@ -396,7 +514,9 @@ StepStats Engine::decode_steps(int k) {
   if (rounds_done_ + k + 1 >= rounds_cap_ || (int)max_prompt + rounds_done_ + k + 1 > max_ctx_)
     throw std::runtime_error("context capacity exhausted (prompt + generated tokens > max_ctx)");
   for (auto& w : workers_)
-    if (w->stage->spec().last()) {
+    if (w->stage->spec().last() && cpu_) {
+      w->tok_t.clear();
+    } else if (w->stage->spec().last()) {
       HIP_OK(hipSetDevice(w->device));
       for (auto e : w->tok_ev) (void)hipEventDestroy(e);
       w->tok_ev.assign((size_t)k * M_, nullptr);
@@ -415,7 +535,9 @@ StepStats Engine::decode_steps(int k) {
   StepStats ss;
   ss.wall_ms = now_ms() - t0;
   for (auto& w : workers_)
-    if (w->stage->spec().last()) {
+    if (w->stage->spec().last() && cpu_) {
+      for (size_t i = M_; i < w->tok_t.size(); ++i) ss.token_ms.push_back(w->tok_t[i] - w->tok_t[i - M_]);
+    } else if (w->stage->spec().last()) {
       for (int r = 1; r < k; ++r)
         for (int mb = 0; mb < M_; ++mb) {
           float ms = 0;
@@ -489,9 +611,15 @@ int Engine::copy_logits(int mb, float* out, int rows) {
   (void)mb;
   for (auto& w : workers_)
     if (w->stage->spec().last()) {
+      if (cpu_) {
+        for (int r = 0; r < rows; ++r)
+          std::memcpy(out + (size_t)r * cfg_.vocab, w->stage->logits_ptr() + (size_t)r * w->stage->logits_ld(),
+                      (size_t)cfg_.vocab * 4);
+        return 0;
+      }
       HIP_OK(hipSetDevice(w->device));
       HIP_OK(hipStreamSynchronize(w->stage->stream()));
-      HIP_OK(hipMemcpy2D(out, (size_t)cfg_.vocab * 4, w->stage->logits(), (size_t)w->stage->logits_ld() * 4,
+      HIP_OK(hipMemcpy2D(out, (size_t)cfg_.vocab * 4, w->stage->logits_ptr(), (size_t)w->stage->logits_ld() * 4,
                          (size_t)cfg_.vocab * 4, rows, hipMemcpyDeviceToHost));
       return 0;
     }
@@ -505,6 +633,7 @@ Json Engine::info() const {
   j["mb_size"] = B_;
   j["max_ctx"] = max_ctx_;
   j["mode"] = mode_;
+  j["backend"] = cpu_ ? "cpu" : "hip";
   j["load_ms"] = load_ms_;
   Json st = Json::array();
   for (auto& s : specs_) {

@@ -75,18 +75,21 @@ class Engine {
 
  private:
   struct Worker {
-    std::unique_ptr<HipStage> stage;
+    std::unique_ptr<Stage> stage;
     Link* in = nullptr;    // activations from s-1 (or ring tokens from S-1 for s = 0)
     Link* out = nullptr;   // activations to s+1 (or ring tokens to 0 for s = S-1)
     hipStream_t send_st = nullptr, recv_st = nullptr;
     std::vector<hipEvent_t> comp_ev, sent_ev, recv_ev;
     std::vector<bool> sent_valid;
     std::vector<hipEvent_t> tok_ev;   // last stage: per (round, mb) timing events
+    std::vector<double> tok_t;        // CPU backend: host timestamps of the same
+    std::vector<bool> ring_pending;   // CPU backend, first stage: ring token not yet received
     int device = 0;
   };
 
   void build_links(const Json& cfg);
   void run_items(Worker& w, const std::vector<Item>& items);
+  void run_items_cpu(Worker& w, const std::vector<Item>& items);
   void run_all(const std::vector<Item>& items);
   void post_ring_recv(Worker& w, int mb);
   void sync_all();
@@ -105,6 +108,8 @@ class Engine {
   std::vector<std::vector<int32_t>> prompts_;
   std::vector<std::vector<int32_t>> gen_;          // generated tokens per sequence
   int32_t* out_host_ = nullptr;                    // pinned [rounds_cap][M*B]
+  std::vector<int32_t> out_vec_;                   // CPU backend storage of out_host_
+  bool cpu_ = false;
   int rounds_cap_ = 0, rounds_done_ = 0;
   bool started_ = false;
   double load_ms_ = 0;

@@ -51,11 +51,10 @@ HipStage::HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOpt
 }
 
 HipStage::~HipStage() {
-  hipSetDevice(spec_.device);
+  (void)hipSetDevice(spec_.device);
   destroy_graphs();
-  for (void* p : allocs_) hipFree(p);
-  if (pf_host_) hipHostFree(pf_host_);
-  if (stream_) hipStreamDestroy(stream_);
+  for (void* p : allocs_) (void)hipFree(p);
+  if (stream_) (void)hipStreamDestroy(stream_);
 }
 
 void* HipStage::dmalloc(size_t bytes) {
@@ -82,6 +81,23 @@ PackedMat HipStage::upload_packed(int t, int64_t N, int64_t K, const std::functi
   m.d = (uint8_t*)dmalloc(m.dims.bytes);
   HIP_OK(hipMemcpy(m.d, host.data(), m.dims.bytes, hipMemcpyHostToDevice));
   weight_bytes_ += m.dims.bytes;
+  return m;
+}
+
+PackedMat HipStage::upload_packed_experts(int t, int E, int64_t N, int64_t K, size_t* stride,
+                                          const std::function<const uint8_t*(int, int64_t)>& row) {
+  PackedMat m;
+  m.ptype = pack_type_of(t);
+  if (m.ptype < 0) throw std::runtime_error(std::string("unsupported expert type ") + type_name(t));
+  m.dims = packed_dims(m.ptype, N, K);
+  *stride = m.dims.bytes;
+  std::vector<uint8_t> host(m.dims.bytes);
+  m.d = (uint8_t*)dmalloc(m.dims.bytes * E);
+  for (int e = 0; e < E; ++e) {
+    pack_t16(t, N, K, [&](int64_t n) { return row(e, n); }, host.data());
+    HIP_OK(hipMemcpy(m.d + (size_t)e * m.dims.bytes, host.data(), m.dims.bytes, hipMemcpyHostToDevice));
+  }
+  weight_bytes_ += m.dims.bytes * E;
   return m;
 }
 
@@ -156,7 +172,41 @@ void HipStage::load_gguf(const GgufFile& f) {
     }
     L.wo = pack_mat(need(p + "attn_output.weight"));
     if (cfg_.n_expert) {
-      throw std::runtime_error("MoE weights: use load path with experts (not yet wired)");
+      // Mixtral: router [E][d] + stacked experts (ffn_*_exps [E][F][d]) or legacy per-expert tensors
+      L.moe = true;
+      const int E = cfg_.n_expert;
+      L.ex.router = pack_mat(need(p + "ffn_gate_inp.weight"));
+      std::vector<const GgufTensor*> g(E), u(E), dn(E);
+      const GgufTensor* sg = f.tensor(p + "ffn_gate_exps.weight");
+      for (int e = 0; e < E; ++e) {
+        if (sg) {
+          g[e] = sg;
+          u[e] = &need(p + "ffn_up_exps.weight");
+          dn[e] = &need(p + "ffn_down_exps.weight");
+        } else {
+          const std::string s = "." + std::to_string(e) + ".weight";
+          g[e] = &need(p + "ffn_gate" + s);
+          u[e] = &need(p + "ffn_up" + s);
+          dn[e] = &need(p + "ffn_down" + s);
+        }
+      }
+      if (g[0]->type != u[0]->type) throw std::runtime_error("MoE gate/up types differ");
+      const int64_t F = cfg_.d_ff, D = cfg_.d_model;
+      // row n of expert e of a (possibly stacked) tensor
+      auto erow = [&](const GgufTensor* t, int e, int64_t n, int64_t rows) -> const uint8_t* {
+        const size_t rb = row_bytes(t->type, t->ne[0]);
+        return t->data + ((sg ? (size_t)e * rows : 0) + n) * rb;
+      };
+      L.ex.gateup = upload_packed_experts(g[0]->type, E, 2 * F, D, &L.ex.gateup_stride,
+                                          [&](int e, int64_t n) -> const uint8_t* {
+                                            bool up;
+                                            const int64_t r = gateup_src_row(n, &up);
+                                            if (r >= F) return nullptr;
+                                            return erow(up ? u[e] : g[e], e, r, F);
+                                          });
+      L.ex.down = upload_packed_experts(dn[0]->type, E, D, F, &L.ex.down_stride,
+                                        [&](int e, int64_t n) { return erow(dn[e], e, n, D); });
+      continue;
     }
     const GgufTensor& tg = need(p + "ffn_gate.weight");
     const GgufTensor& tu = need(p + "ffn_up.weight");
@@ -218,7 +268,24 @@ void HipStage::init_synthetic(const std::string& ftype, uint64_t seed) {
       L.qkv.push_back({alloc_packed_random(t.v, kvd, d, s + 3), qd + kvd});
     }
     L.wo = alloc_packed_random(t.o, d, qd, s + 4);
-    if (cfg_.n_expert) throw std::runtime_error("synthetic MoE not wired yet");
+    if (cfg_.n_expert) {
+      const int E = cfg_.n_expert;
+      L.moe = true;
+      L.ex.router = alloc_packed_random(T_F16, E, d, s + 7);
+      auto experts = [&](int ty, int64_t N, int64_t K, size_t* stride, uint64_t sd) {
+        PackedMat m;
+        m.ptype = pack_type_of(ty);
+        m.dims = packed_dims(m.ptype, N, K);
+        *stride = m.dims.bytes;
+        m.d = (uint8_t*)dmalloc(m.dims.bytes * E);
+        launch_init_packed(m.d, m.dims.bytes * E, m.ptype, 1.0f / std::sqrt((float)K), sd, stream_);
+        weight_bytes_ += m.dims.bytes * E;
+        return m;
+      };
+      L.ex.gateup = experts(t.gate, 2 * F, d, &L.ex.gateup_stride, s + 5);
+      L.ex.down = experts(t.down, d, F, &L.ex.down_stride, s + 6);
+      continue;
+    }
     L.fused_gateup = true;
     L.gateup = alloc_packed_random(t.gate, 2 * F, d, s + 5);
     L.down = alloc_packed_random(t.down, d, F, s + 6);
@@ -258,6 +325,16 @@ void HipStage::alloc_runtime() {
   bool any_unfused = false;
   for (auto& L : layers_) any_unfused |= !L.fused_gateup;
   if (any_unfused) gu_ = (float*)zalloc((size_t)scratch_rows_ * 2 * cfg_.d_ff * 4);
+  if (cfg_.n_expert) {
+    if (cfg_.n_expert > 64 || cfg_.n_expert_used > 8 || cfg_.n_expert_used < 1)
+      throw std::runtime_error("MoE: need n_expert <= 64 and 1 <= n_expert_used <= 8");
+    const int k = cfg_.n_expert_used;
+    moe_logits_ = (float*)zalloc((size_t)scratch_rows_ * 64 * 4);
+    moe_counts_ = (int32_t*)zalloc(64 * 4);
+    moe_lists_ = (int32_t*)zalloc((size_t)cfg_.n_expert * scratch_rows_ * k * 4);
+    moe_w_ = (float*)zalloc((size_t)scratch_rows_ * k * 4);
+    moe_h_ = (f16*)zalloc((size_t)scratch_rows_ * k * Kff_ * 2);
+  }
   if (spec_.last()) {
     logits_ld_ = (int)round_up(cfg_.vocab, 16);
     logits_ = (float*)zalloc((size_t)B * logits_ld_ * 4);
@@ -320,12 +397,19 @@ void HipStage::alloc_runtime() {
           weight_bytes_ / 1073741824.0, kv_bytes_ / 1073741824.0, n_slots, opt_.max_ctx);
 }
 
-void HipStage::set_positions(int mb, const std::vector<int32_t>& pos, hipStream_t st) {
+void HipStage::set_positions(int mb, const std::vector<int32_t>& pos) {
+  HIP_OK(hipSetDevice(spec_.device));
   std::vector<int32_t> p(std::max(opt_.mb_size, 16), 0), k(std::max(opt_.mb_size, 16), 1);
   for (size_t i = 0; i < pos.size() && i < p.size(); ++i) { p[i] = pos[i]; k[i] = pos[i] + 1; }
-  HIP_OK(hipMemcpyAsync(pos_[mb], p.data(), p.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_OK(hipMemcpyAsync(kvlen_[mb], k.data(), k.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_OK(hipStreamSynchronize(st));
+  HIP_OK(hipMemcpyAsync(pos_[mb], p.data(), p.size() * 4, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipMemcpyAsync(kvlen_[mb], k.data(), k.size() * 4, hipMemcpyHostToDevice, stream_));
+  HIP_OK(hipStreamSynchronize(stream_));
+}
+
+void HipStage::set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) {
+  const bool changed = temp != temp_ || top_k != top_k_ || top_p != top_p_ || min_p != min_p_ || seed != seed_;
+  Stage::set_sampling(temp, top_k, top_p, min_p, seed);
+  if (changed && !graphs_.empty() && spec_.last()) capture_graphs();
 }
 
 void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
@@ -348,9 +432,33 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   }
 }
 
-void HipStage::layer_forward(int li, int M, int mb, float* x, const int32_t* pos, const int32_t* kvlen,
-                             const int32_t* slot, int tq, bool decode, hipStream_t st) {
-  (void)mb;
+void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
+  const int E = cfg_.n_expert, k = cfg_.n_expert_used, d = cfg_.d_model, F = cfg_.d_ff;
+  gemv(L.ex.router, EPI_STORE, xn_, Kd_, M, moe_logits_, 64, nullptr, 0, E, false, st);
+  MoeRouteParams rp{};
+  rp.logits = moe_logits_; rp.ld = 64; rp.M = M; rp.E = E; rp.k = k;
+  rp.counts = moe_counts_; rp.lists = moe_lists_; rp.list_cap = scratch_rows_ * k; rp.weights = moe_w_;
+  launch_moe_route(rp, st);
+  MoeGemvParams gp{};
+  gp.W = L.ex.gateup.d; gp.estride = L.ex.gateup_stride;
+  gp.ntiles = (int)L.ex.gateup.dims.ntiles; gp.nsb = (int)L.ex.gateup.dims.nsb;
+  gp.X = xn_; gp.ldx = Kd_; gp.x_per_slot = 0; gp.k = k;
+  gp.counts = moe_counts_; gp.lists = moe_lists_; gp.list_cap = rp.list_cap; gp.E = E;
+  gp.H = moe_h_; gp.ldh = Kff_; gp.n_valid = F;
+  launch_moe_gemv(L.ex.gateup.ptype, EPI_SWIGLU, gp, 1, st);
+  MoeGemvParams dp = gp;
+  dp.W = L.ex.down.d; dp.estride = L.ex.down_stride;
+  dp.ntiles = (int)L.ex.down.dims.ntiles; dp.nsb = (int)L.ex.down.dims.nsb;
+  dp.X = moe_h_; dp.ldx = Kff_; dp.x_per_slot = 1; dp.H = nullptr; dp.ldh = 0;
+  dp.Y = x; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
+  // only ~k/E of the expert grid is busy: size the split for the active experts
+  const int active = std::min(E, M * k);
+  const int nsplit = std::max(1, std::min(dp.nsb / 4, 4096 / std::max(1, dp.ntiles * active)));
+  launch_moe_gemv(L.ex.down.ptype, EPI_ATOMIC, dp, nsplit, st);
+}
+
+void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* kvlen,
+                             const int32_t* slot, bool decode, hipStream_t st) {
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
   launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st);
@@ -380,6 +488,10 @@ void HipStage::layer_forward(int li, int M, int mb, float* x, const int32_t* pos
   launch_attention(ap, st);
   gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
   launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+  if (L.moe) {
+    moe_ffn(L, M, st, x);
+    return;
+  }
   if (L.fused_gateup) {
     gemv(L.gateup, EPI_SWIGLU, xn_, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st);
   } else {
@@ -391,11 +503,19 @@ void HipStage::layer_forward(int li, int M, int mb, float* x, const int32_t* pos
   gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
 }
 
-void HipStage::head(int M, const float* x, int32_t* tok_out, hipStream_t st) {
+void HipStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st) {
   const int d = cfg_.d_model;
   launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
   gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
-  launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st);
+  if (temp_ > 0.f) {
+    SampleParams sp{};
+    sp.logits = logits_; sp.ld = logits_ld_; sp.n = cfg_.vocab; sp.M = M;
+    sp.temp = temp_; sp.top_k = top_k_; sp.top_p = top_p_; sp.min_p = min_p_;
+    sp.seed = seed_ ^ (salt * 0x9E3779B97F4A7C15ULL); sp.step = step_; sp.tokens = tok_out;
+    launch_sample(sp, st);
+  } else {
+    launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st);
+  }
 }
 
 void HipStage::prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk,
@@ -408,8 +528,8 @@ void HipStage::prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens
   if (spec_.first()) launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tokens_dev, T, x,
                                   cfg_.d_model, st);
   for (size_t li = 0; li < layers_.size(); ++li)
-    layer_forward((int)li, T, mb, x, pf_pos_, pf_kvlen_, pf_slot_, 0, false, st);
-  if (spec_.last() && last_chunk) head(1, x + (size_t)(T - 1) * cfg_.d_model, tok_[mb] + b, st);
+    layer_forward((int)li, T, x, pf_pos_, pf_kvlen_, pf_slot_, false, st);
+  if (spec_.last() && last_chunk) head(1, x + (size_t)(T - 1) * cfg_.d_model, tok_[mb] + b, 1000003ULL + sl, st);
 }
 
 void HipStage::decode_eager(int mb, hipStream_t st) {
@@ -418,8 +538,8 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
   if (spec_.first())
     launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tok_[mb], B, x, cfg_.d_model, st);
   for (size_t li = 0; li < layers_.size(); ++li)
-    layer_forward((int)li, B, mb, x, pos_[mb], kvlen_[mb], slot_[mb], 1, true, st);
-  if (spec_.last()) head(B, x, tok_[mb], st);
+    layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
+  if (spec_.last()) head(B, x, tok_[mb], (uint64_t)mb + 1, st);
   launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
 }
 
@@ -440,7 +560,7 @@ void HipStage::capture_graphs() {
 }
 
 void HipStage::destroy_graphs() {
-  for (auto g : graphs_) hipGraphExecDestroy(g);
+  for (auto g : graphs_) (void)hipGraphExecDestroy(g);
   graphs_.clear();
 }
 

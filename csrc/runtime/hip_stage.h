@@ -4,13 +4,16 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "kernels_api.h"
 #include "model.h"
 #include "qtypes.h"
+#include "stage.h"
 
 namespace mp {
 
@@ -22,15 +25,6 @@ class GgufFile;
     if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + \
                                                    " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
   } while (0)
-
-struct StageOptions {
-  int n_mb = 1;             // micro-batches in flight
-  int mb_size = 1;          // sequences per micro-batch
-  int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
-  int prefill_chunk = 256;  // max tokens per prefill chunk
-  bool use_graphs = true;
-  int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
-};
 
 // ggml types of the 2-D weights when initialising a synthetic model on device
 struct SyntheticTypes {
@@ -52,10 +46,11 @@ struct MatSeg {  // one launch of a (possibly merged) projection
 };
 
 struct ExpertW {  // MoE layer weights (Mixtral); experts stored back to back
-  uint8_t* gateup = nullptr; int gu_ptype = -1; PackedDims gu_dims{}; size_t gu_stride = 0;
-  uint8_t* down = nullptr; int dn_ptype = -1; PackedDims dn_dims{}; size_t dn_stride = 0;
-  float* router = nullptr;    // [E][d] f32
-  uint8_t* router_packed = nullptr; PackedMat router_m;
+  PackedMat gateup;            // E interleaved gate/up matrices, stride gateup_stride bytes
+  size_t gateup_stride = 0;
+  PackedMat down;              // E down matrices
+  size_t down_stride = 0;
+  PackedMat router;            // [E][d] router (f16 packed)
 };
 
 struct LayerW {
@@ -71,60 +66,62 @@ struct LayerW {
   ExpertW ex;
 };
 
-class HipStage {
+class HipStage : public Stage {
  public:
   HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOptions& opt);
-  ~HipStage();
+  ~HipStage() override;
 
-  void load_gguf(const GgufFile& f);
-  void init_synthetic(const std::string& ftype, uint64_t seed);
-  void alloc_runtime();   // KV cache, buffers, rope tables (after weights)
+  bool is_gpu() const override { return true; }
+  void load_gguf(const GgufFile& f) override;
+  void init_synthetic(const std::string& ftype, uint64_t seed) override;
+  void alloc_runtime() override;   // KV cache, buffers, rope tables (after weights)
 
-  const StageSpec& spec() const { return spec_; }
+  const StageSpec& spec() const override { return spec_; }
   const ModelConfig& cfg() const { return cfg_; }
-  hipStream_t stream() const { return stream_; }
+  hipStream_t stream() const override { return stream_; }
   int device() const { return spec_.device; }
 
-  // --- per micro-batch buffers (device) ---
-  float* act(int mb) { return act_[mb]; }          // [act_rows][d] f32 residual in/out
-  int32_t* tokens(int mb) { return tok_[mb]; }     // [mb_size] (first: input, last: output)
-  size_t act_bytes(int rows) const { return (size_t)rows * cfg_.d_model * sizeof(float); }
+  float* act(int mb) override { return act_[mb]; }          // [act_rows][d] f32 residual in/out
+  int32_t* tokens(int mb) override { return tok_[mb]; }     // [mb_size] (first: input, last: output)
+  int32_t* prompt_buf() override { return prompt_dev_; }
   int act_rows() const { return act_rows_; }
-
-  // --- sequence state ---
-  // set positions for micro-batch mb (host values) before decode; kvlen = pos + 1
-  void set_positions(int mb, const std::vector<int32_t>& pos, hipStream_t st);
   int slot_of(int mb, int b) const { return mb * opt_.mb_size + b; }
+
+  // positions of micro-batch mb (host values) before decode; kvlen = pos + 1
+  void set_positions(int mb, const std::vector<int32_t>& pos) override;
 
   // Prefill T tokens of sequence (mb, b) starting at position p0.  First stage: tokens_dev holds
   // the T token ids (device); otherwise act(mb) holds the incoming activations.  On the last
-  // stage and `last_chunk`, the greedy next token is written to tokens(mb)[b].
-  void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk, hipStream_t st);
+  // stage and `last_chunk`, the next token is written to tokens(mb)[b].
+  void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk,
+                     hipStream_t st) override;
 
   // One decode step for micro-batch mb (graph replay if captured).
-  void decode(int mb, hipStream_t st);
-  void capture_graphs();
+  void decode(int mb, hipStream_t st) override;
+  void capture_graphs() override;
   void destroy_graphs();
+  // sampling parameters are baked into the decode graphs: re-capture when they change
+  void set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) override;
 
-  // host prompt staging (pinned) for the first stage
-  int32_t* prompt_dev() { return prompt_dev_; }
-  int prompt_cap() const { return opt_.prefill_chunk; }
+  size_t weight_bytes() const override { return weight_bytes_; }
+  size_t kv_bytes() const override { return kv_bytes_; }
+  const float* logits_ptr() const override { return logits_; }
+  int logits_ld() const override { return logits_ld_; }
 
-  size_t weight_bytes() const { return weight_bytes_; }
-  size_t kv_bytes() const { return kv_bytes_; }
-  float* logits() { return logits_; }
-  int logits_ld() const { return logits_ld_; }
-
-  // reference decode body (no graph), exposed for tests
+  // decode body without graph (captured by capture_graphs)
   void decode_eager(int mb, hipStream_t st);
 
  private:
-  void layer_forward(int li, int M, int mb, float* x, const int32_t* pos, const int32_t* kvlen,
-                     const int32_t* slot, int tq, bool decode, hipStream_t st);
+  void layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* kvlen, const int32_t* slot,
+                     bool decode, hipStream_t st);
+  void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
             int n_valid, bool allow_split, hipStream_t st);
-  void head(int M, const float* x, int32_t* tok_out, hipStream_t st);
+  void head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
   PackedMat upload_packed(int ggml_type, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row);
+  // E matrices of N x K packed back to back (MoE experts); row(e, n)
+  PackedMat upload_packed_experts(int ggml_type, int E, int64_t N, int64_t K, size_t* stride,
+                                  const std::function<const uint8_t*(int, int64_t)>& row);
   PackedMat alloc_packed_random(int ggml_type, int64_t N, int64_t K, uint64_t seed);
   float* upload_f32(const float* h, size_t n);
   void* dmalloc(size_t bytes);
@@ -153,7 +150,7 @@ class HipStage {
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
   // MoE scratch
   float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
-  float* moe_w_ = nullptr; int32_t* moe_eid_ = nullptr; f16* moe_h_ = nullptr;
+  float* moe_w_ = nullptr; f16* moe_h_ = nullptr;
   // KV
   std::vector<f16*> kc_, vc_;
   int32_t* block_table_ = nullptr; int max_pages_ = 0;
@@ -165,7 +162,6 @@ class HipStage {
   int32_t* step_ = nullptr;
   // prefill metadata
   int32_t* pf_pos_ = nullptr; int32_t* pf_kvlen_ = nullptr; int32_t* pf_slot_ = nullptr;
-  int32_t* pf_host_ = nullptr;   // pinned staging
   int32_t* prompt_dev_ = nullptr;
   // graphs
   std::vector<hipGraphExec_t> graphs_;

@@ -111,12 +111,13 @@ void launch_f32_to_f16(const float* x, int ldx, int n, int M, f16* y, int ldy, h
 
 // MoE
 struct MoeRouteParams {
-  const float* logits;   // [M][E] router logits
-  int M, E, k;
+  const float* logits;   // [M][ld] router logits
+  int ld;
+  int M, E, k;           // E <= 64, k <= 8
   int32_t* counts;       // [E]
-  int32_t* lists;        // [E][M] token-slot ids (token*k + j)
-  float* weights;        // [M*k]
-  int32_t* expert_of;    // [M*k]
+  int32_t* lists;        // [E][list_cap] token-slot ids (token*k + j)
+  int list_cap;
+  float* weights;        // [M*k] renormalised top-k softmax weights
 };
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
 struct MoeGemvParams {
@@ -125,14 +126,15 @@ struct MoeGemvParams {
   int ntiles, nsb;
   const f16* X; int ldx; int x_per_slot;  // x row = x_per_slot ? slot : slot / k
   int k;
-  const int32_t* counts; const int32_t* lists;
-  int max_tok;           // max tokens per expert handled (<=16 per launch chunk)
+  const int32_t* counts; const int32_t* lists; int list_cap;
   int E;
   f16* H; int ldh;       // SWIGLU out per slot [M*k][ldh]
   float* Y; int ldy;     // down out: atomic add weight*y into Y[token]
   const float* weights;
   int n_valid;
+  int sb_per_split;      // set by the launcher
 };
-void launch_moe_gemv(int ptype, int epi, const MoeGemvParams& p, hipStream_t st);
+void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
+void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st);
 
 }  // namespace mp

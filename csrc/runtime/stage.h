@@ -1,0 +1,62 @@
+// Stage interface: one pipeline stage (contiguous layer range) on one device.
+//   HipStage: MI355X, hand-written HIP kernels, hipGraph decode (hip_stage.h)
+//   CpuStage: host reference / plumbing backend (BASELINE.json config 1: "single-stage via
+//             orchestrator on the CPU backend"; also the CPU test vehicle of the pipeline runtime)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace mp {
+
+class GgufFile;
+
+struct StageOptions {
+  int n_mb = 1;             // micro-batches in flight
+  int mb_size = 1;          // sequences per micro-batch
+  int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
+  int prefill_chunk = 256;  // max tokens per prefill chunk
+  bool use_graphs = true;
+  int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
+  int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
+};
+
+class Stage {
+ public:
+  virtual ~Stage() = default;
+  virtual bool is_gpu() const = 0;
+  virtual const StageSpec& spec() const = 0;
+  virtual hipStream_t stream() const = 0;                 // nullptr on CPU
+  virtual void load_gguf(const GgufFile& f) = 0;
+  virtual void init_synthetic(const std::string& ftype, uint64_t seed) = 0;
+  virtual void alloc_runtime() = 0;
+  virtual void capture_graphs() {}
+
+  // per micro-batch buffers (device memory for HIP, host memory for CPU)
+  virtual float* act(int mb) = 0;          // [rows][d] f32 residual in/out
+  virtual int32_t* tokens(int mb) = 0;     // [mb_size]
+  virtual int32_t* prompt_buf() = 0;       // [n_slots][max_ctx] token ids (first stage)
+  virtual void set_positions(int mb, const std::vector<int32_t>& pos) = 0;
+  virtual void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens, bool last_chunk,
+                             hipStream_t st) = 0;
+  virtual void decode(int mb, hipStream_t st) = 0;
+  virtual const float* logits_ptr() const = 0;   // last computed logits (device/host)
+  virtual int logits_ld() const = 0;
+  virtual size_t weight_bytes() const = 0;
+  virtual size_t kv_bytes() const = 0;
+  // sampling configuration for the last stage (temp <= 0: greedy)
+  virtual void set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) {
+    temp_ = temp; top_k_ = top_k; top_p_ = top_p; min_p_ = min_p; seed_ = seed;
+  }
+
+ protected:
+  float temp_ = 0.f, top_p_ = 1.f, min_p_ = 0.f;
+  int top_k_ = 0;
+  uint64_t seed_ = 0;
+};
+
+}  // namespace mp

@@ -30,12 +30,12 @@ LocalLink::LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_sl
   int cur = 0;
   HIP_OK(hipGetDevice(&cur));
   if (src_dev_ != dst_dev_) {
-    hipSetDevice(src_dev_);
-    hipDeviceEnablePeerAccess(dst_dev_, 0);
-    hipGetLastError();
-    hipSetDevice(dst_dev_);
-    hipDeviceEnablePeerAccess(src_dev_, 0);
-    hipGetLastError();
+    (void)hipSetDevice(src_dev_);
+    (void)hipDeviceEnablePeerAccess(dst_dev_, 0);
+    (void)hipGetLastError();
+    (void)hipSetDevice(dst_dev_);
+    (void)hipDeviceEnablePeerAccess(src_dev_, 0);
+    (void)hipGetLastError();
   }
   slots_.resize(n_slots);
   ready_.resize(n_slots);
@@ -54,9 +54,9 @@ LocalLink::LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_sl
 
 LocalLink::~LocalLink() {
   for (size_t i = 0; i < slots_.size(); ++i) {
-    hipFree(slots_[i]);
-    hipEventDestroy(ready_[i]);
-    hipEventDestroy(freed_[i]);
+    (void)hipFree(slots_[i]);
+    (void)hipEventDestroy(ready_[i]);
+    (void)hipEventDestroy(freed_[i]);
   }
 }
 
@@ -265,6 +265,40 @@ void TcpLink::recv(void* buf, size_t bytes, hipStream_t st) {
   } else {
     full_read(fd_, buf, bytes);
   }
+}
+
+}  // namespace mp
+
+namespace mp {
+
+// ---------------------------------------------------------------- HostLink
+void HostLink::send(const void* buf, size_t bytes, hipStream_t) {
+  std::vector<uint8_t> m((const uint8_t*)buf, (const uint8_t*)buf + bytes);
+  std::unique_lock<std::mutex> l(mu_);
+  if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || q_.size() < max_q_; }))
+    throw std::runtime_error("HostLink: send timed out (peer stalled)");
+  if (aborted_) throw std::runtime_error("HostLink: aborted");
+  q_.push_back(std::move(m));
+  bytes_sent += bytes;
+  ++msgs_sent;
+  cv_.notify_all();
+}
+
+void HostLink::recv(void* buf, size_t bytes, hipStream_t) {
+  std::unique_lock<std::mutex> l(mu_);
+  if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !q_.empty(); }))
+    throw std::runtime_error("HostLink: recv timed out (peer stalled)");
+  if (aborted_) throw std::runtime_error("HostLink: aborted");
+  if (q_.front().size() != bytes) throw std::runtime_error("HostLink: message size mismatch");
+  std::memcpy(buf, q_.front().data(), bytes);
+  q_.pop_front();
+  cv_.notify_all();
+}
+
+void HostLink::abort() {
+  std::lock_guard<std::mutex> l(mu_);
+  aborted_ = true;
+  cv_.notify_all();
 }
 
 }  // namespace mp

@@ -56,6 +56,24 @@ class LocalLink : public Link {
   bool aborted_ = false;
 };
 
+// ---------------------------------------------------------------- HostLink
+// same-process hand-off between CPU stages (copying FIFO of host messages)
+class HostLink : public Link {
+ public:
+  explicit HostLink(size_t max_queued = 64) : max_q_(max_queued) {}
+  void send(const void* buf, size_t bytes, hipStream_t st) override;
+  void recv(void* buf, size_t bytes, hipStream_t st) override;
+  const char* kind() const override { return "host"; }
+  void abort() override;
+
+ private:
+  std::deque<std::vector<uint8_t>> q_;
+  size_t max_q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool aborted_ = false;
+};
+
 // ---------------------------------------------------------------- RcclLink
 struct RcclComm;  // opaque (ncclComm_t)
 class RcclLink : public Link {
