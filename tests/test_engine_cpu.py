@@ -1,0 +1,143 @@
+"""CPU-backend engine tests (no GPU): the CpuStage model against the torch fp32 oracle, the
+pipeline runtime (multi-stage in one process over HostLinks, multi-process over TCP links),
+micro-batch invariance and seeded sampling.  These exercise the same scheduler/ring code the
+GPU path uses (engine.cpp), so the pipeline logic is covered on every CPU test run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO, make_model
+
+
+def nmse(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(((a - b) ** 2).sum() / ((b ** 2).sum() + 1e-30))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name,ftype", [("stories15m", "F32"), ("tiny-gqa", "Q8_0"), ("tiny-gqa", "Q4_K_M"),
+                                        ("tiny-l3", "Q6_K"), ("tiny-moe", "Q5_K_M"), ("tiny-gqa", "BF16")])
+def test_cpu_engine_matches_reference(native, model_dir, name, ftype):
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, name, ftype)
+    ref = RefLlama.from_gguf(path)
+    rng = np.random.default_rng(0)
+    prompt = [int(t) for t in rng.integers(3, cfg.vocab, 21)]
+    with Engine(gguf=path, backend="cpu", max_ctx=128, prefill_chunk=16, threads=4) as eng:
+        eng.start([prompt])
+        lg = eng.logits()[0]
+        ref.reset()
+        rl = ref.forward(prompt, 0)[-1].numpy()
+        assert nmse(lg, rl) < 1e-8, nmse(lg, rl)
+        pos = len(prompt)
+        for step in range(4):
+            tok = eng.tokens()[0][-1]
+            assert tok == int(rl.argmax()), step
+            eng.decode(1)
+            lg = eng.logits()[0]
+            rl = ref.forward([tok], pos)[-1].numpy()
+            pos += 1
+            assert nmse(lg, rl) < 1e-8, (step, nmse(lg, rl))
+
+
+@pytest.mark.parametrize("stages,n_mb", [(2, 2), (3, 3), (4, 1)])
+def test_cpu_pipeline_matches_pp1(native, model_dir, stages, n_mb):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(1)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 40, 3, 17, 5, 2)[: 2 * n_mb]]
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=1, mb_size=len(prompts), prefill_chunk=16) as eng:
+        ref_out, _ = eng.generate(prompts, 7)
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=n_mb, mb_size=2, prefill_chunk=16,
+                stages=stages, split="even") as eng:
+        assert len(eng.info["stages"]) == stages
+        out, _ = eng.generate(prompts, 7)
+        # a second generation on the same engine (ring drained, KV slots reused)
+        out2, _ = eng.generate(prompts[:1], 5)
+    assert out == ref_out
+    assert out2[0] == ref_out[0][:5]
+
+
+def test_cpu_microbatch_invariance(native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-moe", "Q8_0")
+    prompts = [[11, 12, 13], [400, 5, 6, 7, 8, 9, 10], [42]]
+    singles = []
+    with Engine(gguf=path, backend="cpu", max_ctx=64) as eng:
+        for p in prompts:
+            o, _ = eng.generate([p], 6)
+            singles.append(o[0])
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=2, mb_size=2) as eng:
+        o, _ = eng.generate(prompts, 6)
+    assert o == singles
+
+
+def test_cpu_sampling_seeded(native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts = [[5, 6, 7], [8, 9, 10, 11]]
+    outs = []
+    for seed in (7, 7, 8):
+        with Engine(gguf=path, backend="cpu", max_ctx=64, mb_size=2, temp=1.5, top_k=40, top_p=0.9,
+                    min_p=0.01, seed=seed) as eng:
+            o, _ = eng.generate(prompts, 12)
+            outs.append(o)
+    assert outs[0] == outs[1] and outs[0] != outs[2]
+    assert all(0 <= t < cfg.vocab for seq in outs[0] for t in seq)
+
+
+def test_cpu_synthetic_bench(native):
+    from mipipe.engine import Engine
+    syn = dict(n_layer=2, d_model=256, n_head=4, n_head_kv=2, d_ff=512, vocab=1024)
+    with Engine(synthetic=syn, backend="cpu", ftype="Q4_K_M", max_ctx=128, n_mb=2, mb_size=2, stages=2) as eng:
+        r = eng.bench(prompt_len=8, warmup=1, steps=4)
+    assert r["decode_tok_s"] > 0 and r["p50_ms"] > 0
+
+
+_MP_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+from mipipe.engine import Engine
+cfg = json.loads(sys.argv[1])
+with Engine(**cfg) as eng:
+    out, _ = eng.generate({prompts!r}, 7)
+    print("OUT " + json.dumps(out if cfg["rank"] == cfg["world"] - 1 else None), flush=True)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cpu_multiprocess_tcp_pipeline(native, model_dir, world):
+    """One process per stage (the torchrun layout of bench.py / mi-cli --world/--rank), TCP ring."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    prompts = [[3, 4, 5, 6], [7, 8], [9, 10, 11]]
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=3, mb_size=1) as eng:
+        ref_out, _ = eng.generate(prompts, 7)
+    port = free_port()
+    script = _MP_SCRIPT.format(repo=REPO, prompts=prompts)
+    procs = []
+    for r in range(world):
+        c = dict(gguf=path, backend="cpu", mode="mp", world=world, rank=r, link="tcp", base_port=port,
+                 max_ctx=64, n_mb=3, mb_size=1, split="even", threads=2)
+        procs.append(subprocess.Popen([sys.executable, "-c", script, json.dumps(c)], stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, cwd=REPO))
+    outs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, o[-3000:]
+        outs.append(o)
+    last = [l for l in outs[-1].splitlines() if l.startswith("OUT ")]
+    assert last and json.loads(last[0][4:]) == ref_out
