@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = #GPUs)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--link", default="rccl", choices=["rccl", "tcp"], help="stage-to-stage transport (N > 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,10 +68,15 @@ def main():
     cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
                prefill_chunk=256, graphs=not args.no_graphs, split="cost", seed=1234)
     if world > 1:
-        ids = [rccl_unique_id_hex() for _ in range(world)] if rank == 0 else None
-        obj = [ids]
-        dist.broadcast_object_list(obj, src=0)
-        cfg.update(mode="mp", world=world, rank=rank, device=local_rank, rccl_ids=obj[0])
+        cfg.update(mode="mp", world=world, rank=rank, device=local_rank, link=args.link)
+        if args.link == "rccl":
+            # link r = stage r -> stage (r+1) % N; its sender (rank r) creates the RCCL unique id,
+            # so every bootstrap root lives in a process that is a member of that communicator
+            ids = [None] * world
+            dist.all_gather_object(ids, rccl_unique_id_hex())
+            cfg["rccl_ids"] = ids
+        else:
+            cfg["base_port"] = int(os.environ.get("MASTER_PORT", "29500")) + 11
     else:
         cfg.update(mode="local", stages=1, devices=[local_rank])
 

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <numeric>
@@ -72,6 +73,10 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   if (j.has("log_file")) log_set_file(j.get_str("log_file", ""));
   mode_ = j.get_str("mode", "local");
   cpu_ = j.get_str("backend", "hip") == "cpu";
+  watchdog_s_ = j.get_num("watchdog_s", 600.0);
+  if (j.has("fault")) fault_ = j["fault"];
+  else if (const char* fe = std::getenv("MIPIPE_FAULT")) fault_ = Json::parse(fe);
+  if (j.get_bool("trace", false)) enable_trace(true);
   M_ = std::max(1, j.get_int("n_mb", 1));
   B_ = std::max(1, j.get_int("mb_size", 1));
   if (B_ > 16) throw std::runtime_error("mb_size > 16 not supported (decode micro-batch is one MFMA row tile)");
@@ -254,6 +259,7 @@ void Engine::build_links(const Json& j) {
     std::vector<std::string> hosts(S_, "127.0.0.1");
     if (j.has("hosts"))
       for (int r = 0; r < S_ && r < (int)j["hosts"].arr().size(); ++r) hosts[r] = j["hosts"].arr()[r].str();
+    if (j.has("next_host")) hosts[(rank_ + 1) % S_] = j.get_str("next_host", "127.0.0.1");   // prima.cpp --next
     const double to = j.get_num("connect_timeout", 120.0);
     const int in_l = (rank_ - 1 + S_) % S_, out_l = rank_;
     Worker& w = *workers_[0];
@@ -306,6 +312,44 @@ void Engine::post_ring_recv(Worker& w, int mb) {
   HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
 }
 
+// Fault injection: config "fault" (or env MIPIPE_FAULT, same JSON) =
+//   {"stage": k, "delay_ms": d}          sleep d ms before every item of stage k
+//   {"stage": k, "fail_at": n}           throw at the n-th item stage k runs
+//   {"stage": k, "drop_send_at": n}      silently skip the n-th send of stage k (peer stalls ->
+//                                        the watchdog / link timeouts must surface it)
+bool Engine::fault_hook(Worker& w, const char* what) {
+  if (!fault_.is_obj() || fault_.get_int("stage", -1) != w.stage->spec().stage) return false;
+  const long n = w.items_seen;
+  if (fault_.has("delay_ms")) std::this_thread::sleep_for(std::chrono::microseconds((long)(1000 * fault_.get_num("delay_ms", 0))));
+  if (std::strcmp(what, "item") == 0 && fault_.get_int("fail_at", -1) == n)
+    throw std::runtime_error("injected fault at item " + std::to_string(n) + " of stage " + std::to_string(w.stage->spec().stage));
+  if (std::strcmp(what, "send") == 0 && fault_.get_int("drop_send_at", -1) == w.sends_seen++) {
+    MP_LOGW("fault injection: dropping send %ld of stage %d", w.sends_seen - 1, w.stage->spec().stage);
+    return true;
+  }
+  return false;
+}
+
+// timeline span (Chrome trace, --trace): HIP events on stream s, or host time for CPU stages
+void Engine::span(Worker& w, hipStream_t s, int tid, const std::string& name, const std::function<void()>& body) {
+  if (!trace_) return body();
+  Worker::TraceRecT r;
+  r.name = name;
+  r.tid = tid;
+  if (cpu_) {
+    r.ta = now_ms();
+    body();
+    r.tb = now_ms();
+  } else {
+    HIP_OK(hipEventCreate(&r.a));
+    HIP_OK(hipEventRecord(r.a, s));
+    body();
+    HIP_OK(hipEventCreate(&r.b));
+    HIP_OK(hipEventRecord(r.b, s));
+  }
+  w.tr.push_back(r);
+}
+
 // CPU stages: the same item schedule, blocking host transfers.  The first stage receives the
 // ring token of micro-batch mb lazily (right before its next DECODE) and drains the ring at the
 // end of the item list, like the GPU path's posted ring receives.
@@ -313,49 +357,61 @@ void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
   Stage& st = *w.stage;
   const bool first = st.spec().first(), last = st.spec().last();
   const size_t d4 = (size_t)cfg_.d_model * 4;
+  auto recv = [&](int mb, void* buf, size_t bytes, const char* what) {
+    span(w, nullptr, 2, std::string("recv ") + what + " mb" + std::to_string(mb), [&] { w.in->recv(buf, bytes, nullptr); });
+  };
+  auto send = [&](int mb, const void* buf, size_t bytes, const char* what) {
+    if (fault_hook(w, "send")) return;
+    span(w, nullptr, 1, std::string("send ") + what + " mb" + std::to_string(mb), [&] { w.out->send(buf, bytes, nullptr); });
+  };
   for (const Item& it : items) {
     const int mb = it.mb;
+    fault_hook(w, "item");
+    ++w.items_seen;
     switch (it.kind) {
       case Item::PREFILL: {
-        if (!first) w.in->recv(st.act(mb), (size_t)it.T * d4, nullptr);
-        st.prefill_chunk(mb, it.b, it.p0, it.T,
-                         first ? st.prompt_buf() + (size_t)(mb * B_ + it.b) * max_ctx_ + it.p0 : nullptr,
-                         it.last_chunk, nullptr);
-        if (!last) w.out->send(st.act(mb), (size_t)it.T * d4, nullptr);
+        if (!first) recv(mb, st.act(mb), (size_t)it.T * d4, "act");
+        span(w, nullptr, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T), [&] {
+          st.prefill_chunk(mb, it.b, it.p0, it.T,
+                           first ? st.prompt_buf() + (size_t)(mb * B_ + it.b) * max_ctx_ + it.p0 : nullptr,
+                           it.last_chunk, nullptr);
+        });
+        if (!last) send(mb, st.act(mb), (size_t)it.T * d4, "act");
         break;
       }
       case Item::PREFILL_END: {
         if (last) std::memcpy(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4);
         if (S_ > 1) {
-          if (last) w.out->send(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          if (last) send(mb, st.tokens(mb), (size_t)B_ * 4, "tok");
           if (first) w.ring_pending[mb] = true;
         }
         break;
       }
       case Item::DECODE: {
-        if (!first) w.in->recv(st.act(mb), (size_t)B_ * d4, nullptr);
+        if (!first) recv(mb, st.act(mb), (size_t)B_ * d4, "act");
         else if (w.ring_pending[mb]) {
-          w.in->recv(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          recv(mb, st.tokens(mb), (size_t)B_ * 4, "tok");
           w.ring_pending[mb] = false;
         }
-        st.decode(mb, nullptr);
+        span(w, nullptr, 0, "decode mb" + std::to_string(mb), [&] { st.decode(mb, nullptr); });
         if (last) {
           w.tok_t.push_back(now_ms());
           std::memcpy(out_host_ + ((size_t)(it.round + 1) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4);
         }
         if (S_ > 1) {
-          if (!last) w.out->send(st.act(mb), (size_t)B_ * d4, nullptr);
-          else w.out->send(st.tokens(mb), (size_t)B_ * 4, nullptr);
+          if (!last) send(mb, st.act(mb), (size_t)B_ * d4, "act");
+          else send(mb, st.tokens(mb), (size_t)B_ * 4, "tok");
           if (first) w.ring_pending[mb] = true;
         }
         break;
       }
     }
+    ++w.progress;
   }
   if (first && S_ > 1)
     for (int mb = 0; mb < M_; ++mb)
       if (w.ring_pending[mb]) {
-        w.in->recv(st.tokens(mb), (size_t)B_ * 4, nullptr);
+        recv(mb, st.tokens(mb), (size_t)B_ * 4, "tok");
         w.ring_pending[mb] = false;
       }
 }
@@ -367,31 +423,43 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
   hipStream_t cs = st.stream();
   const bool first = st.spec().first(), last = st.spec().last();
   const size_t d4 = (size_t)cfg_.d_model * 4;
+  if (trace_ && !w.tr_base) {
+    HIP_OK(hipEventCreate(&w.tr_base));
+    HIP_OK(hipEventRecord(w.tr_base, cs));
+    HIP_OK(hipEventSynchronize(w.tr_base));
+    w.tr_base_ms = now_ms();
+  }
   auto recv_into = [&](int mb, void* buf, size_t bytes) {
     if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(w.recv_st, w.sent_ev[mb], 0));
     HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
     HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
-    w.in->recv(buf, bytes, w.recv_st);
+    span(w, w.recv_st, 2, "recv act mb" + std::to_string(mb), [&] { w.in->recv(buf, bytes, w.recv_st); });
     HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
     HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
   };
   auto send_from = [&](int mb, const void* buf, size_t bytes) {
+    if (fault_hook(w, "send")) return;
     HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
     HIP_OK(hipStreamWaitEvent(w.send_st, w.comp_ev[mb], 0));
-    w.out->send(buf, bytes, w.send_st);
+    span(w, w.send_st, 1, std::string(last ? "send tok" : "send act") + " mb" + std::to_string(mb),
+         [&] { w.out->send(buf, bytes, w.send_st); });
     HIP_OK(hipEventRecord(w.sent_ev[mb], w.send_st));
     w.sent_valid[mb] = true;
   };
   for (const Item& it : items) {
     const int mb = it.mb;
+    fault_hook(w, "item");
+    ++w.items_seen;
     switch (it.kind) {
       case Item::PREFILL: {
         const size_t bytes = (size_t)it.T * d4;
         if (!first) recv_into(mb, st.act(mb), bytes);
         else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
         const int slot = mb * B_ + it.b;
-        st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_buf() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
-                         it.last_chunk, cs);
+        span(w, cs, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T), [&] {
+          st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_buf() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
+                           it.last_chunk, cs);
+        });
         if (!last) send_from(mb, st.act(mb), bytes);
         break;
       }
@@ -408,7 +476,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         if (!first) recv_into(mb, st.act(mb), (size_t)B_ * d4);
         else if (S_ > 1) HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
         if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
-        st.decode(mb, cs);
+        span(w, cs, 0, "decode mb" + std::to_string(mb), [&] { st.decode(mb, cs); });
         if (last) {
           const size_t ev_i = (size_t)(it.round - rounds_done_) * M_ + mb;
           if (ev_i < w.tok_ev.size()) HIP_OK(hipEventRecord(w.tok_ev[ev_i], cs));
@@ -423,12 +491,18 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         break;
       }
     }
+    ++w.progress;
   }
 }
 
 void Engine::run_all(const std::vector<Item>& items) {
   if (workers_.size() == 1) {
-    run_items(*workers_[0], items);
+    try {
+      run_items(*workers_[0], items);
+    } catch (...) {
+      for (auto& l : links_) l->abort();
+      throw;
+    }
   } else {
     std::vector<std::thread> th;
     std::vector<std::exception_ptr> errs(workers_.size());
@@ -443,20 +517,118 @@ void Engine::run_all(const std::vector<Item>& items) {
       });
     for (auto& t : th) t.join();
     for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
+      if (e) {
+        failed_ = true;
+        std::rethrow_exception(e);
+      }
   }
   sync_all();
+  if (trace_) collect_trace();
 }
 
+void Engine::collect_trace() {
+  for (auto& wp : workers_) {
+    Worker& w = *wp;
+    const int pid = w.stage->spec().stage;
+    for (auto& r : w.tr) {
+      double ta = r.ta, tb = r.tb;
+      if (!cpu_) {
+        float ea = 0, eb = 0;
+        HIP_OK(hipEventElapsedTime(&ea, w.tr_base, r.a));
+        HIP_OK(hipEventElapsedTime(&eb, w.tr_base, r.b));
+        ta = w.tr_base_ms + ea;
+        tb = w.tr_base_ms + eb;
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+      }
+      Json e = Json::object();
+      e["name"] = r.name;
+      e["ph"] = "X";
+      e["pid"] = pid;
+      e["tid"] = r.tid;
+      e["ts"] = (ta - trace_t0_) * 1e3;
+      e["dur"] = std::max(0.0, (tb - ta) * 1e3);
+      trace_events_.push_back(e.dump());
+    }
+    w.tr.clear();
+  }
+}
+
+void Engine::enable_trace(bool on) {
+  trace_ = on;
+  if (on && trace_t0_ == 0) trace_t0_ = now_ms();
+}
+
+void Engine::write_trace(const std::string& path) const {
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) throw std::runtime_error("cannot write trace " + path);
+  fputs("{\"traceEvents\":[\n", f);
+  static const char* tnames[3] = {"compute", "send", "recv"};
+  bool firstl = true;
+  for (auto& wp : workers_)
+    for (int t = 0; t < 3; ++t) {
+      Json m = Json::object();
+      m["name"] = "thread_name";
+      m["ph"] = "M";
+      m["pid"] = wp->stage->spec().stage;
+      m["tid"] = t;
+      Json a = Json::object();
+      a["name"] = std::string(tnames[t]);
+      m["args"] = a;
+      fprintf(f, "%s%s", firstl ? "" : ",\n", m.dump().c_str());
+      firstl = false;
+    }
+  for (auto& e : trace_events_) {
+    fprintf(f, "%s%s", firstl ? "" : ",\n", e.c_str());
+    firstl = false;
+  }
+  fputs("\n]}\n", f);
+  fclose(f);
+}
+
+Json Engine::health() const {
+  Json j = Json::object();
+  j["ok"] = !failed_;
+  Json st = Json::array();
+  for (auto& w : workers_) {
+    Json o = Json::object();
+    o["stage"] = w->stage->spec().stage;
+    o["items_done"] = (int64_t)w->progress.load();
+    if (w->out) {
+      o["bytes_sent"] = (int64_t)w->out->bytes_sent;
+      o["msgs_sent"] = (int64_t)w->out->msgs_sent;
+      o["link"] = std::string(w->out->kind());
+    }
+    st.push(o);
+  }
+  j["stages"] = st;
+  return j;
+}
+
+// Stream drain with a watchdog: a peer that never sends (dead process, dropped
+// message) would otherwise hang hipStreamSynchronize on a posted receive forever.  After
+// `watchdog_s` without completion the links are aborted (ncclCommAbort for RCCL) and the
+// engine reports the stall.
 void Engine::sync_all() {
   if (cpu_) return;
+  const double deadline = now_ms() + watchdog_s_ * 1e3;
   for (auto& w : workers_) {
     HIP_OK(hipSetDevice(w->device));
-    HIP_OK(hipStreamSynchronize(w->stage->stream()));
-    HIP_OK(hipStreamSynchronize(w->send_st));
-    // the first stage keeps ring receives posted for the next round; they complete once the last
-    // stage sends, which it has (every DECODE / PREFILL_END sends), so this does not block forever
-    HIP_OK(hipStreamSynchronize(w->recv_st));
+    for (hipStream_t s : {w->stage->stream(), w->send_st, w->recv_st}) {
+      for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) HIP_OK(e);
+        if (now_ms() > deadline) {
+          failed_ = true;
+          for (auto& l : links_) l->abort();
+          throw std::runtime_error("pipeline watchdog: stage " + std::to_string(w->stage->spec().stage) +
+                                   " made no progress for " + std::to_string((int)watchdog_s_) +
+                                   " s (peer stalled or lost); links aborted");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
   }
 }
 

@@ -54,6 +54,8 @@ class Engine {
   int n_stages() const { return S_; }
   int n_mb() const { return M_; }
   int mb_size() const { return B_; }
+  int max_ctx() const { return max_ctx_; }
+  double load_ms() const { return load_ms_; }
   bool owns_last() const;
   bool owns_first() const;
 
@@ -68,6 +70,11 @@ class Engine {
                 std::vector<std::vector<int32_t>>* out);
   Json bench(int prompt_len, int warmup, int steps);
   int copy_logits(int mb, float* out, int rows);
+  // Chrome-trace timeline of compute / send / recv spans per stage
+  void enable_trace(bool on);
+  void write_trace(const std::string& path) const;
+  // heartbeat counters + link byte counters per owned stage; "ok" false after a fault
+  Json health() const;
 
   // streaming hook: called on the host (from the worker of the last stage) after each round
   // with (sequence index, token) pairs
@@ -84,12 +91,21 @@ class Engine {
     std::vector<hipEvent_t> tok_ev;   // last stage: per (round, mb) timing events
     std::vector<double> tok_t;        // CPU backend: host timestamps of the same
     std::vector<bool> ring_pending;   // CPU backend, first stage: ring token not yet received
+    std::atomic<long> progress{0};   // items completed (heartbeat)
+    long items_seen = 0, sends_seen = 0;
+    struct TraceRecT { std::string name; int tid = 0; hipEvent_t a = nullptr, b = nullptr; double ta = 0, tb = 0; };
+    std::vector<TraceRecT> tr;
+    hipEvent_t tr_base = nullptr;
+    double tr_base_ms = 0;
     int device = 0;
   };
 
   void build_links(const Json& cfg);
   void run_items(Worker& w, const std::vector<Item>& items);
   void run_items_cpu(Worker& w, const std::vector<Item>& items);
+  void span(Worker& w, hipStream_t s, int tid, const std::string& name, const std::function<void()>& body);
+  bool fault_hook(Worker& w, const char* what);
+  void collect_trace();
   void run_all(const std::vector<Item>& items);
   void post_ring_recv(Worker& w, int mb);
   void sync_all();
@@ -110,6 +126,10 @@ class Engine {
   int32_t* out_host_ = nullptr;                    // pinned [rounds_cap][M*B]
   std::vector<int32_t> out_vec_;                   // CPU backend storage of out_host_
   bool cpu_ = false;
+  bool trace_ = false, failed_ = false;
+  double trace_t0_ = 0, watchdog_s_ = 600;
+  std::vector<std::string> trace_events_;
+  Json fault_;
   int rounds_cap_ = 0, rounds_done_ = 0;
   bool started_ = false;
   double load_ms_ = 0;

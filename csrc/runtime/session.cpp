@@ -1,0 +1,138 @@
+#include "session.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+
+#include "gguf.h"
+#include "log.h"
+
+namespace mp {
+
+namespace {
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// complete-UTF-8 emitter per sequence
+struct Utf8Acc {
+  std::string buf;
+  std::string push(const std::string& b) {
+    buf += b;
+    size_t cut = buf.size();
+    for (size_t k = 1; k <= 4 && k <= buf.size(); ++k) {
+      const unsigned char c = (unsigned char)buf[buf.size() - k];
+      if ((c & 0xC0) == 0x80) continue;
+      const int need = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 1;
+      if (need > (int)k) cut = buf.size() - k;
+      break;
+    }
+    std::string o = buf.substr(0, cut);
+    buf.erase(0, cut);
+    return o;
+  }
+};
+}  // namespace
+
+Session::Session(Engine& eng, const std::string& gguf_path) : eng_(eng) {
+  if (!gguf_path.empty()) {
+    gguf_.reset(new GgufFile(gguf_path));
+    if (gguf_->get("tokenizer.ggml.tokens")) tok_.reset(new Tokenizer(Tokenizer::from_gguf(*gguf_)));
+  }
+  if (!tok_) MP_LOGW("no tokenizer in the model: using a byte-level stand-in (synthetic model)");
+}
+
+Session::~Session() = default;
+
+std::vector<int32_t> Session::encode(const std::string& text) const {
+  if (tok_) return tok_->encode(text, tok_->add_bos_default(), true);
+  std::vector<int32_t> o{1};
+  const int V = eng_.model().vocab;
+  for (unsigned char c : text) o.push_back((int32_t)((c + 3) % V));
+  return o;
+}
+
+std::string Session::piece(int32_t id) const {
+  if (tok_) return tok_->piece(id);
+  return "[" + std::to_string(id) + "]";
+}
+
+bool Session::is_eog(int32_t id) const { return tok_ && tok_->is_eog(id); }
+
+std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
+  if ((int)reqs.size() > capacity()) throw std::runtime_error("more requests than sequence slots");
+  std::vector<GenResult> res(reqs.size());
+  std::vector<std::vector<int32_t>> prompts(reqs.size());
+  const int max_ctx = eng_.max_ctx();
+  int max_prompt = 0;
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    prompts[i] = encode(reqs[i].prompt);
+    if ((int)prompts[i].size() >= max_ctx) {   // keep the tail (most recent context)
+      prompts[i].erase(prompts[i].begin(), prompts[i].end() - (max_ctx / 2));
+      MP_LOGW("prompt of sequence %zu truncated to %d tokens (context %d)", i, max_ctx / 2, max_ctx);
+    }
+    res[i].n_prompt = (int)prompts[i].size();
+    max_prompt = std::max(max_prompt, res[i].n_prompt);
+  }
+  int n_max = 0;
+  for (auto& r : reqs) n_max = std::max(n_max, r.n_predict);
+  n_max = std::max(0, std::min(n_max, max_ctx - max_prompt - 1));
+  // all ranks of a multi-process pipeline must run the same number of rounds: early stop only
+  // when this process owns the whole pipeline
+  const bool early_stop = eng_.owns_first() && eng_.owns_last();
+  const bool emit = eng_.owns_last();
+  std::vector<Utf8Acc> acc(reqs.size());
+  std::vector<bool> active(reqs.size(), true);
+  auto consume = [&](size_t i, int32_t t, int step) {
+    if (!active[i]) return;
+    GenResult& r = res[i];
+    if (step >= reqs[i].n_predict) { active[i] = false; r.stop = "length"; return; }
+    if (is_eog(t)) { active[i] = false; r.stop = "eog"; return; }
+    r.tokens.push_back(t);
+    r.n_gen++;
+    const std::string p = acc[i].push(piece(t));
+    r.text += p;
+    if (emit && !p.empty() && reqs[i].on_piece && !reqs[i].on_piece(p)) { active[i] = false; r.stop = "cancelled"; }
+  };
+  const double t0 = now_ms();
+  eng_.start(prompts);
+  const double t1 = now_ms();
+  if (n_max > 0)
+    for (size_t i = 0; i < reqs.size(); ++i) consume(i, eng_.tokens()[i].back(), 0);
+  int step = 1;
+  auto any_active = [&] { return std::any_of(active.begin(), active.end(), [](bool b) { return b; }); };
+  while (step < n_max && (!early_stop || any_active())) {
+    eng_.decode_steps(1);
+    const auto toks = eng_.tokens();
+    for (size_t i = 0; i < reqs.size(); ++i) consume(i, toks[i].back(), step);
+    ++step;
+  }
+  const double t2 = now_ms();
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    if (active[i]) res[i].stop = n_max < reqs[i].n_predict ? "context" : "length";
+    const std::string tail = acc[i].buf;
+    if (!tail.empty()) {
+      res[i].text += tail;
+      if (emit && active[i] && reqs[i].on_piece) reqs[i].on_piece(tail);
+    }
+    res[i].prefill_ms = t1 - t0;
+    res[i].decode_ms = t2 - t1;
+  }
+  return res;
+}
+
+std::string Session::perf_summary(const GenResult& r, double load_ms) {
+  char b[1024];
+  const int ng = std::max(0, r.n_gen - 1);   // the first token comes out of the prefill
+  snprintf(b, sizeof(b),
+           "mi_perf_context_print:        load time = %10.2f ms\n"
+           "mi_perf_context_print: prompt eval time = %10.2f ms / %5d tokens (%8.2f ms per token, %8.2f tokens per second)\n"
+           "mi_perf_context_print:        eval time = %10.2f ms / %5d runs   (%8.2f ms per token, %8.2f tokens per second)\n"
+           "mi_perf_context_print:       total time = %10.2f ms / %5d tokens\n",
+           load_ms, r.prefill_ms, r.n_prompt, r.prefill_ms / std::max(1, r.n_prompt),
+           1e3 * r.n_prompt / std::max(1e-9, r.prefill_ms), r.decode_ms, ng, r.decode_ms / std::max(1, ng),
+           1e3 * ng / std::max(1e-9, r.decode_ms), r.prefill_ms + r.decode_ms, r.n_prompt + r.n_gen);
+  return b;
+}
+
+}  // namespace mp

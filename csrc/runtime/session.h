@@ -1,0 +1,53 @@
+// Session = engine + tokenizer + the text-level generation loop shared by mi-cli and the
+// orchestrator (the role llama-cli's main loop plays for the reference):
+// tokenize, prefill, decode token by token, stream UTF-8-safe pieces, stop at end-of-generation
+// or n_predict, cancel on request (client disconnect), and the llama.cpp-style perf summary.
+#pragma once
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "tokenizer.h"
+
+namespace mp {
+
+struct GenRequest {
+  std::string prompt;
+  int n_predict = 200;
+  // receives text pieces (complete UTF-8); return false to cancel this sequence
+  std::function<bool(const std::string& piece)> on_piece;
+};
+
+struct GenResult {
+  int n_prompt = 0, n_gen = 0;
+  double prefill_ms = 0, decode_ms = 0;
+  std::string text;
+  std::string stop;   // "eog" | "length" | "cancelled" | "context"
+  std::vector<int32_t> tokens;
+};
+
+class Session {
+ public:
+  // gguf may be empty (synthetic model: byte-level stand-in tokenizer)
+  Session(Engine& eng, const std::string& gguf_path);
+  ~Session();
+  Engine& engine() { return eng_; }
+  int capacity() const { return eng_.n_mb() * eng_.mb_size(); }
+  std::vector<int32_t> encode(const std::string& text) const;
+  std::string piece(int32_t id) const;
+  bool is_eog(int32_t id) const;
+
+  // runs up to capacity() requests together (one sequence slot each)
+  std::vector<GenResult> run(std::vector<GenRequest>& reqs);
+  // llama.cpp-style summary lines (prompt eval / eval / total)
+  static std::string perf_summary(const GenResult& r, double load_ms);
+
+ private:
+  Engine& eng_;
+  std::unique_ptr<GgufFile> gguf_;
+  std::unique_ptr<Tokenizer> tok_;
+};
+
+}  // namespace mp

@@ -27,6 +27,7 @@ class Tokenizer {
 
   int n_vocab() const { return (int)tokens_.size(); }
   int bos() const { return bos_; }
+  bool add_bos_default() const { return add_bos_default_; }
   int eos() const { return eos_; }
   int eot() const { return eot_; }
   Kind kind() const { return kind_; }

@@ -88,7 +88,8 @@ class RcclLink : public Link {
 
  private:
   void* comm_;
-  int rank_, dev_;
+  int rank_;
+  [[maybe_unused]] int dev_;
 };
 
 // creates the two ends of a link between devices a -> b inside one process (ncclCommInitAll)

@@ -1,0 +1,696 @@
+// orchestrator: the HTTP front-end (reference `orchestrator/src/main.rs`, SURVEY.md C1-C10, D5, D7,
+// D12), C++ instead of Rust/axum and with the engine IN-PROCESS: the model is loaded once at
+// start-up (the reference spawns a fresh llama-cli per request and reloads the GGUF every time,
+// `main.rs:35-57`).
+//
+//   POST /chat        {"prompt": str, "n_predict"?: int} -> text/event-stream of
+//                     data: {"msg_type": "log"|"token", "content": str}   (main.rs:23-27,97)
+//                     keep-alive comment every 1 s (main.rs:97); generation is cancelled when the
+//                     client disconnects (the reference lets the child run on, main.rs:77,91)
+//   POST /completion  {"prompt", "n_predict"} -> {"content", "response", "tokens_predicted", ...}
+//                     (the PDF's proxy design, p.9-10, llama-server style)
+//   GET  /metrics     Prometheus text (requests, tokens, tok/s, p50/p90/p99 per token, stage
+//                     heartbeats, link bytes)
+//   GET  /health      engine health JSON
+//   GET  /*           static files (default ./static, index.html at /) (main.rs:104)
+//   CORS: Access-Control-Allow-Origin * on every response, OPTIONS preflight (main.rs:105)
+//   errors as axum's Json extractor: 415 (not application/json), 400 (bad JSON), 422 (no
+//   "prompt" string), 405 (wrong method), 404; optional --api-key (401) and --rate-limit (429)
+//
+// Concurrency: connection thread per client; one generation thread batches up to
+// n_mb * mb_size queued requests into one engine run (request-level batching).
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cli_common.h"
+#include "engine.h"
+#include "log.h"
+#include "session.h"
+
+using namespace mp;
+
+namespace {
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ------------------------------------------------------------------ events / jobs
+struct Event {
+  std::string type;      // "log" | "token" | "end"
+  std::string content;
+};
+
+struct Job {
+  std::string prompt;
+  int n_predict = 200;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Event> q;
+  bool done = false;
+  std::atomic<bool> cancelled{false};
+  GenResult result;
+  void push(Event e) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      q.push_back(std::move(e));
+    }
+    cv.notify_all();
+  }
+  void finish() {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      done = true;
+    }
+    cv.notify_all();
+  }
+};
+
+struct Metrics {
+  std::mutex mu;
+  uint64_t requests = 0, completed = 0, cancelled = 0, errors = 0, prompt_tokens = 0, gen_tokens = 0;
+  double last_decode_tok_s = 0, last_prefill_tok_s = 0;
+  std::vector<double> token_ms;   // recent per-token latencies
+  void add_latency(double ms) {
+    token_ms.push_back(ms);
+    if (token_ms.size() > 4096) token_ms.erase(token_ms.begin(), token_ms.begin() + 2048);
+  }
+};
+
+double pctl(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1) + 0.5))];
+}
+
+// ------------------------------------------------------------------ server state
+struct Server {
+  std::unique_ptr<Engine> eng;
+  std::unique_ptr<Session> sess;
+  bool mock = false;
+  int mock_delay_ms = 2;
+  int capacity = 1;
+  int default_n = 200;
+  std::string static_dir = "static";
+  std::string api_key;
+  int rate_limit = 0;   // requests per minute per client IP (0 = off)
+  std::mutex rl_mu;
+  std::map<std::string, std::deque<double>> rl_hist;
+  std::vector<std::string> startup_logs;
+  std::mutex jobs_mu;
+  std::condition_variable jobs_cv;
+  std::deque<std::shared_ptr<Job>> pending;
+  std::vector<std::shared_ptr<Job>> active;
+  std::mutex active_mu;
+  Metrics metrics;
+  std::atomic<bool> stop{false};
+  std::atomic<int> connections{0};
+};
+
+Server* g_srv = nullptr;
+
+void broadcast_log(const std::string& line) {
+  if (!g_srv) return;
+  std::lock_guard<std::mutex> l(g_srv->active_mu);
+  for (auto& j : g_srv->active) j->push({"log", line});
+}
+
+// mock generation (no model): echoes words for API tests (SURVEY.md T6 "mock engine")
+GenResult mock_run(Job& j, int delay_ms) {
+  GenResult r;
+  r.n_prompt = (int)j.prompt.size();
+  std::vector<std::string> words = {" once", " upon", " a", " time", " there", " was", " a", " pipeline", ".",
+                                    " \xc3\xa7", "\xc4\x9f", " \xf0\x9f\x9a\x80"};
+  const double t0 = now_ms();
+  for (int i = 0; i < j.n_predict; ++i) {
+    if (j.cancelled) { r.stop = "cancelled"; break; }
+    const std::string& w = words[i % words.size()];
+    r.text += w;
+    r.n_gen++;
+    j.push({"token", w});
+    std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
+  }
+  if (r.stop.empty()) r.stop = "length";
+  r.decode_ms = now_ms() - t0;
+  return r;
+}
+
+void generation_loop(Server& S) {
+  while (!S.stop) {
+    std::vector<std::shared_ptr<Job>> batch;
+    {
+      std::unique_lock<std::mutex> l(S.jobs_mu);
+      S.jobs_cv.wait_for(l, std::chrono::milliseconds(200), [&] { return !S.pending.empty() || S.stop; });
+      while (!S.pending.empty() && (int)batch.size() < S.capacity) {
+        batch.push_back(S.pending.front());
+        S.pending.pop_front();
+      }
+    }
+    if (batch.empty()) continue;
+    {
+      std::lock_guard<std::mutex> l(S.active_mu);
+      S.active = batch;
+    }
+    for (auto& j : batch) {
+      j->push({"log", "orchestrator: request accepted (" + std::to_string(batch.size()) + " in this batch)\n"});
+      for (auto& s : S.startup_logs) j->push({"log", s});
+    }
+    try {
+      std::vector<GenResult> res;
+      if (S.mock) {
+        for (auto& j : batch) res.push_back(mock_run(*j, S.mock_delay_ms));
+      } else {
+        std::vector<GenRequest> reqs(batch.size());
+        for (size_t i = 0; i < batch.size(); ++i) {
+          reqs[i].prompt = batch[i]->prompt;
+          reqs[i].n_predict = batch[i]->n_predict;
+          Job* jp = batch[i].get();
+          reqs[i].on_piece = [jp](const std::string& p) {
+            if (jp->cancelled) return false;
+            jp->push({"token", p});
+            return true;
+          };
+        }
+        res = S.sess->run(reqs);
+      }
+      for (size_t i = 0; i < batch.size(); ++i) {
+        auto& j = batch[i];
+        j->result = res[i];
+        const std::string perf = Session::perf_summary(res[i], S.eng ? S.eng->load_ms() : 0.0);
+        j->push({"log", perf});
+        fputs(perf.c_str(), stderr);
+        std::lock_guard<std::mutex> l(S.metrics.mu);
+        S.metrics.completed++;
+        if (res[i].stop == "cancelled") S.metrics.cancelled++;
+        S.metrics.prompt_tokens += res[i].n_prompt;
+        S.metrics.gen_tokens += res[i].n_gen;
+        if (res[i].decode_ms > 0 && res[i].n_gen > 1) {
+          S.metrics.last_decode_tok_s = (res[i].n_gen - 1) * 1e3 / res[i].decode_ms;
+          S.metrics.add_latency(res[i].decode_ms / (res[i].n_gen - 1));
+        }
+        if (res[i].prefill_ms > 0) S.metrics.last_prefill_tok_s = res[i].n_prompt * 1e3 / res[i].prefill_ms;
+      }
+    } catch (const std::exception& e) {
+      MP_LOGE("generation failed: %s", e.what());
+      std::lock_guard<std::mutex> l(S.metrics.mu);
+      S.metrics.errors += batch.size();
+      for (auto& j : batch) j->push({"log", std::string("error: ") + e.what() + "\n"});
+    }
+    {
+      std::lock_guard<std::mutex> l(S.active_mu);
+      S.active.clear();
+    }
+    for (auto& j : batch) j->finish();
+  }
+}
+
+// ------------------------------------------------------------------ HTTP
+struct Request {
+  std::string method, path, query, version;
+  std::map<std::string, std::string> headers;   // lower-case keys
+  std::string body;
+  std::string peer;
+  std::string header(const std::string& k) const {
+    auto it = headers.find(k);
+    return it == headers.end() ? "" : it->second;
+  }
+};
+
+bool write_all(int fd, const std::string& s) {
+  size_t off = 0;
+  while (off < s.size()) {
+    ssize_t w = ::send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+    if (w <= 0) return false;
+    off += (size_t)w;
+  }
+  return true;
+}
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+
+const char* status_text(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 413: return "Payload Too Large";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    case 429: return "Too Many Requests";
+    case 500: return "Internal Server Error";
+    case 503: return "Service Unavailable";
+  }
+  return "Unknown";
+}
+
+const char* kCors =
+    "Access-Control-Allow-Origin: *\r\n"
+    "Access-Control-Allow-Methods: GET, POST, OPTIONS\r\n"
+    "Access-Control-Allow-Headers: *\r\n";
+
+void respond(int fd, int code, const std::string& ctype, const std::string& body, const std::string& extra = "") {
+  std::string h = "HTTP/1.1 " + std::to_string(code) + " " + status_text(code) + "\r\n";
+  if (!ctype.empty()) h += "Content-Type: " + ctype + "\r\n";
+  h += "Content-Length: " + std::to_string(body.size()) + "\r\n";
+  h += kCors;
+  h += extra;
+  h += "Connection: close\r\n\r\n";
+  write_all(fd, h + body);
+}
+
+void respond_text(int fd, int code, const std::string& msg) { respond(fd, code, "text/plain; charset=utf-8", msg); }
+
+bool read_request(int fd, Request& r) {
+  std::string buf;
+  char tmp[8192];
+  size_t hdr_end = std::string::npos;
+  while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
+    ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (n <= 0) return false;
+    buf.append(tmp, (size_t)n);
+    if (buf.size() > (1 << 20)) return false;
+  }
+  const std::string head = buf.substr(0, hdr_end);
+  r.body = buf.substr(hdr_end + 4);
+  size_t eol = head.find("\r\n");
+  const std::string line = head.substr(0, eol);
+  size_t a = line.find(' '), b = line.rfind(' ');
+  if (a == std::string::npos || b == a) return false;
+  r.method = line.substr(0, a);
+  std::string target = line.substr(a + 1, b - a - 1);
+  r.version = line.substr(b + 1);
+  const size_t q = target.find('?');
+  r.path = target.substr(0, q);
+  if (q != std::string::npos) r.query = target.substr(q + 1);
+  size_t pos = eol == std::string::npos ? head.size() : eol + 2;
+  while (pos < head.size()) {
+    size_t e = head.find("\r\n", pos);
+    if (e == std::string::npos) e = head.size();
+    const std::string h = head.substr(pos, e - pos);
+    const size_t c = h.find(':');
+    if (c != std::string::npos) {
+      std::string v = h.substr(c + 1);
+      while (!v.empty() && (v[0] == ' ' || v[0] == '\t')) v.erase(0, 1);
+      r.headers[lower(h.substr(0, c))] = v;
+    }
+    pos = e + 2;
+  }
+  const size_t cl = r.header("content-length").empty() ? 0 : std::stoul(r.header("content-length"));
+  if (cl > (8u << 20)) return false;
+  while (r.body.size() < cl) {
+    ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (n <= 0) return false;
+    r.body.append(tmp, (size_t)n);
+  }
+  r.body.resize(cl);
+  return true;
+}
+
+std::string mime_of(const std::string& p) {
+  auto ends = [&](const char* s) { return p.size() >= strlen(s) && p.compare(p.size() - strlen(s), strlen(s), s) == 0; };
+  if (ends(".html") || ends(".htm")) return "text/html; charset=utf-8";
+  if (ends(".js")) return "application/javascript";
+  if (ends(".css")) return "text/css";
+  if (ends(".json")) return "application/json";
+  if (ends(".png")) return "image/png";
+  if (ends(".svg")) return "image/svg+xml";
+  if (ends(".ico")) return "image/x-icon";
+  return "application/octet-stream";
+}
+
+void serve_static(Server& S, int fd, const Request& r) {
+  std::string p = r.path == "/" ? "/index.html" : r.path;
+  if (p.find("..") != std::string::npos) return respond_text(fd, 404, "Not Found");
+  const std::string full = S.static_dir + p;
+  struct stat stt;
+  if (stat(full.c_str(), &stt) != 0 || !S_ISREG(stt.st_mode)) return respond_text(fd, 404, "Not Found");
+  try {
+    const std::string body = read_file(full);
+    respond(fd, 200, mime_of(full), r.method == "HEAD" ? "" : body);
+  } catch (...) {
+    respond_text(fd, 404, "Not Found");
+  }
+}
+
+// axum Json<ChatRequest> extractor semantics (main.rs:18-21)
+bool parse_prompt_body(int fd, const Request& r, std::string* prompt, int* n_predict, int def_n) {
+  if (lower(r.header("content-type")).find("application/json") == std::string::npos) {
+    respond_text(fd, 415, "Expected request with `Content-Type: application/json`");
+    return false;
+  }
+  Json j;
+  try {
+    j = Json::parse(r.body);
+  } catch (const std::exception& e) {
+    respond_text(fd, 400, std::string("Failed to parse the request body as JSON: ") + e.what());
+    return false;
+  }
+  if (!j.is_obj() || !j.has("prompt") || !j["prompt"].is_str()) {
+    respond_text(fd, 422, "Failed to deserialize the JSON body into the target type: missing field `prompt`");
+    return false;
+  }
+  *prompt = j["prompt"].str();
+  *n_predict = j.get_int("n_predict", def_n);
+  if (*n_predict < 0) *n_predict = def_n;
+  return true;
+}
+
+bool authorized(Server& S, int fd, const Request& r) {
+  if (!S.api_key.empty()) {
+    const std::string a = r.header("authorization"), k = r.header("x-api-key");
+    if (a != "Bearer " + S.api_key && k != S.api_key) {
+      respond_text(fd, 401, "Unauthorized");
+      return false;
+    }
+  }
+  if (S.rate_limit > 0) {
+    std::lock_guard<std::mutex> l(S.rl_mu);
+    auto& h = S.rl_hist[r.peer];
+    const double t = now_ms();
+    while (!h.empty() && t - h.front() > 60000) h.pop_front();
+    if ((int)h.size() >= S.rate_limit) {
+      respond(fd, 429, "text/plain; charset=utf-8", "Too Many Requests", "Retry-After: 60\r\n");
+      return false;
+    }
+    h.push_back(t);
+  }
+  return true;
+}
+
+std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n) {
+  auto job = std::make_shared<Job>();
+  job->prompt = prompt;
+  job->n_predict = n;
+  {
+    std::lock_guard<std::mutex> l(S.metrics.mu);
+    S.metrics.requests++;
+  }
+  printf("request: %s\n", prompt.c_str());   // reference main.rs:32 request log
+  fflush(stdout);
+  {
+    std::lock_guard<std::mutex> l(S.jobs_mu);
+    S.pending.push_back(job);
+  }
+  S.jobs_cv.notify_all();
+  return job;
+}
+
+std::string sse_event(const Event& e) {
+  Json m = Json::object();
+  m["msg_type"] = e.type;
+  m["content"] = e.content;
+  return "data: " + m.dump() + "\n\n";
+}
+
+std::string chunk(const std::string& s) {
+  char h[32];
+  snprintf(h, sizeof(h), "%zx\r\n", s.size());
+  return std::string(h) + s + "\r\n";
+}
+
+void handle_chat(Server& S, int fd, const Request& r) {
+  std::string prompt;
+  int n = S.default_n;
+  if (!parse_prompt_body(fd, r, &prompt, &n, S.default_n)) return;
+  auto job = submit(S, prompt, n);
+  std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/event-stream\r\nCache-Control: no-cache\r\n";
+  h += kCors;
+  h += "Transfer-Encoding: chunked\r\nConnection: close\r\n\r\n";
+  if (!write_all(fd, h)) { job->cancelled = true; return; }
+  double last = now_ms();
+  for (;;) {
+    std::vector<Event> evs;
+    bool done;
+    {
+      std::unique_lock<std::mutex> l(job->mu);
+      job->cv.wait_for(l, std::chrono::milliseconds(100), [&] { return !job->q.empty() || job->done; });
+      while (!job->q.empty()) {
+        evs.push_back(std::move(job->q.front()));
+        job->q.pop_front();
+      }
+      done = job->done;
+    }
+    std::string out;
+    for (auto& e : evs) out += sse_event(e);
+    if (out.empty() && now_ms() - last >= 1000.0) out = ":\n\n";   // keep-alive (main.rs:97)
+    if (!out.empty()) {
+      if (!write_all(fd, chunk(out))) {   // client went away: stop generating for it
+        job->cancelled = true;
+        return;
+      }
+      last = now_ms();
+    }
+    if (done && evs.empty()) break;
+  }
+  write_all(fd, "0\r\n\r\n");
+}
+
+void handle_completion(Server& S, int fd, const Request& r) {
+  std::string prompt;
+  int n = 128;   // PDF p.10: n_predict 128
+  if (!parse_prompt_body(fd, r, &prompt, &n, 128)) return;
+  auto job = submit(S, prompt, n);
+  {
+    std::unique_lock<std::mutex> l(job->mu);
+    job->cv.wait(l, [&] { return job->done; });
+  }
+  const GenResult& g = job->result;
+  Json o = Json::object();
+  o["content"] = g.text;
+  o["response"] = g.text;
+  o["tokens_predicted"] = g.n_gen;
+  o["tokens_evaluated"] = g.n_prompt;
+  o["stop_reason"] = g.stop;
+  Json t = Json::object();
+  t["prompt_ms"] = g.prefill_ms;
+  t["predicted_ms"] = g.decode_ms;
+  t["predicted_per_second"] = g.n_gen > 1 && g.decode_ms > 0 ? (g.n_gen - 1) * 1e3 / g.decode_ms : 0.0;
+  o["timings"] = t;
+  respond(fd, 200, "application/json", o.dump());
+}
+
+void handle_metrics(Server& S, int fd) {
+  std::string m;
+  char b[512];
+  {
+    std::lock_guard<std::mutex> l(S.metrics.mu);
+    auto& M = S.metrics;
+    snprintf(b, sizeof(b),
+             "# TYPE mipipe_requests_total counter\nmipipe_requests_total %llu\n"
+             "# TYPE mipipe_requests_completed_total counter\nmipipe_requests_completed_total %llu\n"
+             "# TYPE mipipe_requests_cancelled_total counter\nmipipe_requests_cancelled_total %llu\n"
+             "# TYPE mipipe_request_errors_total counter\nmipipe_request_errors_total %llu\n"
+             "# TYPE mipipe_prompt_tokens_total counter\nmipipe_prompt_tokens_total %llu\n"
+             "# TYPE mipipe_generated_tokens_total counter\nmipipe_generated_tokens_total %llu\n",
+             (unsigned long long)M.requests, (unsigned long long)M.completed, (unsigned long long)M.cancelled,
+             (unsigned long long)M.errors, (unsigned long long)M.prompt_tokens, (unsigned long long)M.gen_tokens);
+    m += b;
+    snprintf(b, sizeof(b),
+             "# TYPE mipipe_decode_tokens_per_second gauge\nmipipe_decode_tokens_per_second %.3f\n"
+             "# TYPE mipipe_prefill_tokens_per_second gauge\nmipipe_prefill_tokens_per_second %.3f\n"
+             "# TYPE mipipe_token_latency_ms summary\n"
+             "mipipe_token_latency_ms{quantile=\"0.5\"} %.4f\nmipipe_token_latency_ms{quantile=\"0.9\"} %.4f\n"
+             "mipipe_token_latency_ms{quantile=\"0.99\"} %.4f\n",
+             M.last_decode_tok_s, M.last_prefill_tok_s, pctl(M.token_ms, 0.5), pctl(M.token_ms, 0.9),
+             pctl(M.token_ms, 0.99));
+    m += b;
+  }
+  {
+    std::lock_guard<std::mutex> l(S.jobs_mu);
+    snprintf(b, sizeof(b), "# TYPE mipipe_queue_depth gauge\nmipipe_queue_depth %zu\n", S.pending.size());
+    m += b;
+  }
+  snprintf(b, sizeof(b), "# TYPE mipipe_open_connections gauge\nmipipe_open_connections %d\n", S.connections.load());
+  m += b;
+  if (S.eng) {
+    Json h = S.eng->health();
+    m += "# TYPE mipipe_stage_items_done counter\n";
+    for (auto& st : h["stages"].arr()) {
+      snprintf(b, sizeof(b), "mipipe_stage_items_done{stage=\"%d\"} %lld\n", (int)st["stage"].num(),
+               (long long)st.get_num("items_done", 0));
+      m += b;
+    }
+    m += "# TYPE mipipe_link_bytes_sent counter\n";
+    for (auto& st : h["stages"].arr())
+      if (st.has("bytes_sent")) {
+        snprintf(b, sizeof(b), "mipipe_link_bytes_sent{stage=\"%d\",link=\"%s\"} %lld\n", (int)st["stage"].num(),
+                 st.get_str("link", "").c_str(), (long long)st.get_num("bytes_sent", 0));
+        m += b;
+      }
+    snprintf(b, sizeof(b), "# TYPE mipipe_engine_ok gauge\nmipipe_engine_ok %d\n", h.get_bool("ok", false) ? 1 : 0);
+    m += b;
+  }
+  respond(fd, 200, "text/plain; version=0.0.4", m);
+}
+
+void handle_conn(Server& S, int fd, std::string peer) {
+  S.connections++;
+  Request r;
+  r.peer = peer;
+  if (read_request(fd, r)) {
+    try {
+      if (r.method == "OPTIONS") {
+        respond(fd, 204, "", "");
+      } else if (r.path == "/chat") {
+        if (r.method != "POST") respond(fd, 405, "text/plain; charset=utf-8", "Method Not Allowed", "Allow: POST\r\n");
+        else if (authorized(S, fd, r)) handle_chat(S, fd, r);
+      } else if (r.path == "/completion") {
+        if (r.method != "POST") respond(fd, 405, "text/plain; charset=utf-8", "Method Not Allowed", "Allow: POST\r\n");
+        else if (authorized(S, fd, r)) handle_completion(S, fd, r);
+      } else if (r.path == "/metrics" && r.method == "GET") {
+        handle_metrics(S, fd);
+      } else if (r.path == "/health" && r.method == "GET") {
+        Json h = S.eng ? S.eng->health() : Json::object();
+        if (!S.eng) h["ok"] = true;
+        h["mock"] = S.mock;
+        respond(fd, 200, "application/json", h.dump());
+      } else if (r.method == "GET" || r.method == "HEAD") {
+        serve_static(S, fd, r);
+      } else {
+        respond_text(fd, 405, "Method Not Allowed");
+      }
+    } catch (const std::exception& e) {
+      respond_text(fd, 500, e.what());
+    }
+  }
+  ::shutdown(fd, SHUT_RDWR);
+  ::close(fd);
+  S.connections--;
+}
+
+void usage() {
+  fprintf(stderr, "usage: orchestrator (-m MODEL.gguf | --synthetic NAME | --mock) [--port 3005] [--host 0.0.0.0]\n"
+                  "                    [--static DIR] [--api-key KEY] [--rate-limit N/min] [engine flags]\n");
+  print_common_usage(stderr);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  signal(SIGPIPE, SIG_IGN);
+  Server S;
+  g_srv = &S;
+  int port = 3005;   // main.rs:107
+  std::string host = "0.0.0.0";
+  bool mock = false;
+  CliOptions o;
+  std::vector<char*> args(argv, argv + argc);
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--mock")) mock = true;
+  try {
+    auto extra = [&](const std::string& a, const std::function<std::string()>& val) {
+      if (a == "--port") port = std::atoi(val().c_str());
+      else if (a == "--host") host = val();
+      else if (a == "--static") S.static_dir = val();
+      else if (a == "--api-key") S.api_key = val();
+      else if (a == "--rate-limit") S.rate_limit = std::atoi(val().c_str());
+      else if (a == "--mock") {}
+      else if (a == "--mock-delay-ms") S.mock_delay_ms = std::atoi(val().c_str());
+      else if (a == "-h" || a == "--help") { usage(); exit(0); }
+      else return false;
+      return true;
+    };
+    if (mock) {
+      // model flags optional in mock mode
+      std::vector<char*> a2{argv[0], (char*)"--synthetic", (char*)"stories15m"};
+      for (int i = 1; i < argc; ++i) a2.push_back(argv[i]);
+      o = parse_cli((int)a2.size(), a2.data(), extra);
+    } else {
+      o = parse_cli(argc, argv, extra);
+    }
+  } catch (const std::exception& e) {
+    fprintf(stderr, "orchestrator: %s\n", e.what());
+    usage();
+    return 2;
+  }
+  S.mock = mock;
+  S.default_n = o.n_predict;
+  {
+    struct stat stt;
+    if (stat(S.static_dir.c_str(), &stt) != 0) {   // fall back to the package's static/ next to bin/
+      char exe[4096];
+      const ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+      if (n > 0) {
+        exe[n] = 0;
+        std::string d(exe);
+        d = d.substr(0, d.rfind('/'));
+        d = d.substr(0, d.rfind('/')) + "/static";
+        if (stat(d.c_str(), &stt) == 0) S.static_dir = d;
+      }
+    }
+  }
+  // capture start-up logs (placement / offload lines) to replay to every request's log pane
+  log_set_callback([&S](const std::string& line) {
+    if (!S.eng && !S.mock) S.startup_logs.push_back(line);
+    else broadcast_log(line);
+  });
+  try {
+    if (!mock) {
+      if (!o.eng.has("mb_size")) o.eng["mb_size"] = 4;
+      S.eng.reset(new Engine(o.eng));
+      S.sess.reset(new Session(*S.eng, o.eng.get_str("gguf", "")));
+      S.capacity = S.sess->capacity();
+    } else {
+      S.startup_logs.push_back("mock engine: stage 0: layers 0-5 offloaded to GPU 0 (mock)\n");
+      S.capacity = 4;
+    }
+  } catch (const std::exception& e) {
+    MP_LOGE("orchestrator: engine init failed: %s", e.what());
+    return 1;
+  }
+  int ls = socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons((uint16_t)port);
+  if (inet_pton(AF_INET, host.c_str(), &addr.sin_addr) != 1) {
+    MP_LOGE("bad --host %s", host.c_str());
+    return 2;
+  }
+  if (bind(ls, (sockaddr*)&addr, sizeof(addr)) != 0 || listen(ls, 128) != 0) {
+    MP_LOGE("cannot listen on %s:%d: %s", host.c_str(), port, strerror(errno));   // main.rs:109 panics; we exit 1
+    return 1;
+  }
+  std::thread gen(generation_loop, std::ref(S));
+  printf("orchestrator ready on http://%s:%d (static: %s, %s)\n", host.c_str(), port, S.static_dir.c_str(),
+         mock ? "mock engine" : "engine loaded");
+  fflush(stdout);
+  while (!S.stop) {
+    sockaddr_in peer{};
+    socklen_t pl = sizeof(peer);
+    int fd = accept(ls, (sockaddr*)&peer, &pl);
+    if (fd < 0) continue;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    char ip[64];
+    inet_ntop(AF_INET, &peer.sin_addr, ip, sizeof(ip));
+    std::thread(handle_conn, std::ref(S), fd, std::string(ip)).detach();
+  }
+  gen.join();
+  return 0;
+}

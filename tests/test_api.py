@@ -1,0 +1,215 @@
+"""T6 API tests (CPU only): the C++ orchestrator's HTTP/SSE contract (reference
+orchestrator/src/main.rs + static/index.html) and mi-cli, against
+the mock engine and against a real tiny GGUF on the CPU backend (-ngl 0)."""
+import json
+import os
+import socket
+import subprocess
+import threading
+import time
+
+import httpx
+import pytest
+
+from conftest import REPO, make_model
+
+BIN = os.path.join(REPO, "distributed-llm-pipeline_amd", "bin")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Orchestrator:
+    def __init__(self, *args):
+        self.port = free_port()
+        self.proc = subprocess.Popen([os.path.join(BIN, "orchestrator"), "--host", "127.0.0.1",
+                                      "--port", str(self.port), *args],
+                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        self.url = f"http://127.0.0.1:{self.port}"
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                httpx.get(self.url + "/health", timeout=1)
+                return
+            except Exception:
+                if self.proc.poll() is not None:
+                    raise RuntimeError(self.proc.stdout.read())
+                time.sleep(0.1)
+        raise RuntimeError("orchestrator did not come up")
+
+    def close(self):
+        self.proc.terminate()
+        try:
+            self.proc.wait(10)
+        except subprocess.TimeoutExpired:
+            self.proc.kill()
+
+
+def sse_events(resp):
+    """Parse an SSE stream into (events, n_keepalive)."""
+    events, keep, buf = [], 0, ""
+    for chunk in resp.iter_text():
+        buf += chunk
+        while "\n\n" in buf:
+            block, buf = buf.split("\n\n", 1)
+            if block.startswith(":"):
+                keep += 1
+                continue
+            data = "\n".join(l[5:].lstrip(" ") for l in block.split("\n") if l.startswith("data:"))
+            events.append(json.loads(data))
+    return events, keep
+
+
+@pytest.fixture(scope="module")
+def native_bins(native):
+    assert os.path.exists(os.path.join(BIN, "orchestrator")) and os.path.exists(os.path.join(BIN, "mi-cli"))
+    return BIN
+
+
+@pytest.fixture(scope="module")
+def mock_srv(native_bins):
+    s = Orchestrator("--mock", "-n", "12")
+    yield s
+    s.close()
+
+
+def test_chat_sse_contract(mock_srv):
+    with httpx.stream("POST", mock_srv.url + "/chat", json={"prompt": "Once upon a time"}, timeout=30) as r:
+        assert r.status_code == 200
+        assert r.headers["content-type"].startswith("text/event-stream")
+        assert r.headers["access-control-allow-origin"] == "*"
+        ev, _ = sse_events(r)
+    assert all(set(e) == {"msg_type", "content"} for e in ev)
+    logs = [e["content"] for e in ev if e["msg_type"] == "log"]
+    toks = [e["content"] for e in ev if e["msg_type"] == "token"]
+    assert any("offloaded" in l for l in logs)          # placement proof line (index.html:86)
+    assert any("prompt eval time" in l for l in logs)   # perf summary
+    assert len(toks) == 12
+    assert "".join(toks).startswith(" once upon a time")
+    assert "çğ \U0001F680" in "".join(toks)   # multi-byte UTF-8 intact
+
+
+def test_keepalive(native_bins):
+    s = Orchestrator("--mock", "--mock-delay-ms", "1300", "-n", "2")
+    try:
+        with httpx.stream("POST", s.url + "/chat", json={"prompt": "x"}, timeout=30) as r:
+            ev, keep = sse_events(r)
+        assert keep >= 1 and len([e for e in ev if e["msg_type"] == "token"]) == 2
+    finally:
+        s.close()
+
+
+def test_errors_and_cors(mock_srv):
+    u = mock_srv.url
+    assert httpx.get(u + "/chat").status_code == 405
+    assert httpx.post(u + "/chat", content=b'{"prompt":"x"}').status_code == 415
+    assert httpx.post(u + "/chat", content=b"{bad", headers={"content-type": "application/json"}).status_code == 400
+    assert httpx.post(u + "/chat", json={"text": "x"}).status_code == 422
+    assert httpx.post(u + "/chat", json={"prompt": 5}).status_code == 422
+    assert httpx.get(u + "/nope.html").status_code == 404
+    assert httpx.get(u + "/../etc/passwd").status_code == 404
+    r = httpx.options(u + "/chat")
+    assert r.status_code == 204 and r.headers["access-control-allow-origin"] == "*"
+
+
+def test_static_panel(mock_srv):
+    r = httpx.get(mock_srv.url + "/")
+    assert r.status_code == 200 and "text/html" in r.headers["content-type"]
+    assert "startChat" in r.text and "/chat" in r.text and "textContent" in r.text
+
+
+def test_completion_and_metrics(mock_srv):
+    r = httpx.post(mock_srv.url + "/completion", json={"prompt": "hi", "n_predict": 5}, timeout=30)
+    assert r.status_code == 200
+    j = r.json()
+    assert j["content"] == j["response"] and j["tokens_predicted"] == 5
+    m = httpx.get(mock_srv.url + "/metrics").text
+    assert "mipipe_requests_total" in m and "mipipe_token_latency_ms{quantile=\"0.5\"}" in m
+    assert int([l for l in m.splitlines() if l.startswith("mipipe_generated_tokens_total")][0].split()[1]) >= 5
+
+
+def test_disconnect_cancels(native_bins):
+    s = Orchestrator("--mock", "--mock-delay-ms", "50", "-n", "400")
+    try:
+        with httpx.stream("POST", s.url + "/chat", json={"prompt": "x"}, timeout=30) as r:
+            for i, _ in enumerate(r.iter_text()):
+                if i > 3:
+                    break
+        t0 = time.time()
+        while time.time() - t0 < 15:
+            m = httpx.get(s.url + "/metrics").text
+            if "mipipe_requests_cancelled_total 1" in m:
+                break
+            time.sleep(0.2)
+        assert "mipipe_requests_cancelled_total 1" in m
+    finally:
+        s.close()
+
+
+def test_api_key_and_rate_limit(native_bins):
+    s = Orchestrator("--mock", "-n", "2", "--api-key", "sekret", "--rate-limit", "3")
+    try:
+        assert httpx.post(s.url + "/completion", json={"prompt": "x"}).status_code == 401
+        h = {"Authorization": "Bearer sekret"}
+        codes = [httpx.post(s.url + "/completion", json={"prompt": "x"}, headers=h, timeout=30).status_code
+                 for _ in range(4)]
+        assert codes == [200, 200, 200, 429]
+    finally:
+        s.close()
+
+
+@pytest.fixture(scope="module")
+def tiny_gguf(model_dir):
+    path, cfg = make_model(model_dir, "tiny-l3", "Q8_0")
+    return path
+
+
+def test_real_engine_chat_matches_cli(native_bins, tiny_gguf):
+    """Orchestrator (in-process engine, CPU backend) and mi-cli produce the same greedy text."""
+    prompt = "The pipeline sends activations"
+    cli = subprocess.run([os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-p", prompt, "-n", "16", "-c", "256",
+                          "-ngl", "0", "--stages", "2"], capture_output=True, text=True, timeout=120)
+    assert cli.returncode == 0, cli.stderr
+    assert "offloaded" in cli.stderr or "on CPU" in cli.stderr
+    assert "prompt eval time" in cli.stderr
+    assert cli.stdout.startswith(prompt)
+    cli_text = cli.stdout[len(prompt):].rstrip("\n")
+    s = Orchestrator("-m", tiny_gguf, "-ngl", "0", "-n", "16", "-c", "256")
+    try:
+        with httpx.stream("POST", s.url + "/chat", json={"prompt": prompt}, timeout=120) as r:
+            ev, _ = sse_events(r)
+        text = "".join(e["content"] for e in ev if e["msg_type"] == "token")
+        assert text == cli_text
+        # concurrent requests are batched into one engine run and give the same greedy text
+        out = [None] * 3
+        def go(i):
+            out[i] = httpx.post(s.url + "/completion", json={"prompt": prompt, "n_predict": 16}, timeout=120).json()
+        th = [threading.Thread(target=go, args=(i,)) for i in range(3)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        assert all(o["content"] == cli_text for o in out)
+    finally:
+        s.close()
+
+
+def test_cli_daemon_and_bench(native_bins, tiny_gguf):
+    p = subprocess.run([os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-ngl", "0", "-c", "128", "--daemon"],
+                       input=json.dumps({"prompt": "abc", "n_predict": 5}) + "\n", capture_output=True, text=True,
+                       timeout=120)
+    lines = [json.loads(l) for l in p.stdout.splitlines()]
+    assert lines[-1]["done"] and lines[-1]["n_gen"] >= 1
+    b = subprocess.run([os.path.join(BIN, "mi-cli"), "--synthetic", "stories15m", "--ftype", "Q8_0", "-ngl", "0",
+                        "--bench", "--bench-prompt", "8", "--bench-steps", "4", "--bench-warmup", "1", "--mb-size", "2",
+                        "--stages", "2", "--trace", os.path.join(os.path.dirname(tiny_gguf), "tr.json")],
+                       capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr
+    r = json.loads(b.stdout.strip().splitlines()[-1])
+    assert r["decode_tok_s"] > 0
+    tr = json.load(open(os.path.join(os.path.dirname(tiny_gguf), "tr.json")))
+    names = {e["name"].split(" ")[0] for e in tr["traceEvents"] if e["ph"] == "X"}
+    assert {"decode", "send", "recv", "prefill"} <= names

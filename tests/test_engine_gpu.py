@@ -131,3 +131,42 @@ def test_synthetic_moe_engine_runs(cuda, native):
     with Engine(synthetic=syn, ftype="Q4_K_M", max_ctx=256, n_mb=1, mb_size=8) as eng:
         r = eng.bench(prompt_len=40, warmup=2, steps=8)
     assert r["decode_tok_s"] > 0
+
+
+_MP_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+import torch
+from mipipe.engine import Engine
+cfg = json.loads(sys.argv[1])
+with Engine(**cfg) as eng:
+    out, _ = eng.generate({prompts!r}, 7)
+    print("OUT " + json.dumps(out if cfg["rank"] == cfg["world"] - 1 else None), flush=True)
+"""
+
+
+def test_multiprocess_pipeline_one_gpu_tcp(cuda, native, model_dir):
+    """mode="mp" (one process per stage, the torchrun layout of bench.py) with two ranks sharing
+    the single GPU of the box; TCP links (RCCL refuses two ranks on one GPU)."""
+    import json, socket, subprocess, sys
+    from conftest import REPO
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts = [[3, 4, 5, 6], [7, 8], [9, 10, 11], [12]]
+    with Engine(gguf=path, max_ctx=64, n_mb=2, mb_size=2) as eng:
+        ref_out, _ = eng.generate(prompts, 7)
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    script = _MP_SCRIPT.format(repo=REPO, prompts=prompts)
+    procs = []
+    for r in range(2):
+        c = dict(gguf=path, mode="mp", world=2, rank=r, device=0, link="tcp", base_port=port,
+                 max_ctx=64, n_mb=2, mb_size=2, split="even")
+        procs.append(subprocess.Popen([sys.executable, "-c", script, json.dumps(c)], stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, cwd=REPO))
+    outs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=300)
+        assert p.returncode == 0, o[-3000:]
+        outs.append(o)
+    last = [l for l in outs[-1].splitlines() if l.startswith("OUT ")]
+    assert last and json.loads(last[0][4:]) == ref_out
