@@ -33,6 +33,10 @@ MODELS = {
                        vocab=128256, rope_base=500000.0),
     "llama3-8b": dict(name="Llama-3-8B", n_layer=32, d_model=4096, n_head=32, n_head_kv=8, d_ff=14336,
                       vocab=128256, rope_base=500000.0),
+    "mixtral-8x7b": dict(name="Mixtral-8x7B", n_layer=32, d_model=4096, n_head=32, n_head_kv=8, d_ff=14336,
+                         vocab=32000, rope_base=1000000.0, n_expert=8, n_expert_used=2),
+    "tinyllama": dict(name="TinyLlama-1.1B", n_layer=22, d_model=2048, n_head=32, n_head_kv=4, d_ff=5632,
+                      vocab=32000, rope_base=10000.0),
 }
 
 
