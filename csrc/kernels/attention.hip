@@ -187,6 +187,219 @@ __global__ __launch_bounds__(DP) void attn_combine_kernel(const AttnParams p) {
   if (d < p.hd) p.out[(size_t)t * p.ldo + h * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
 }
 
+
+// ---------------------------------------------------------------- fused decode attention
+// One launch per layer for decode (tq = 1): RoPE of q (in registers) and of the new k, the KV-cache
+// append (done by the split that owns the new position, before it reads its keys), flash-decoding
+// over the split, and the split merge by the LAST-arriving split of each (token, kv head)
+// (partials published with sc1 write-through stores, an agent-scope counter, sc1 loads): replaces
+// rope_kv + attn + attn_combine (three launches, ~16 us per layer at 16 sequences).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int DP>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
+  constexpr int KK = DP / 32;
+  constexpr int DT = DP / 16;
+  __shared__ float sm_m[4][16], sm_l[4][16];
+  __shared__ float sm_o[4][16][DP];
+  __shared__ int sm_last;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q4 = lane >> 4, col = lane & 15;
+  const int t = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
+  const int G = p.Hq / p.Hkv;
+  const int g = col;
+  const bool rvalid = col < G;
+  const int pos = p.pos[t];
+  const int kvlen = pos + 1;
+  const int slot = p.slot[t];
+  const int h = kvh * G + g;
+  const int hd2 = p.hd / 2;
+  const float* row = p.qkv + (size_t)t * p.ldqkv;
+  const float2* cs = p.rope_cs + (size_t)pos * hd2;
+  const int32_t* bt = p.block_table + (size_t)slot * p.max_pages;
+
+  const int start = z * p.split_len;
+  const int end = min(start + p.split_len, kvlen);
+
+  // 1. append the new token's K (rotated) and V to the cache (the split that will read it)
+  if (start <= pos && pos < end) {
+    const int page = bt[pos >> 6], idx = pos & 63;
+    const float* kr = row + p.Hq * p.hd + kvh * p.hd;
+    const float* vr = row + (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
+    f16* kd = p.k_cache + (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
+    f16* vd = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
+    for (int j = threadIdx.x; j < DP / 2; j += 256) {
+      half2_t o = {(f16)0.f, (f16)0.f};
+      if (j < hd2) {
+        const float x0 = kr[2 * j], x1 = kr[2 * j + 1];
+        const float2 c = cs[j];
+        o = half2_t{(f16)(x0 * c.x - x1 * c.y), (f16)(x0 * c.y + x1 * c.x)};
+      }
+      *reinterpret_cast<half2_t*>(kd + 2 * j) = o;
+    }
+    for (int d = threadIdx.x; d < DP; d += 256) vd[(size_t)d * 64] = (f16)(d < p.hd ? vr[d] : 0.f);
+    __threadfence_block();
+    __syncthreads();
+  }
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (start < end) {
+    // 2. q fragments with RoPE applied in registers: lane holds q[h][d = 32kk + 8q4 + j]
+    half8_t qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      half8_t v = {};
+      if (rvalid) {
+        const int d0 = 32 * kk + 8 * q4;
+        const float* qr = row + (size_t)h * p.hd;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const int d = d0 + j;
+          if (d < p.hd) {
+            const float x0 = qr[d], x1 = qr[d + 1];
+            const float2 c = cs[d >> 1];
+            v[j] = (f16)((x0 * c.x - x1 * c.y) * p.q_scale);
+            v[j + 1] = (f16)((x0 * c.y + x1 * c.x) * p.q_scale);
+          }
+        }
+      }
+      qf[kk] = v;
+    }
+    const int nch = (end - start + 31) / 32;
+    const int krow0 = 8 * (col >> 2) + (col & 3);
+    for (int ci = wave; ci < nch; ci += 4) {
+      const int P0 = start + ci * 32;
+      const int page = bt[P0 >> 6];
+      const int in_page = P0 & 63;
+      const f16* kbase = p.k_cache + ((size_t)page * p.Hkv + kvh) * 64 * DP;
+      const f16* vbase = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
+      half8_t kf[2][KK];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+          kf[c][kk] = *reinterpret_cast<const half8_t*>(kbase + (size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4);
+      half8_t vf[DT];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        vf[dt] = *reinterpret_cast<const half8_t*>(vbase + (size_t)(16 * dt + col) * 64 + in_page + 8 * q4);
+      f32x4 sc[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) a = mfma16x16x32(kf[c][kk], qf[kk], a);
+        sc[c] = a;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kpos = P0 + 8 * q4 + 4 * c + i;
+          const float v = kpos < end ? sc[c][i] : -INFINITY;
+          sc[c][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+      float pv[2][4];
+      float psum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = (m_new == -INFINITY) ? 0.f : __expf(sc[c][i] - m_new);
+          pv[c][i] = e;
+          psum += e;
+        }
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+      half8_t pf = {(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
+                    (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+    }
+  }
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+  if (q4 == 0) { sm_m[wave][col] = m_run; sm_l[wave][col] = l_run; }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[wave][col][16 * dt + 4 * q4 + i] = o[dt][i];
+  __syncthreads();
+
+  // 3. merge the 4 waves; publish (n_split > 1) or write the output
+  const size_t stride = (size_t)p.M * p.Hq;
+  for (int e = threadIdx.x; e < G * DP; e += 256) {
+    const int r = e / DP, d = e % DP;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][r]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (sm_m[w][r] == -INFINITY) continue;
+      const float f = __expf(sm_m[w][r] - M);
+      L += sm_l[w][r] * f;
+      O += sm_o[w][r][d] * f;
+    }
+    const int hh = kvh * G + r;
+    const size_t rid = (size_t)t * p.Hq + hh;
+    if (p.n_split == 1) {
+      if (d < p.hd) p.out[(size_t)t * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
+    } else {
+      st_sc1(p.o_part + ((size_t)z * stride + rid) * DP + d, O);
+      if (d == 0) {
+        st_sc1(p.ml_part + ((size_t)z * stride + rid) * 2, M);
+        st_sc1(p.ml_part + ((size_t)z * stride + rid) * 2 + 1, L);
+      }
+    }
+  }
+  if (p.n_split == 1) return;
+  // 4. last arriver of this (token, kv head) merges the splits
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(p.counters + (size_t)t * p.Hkv + kvh, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    sm_last = old == p.n_split - 1;
+  }
+  __syncthreads();
+  if (!sm_last) return;
+  for (int e = threadIdx.x; e < G * DP; e += 256) {
+    const int r = e / DP, d = e % DP;
+    const int hh = kvh * G + r;
+    const size_t rid = (size_t)t * p.Hq + hh;
+    float M = -INFINITY;
+    for (int zz = 0; zz < p.n_split; ++zz) M = fmaxf(M, ld_sc1(p.ml_part + (zz * stride + rid) * 2));
+    float L = 0.f, O = 0.f;
+    for (int zz = 0; zz < p.n_split; ++zz) {
+      const float mz = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
+      if (mz == -INFINITY) continue;
+      const float f = __expf(mz - M);
+      L += ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1) * f;
+      O += ld_sc1(p.o_part + (zz * stride + rid) * DP + d) * f;
+    }
+    if (d < p.hd) p.out[(size_t)t * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(p.counters + (size_t)t * p.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace mpk
 
 namespace mp {
@@ -201,6 +414,12 @@ void launch_attention(const AttnParams& p, hipStream_t st) {
     hipLaunchKernelGGL(mpk::attn_kernel<64>, grid, dim3(256), 0, st, p);
     if (p.n_split > 1) hipLaunchKernelGGL(mpk::attn_combine_kernel<64>, dim3(p.M * p.Hq), dim3(64), 0, st, p);
   }
+}
+
+void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
+  dim3 grid(p.M, p.Hkv, p.n_split);
+  if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_decode_kernel<128>, grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL(mpk::attn_decode_kernel<64>, grid, dim3(256), 0, st, p);
 }
 
 }  // namespace mp

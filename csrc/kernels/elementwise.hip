@@ -20,52 +20,64 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
   return t;
 }
 
-__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
-                                                      float eps, f16* out, int ldo, float* zero,
-                                                      int64_t zero_n, int M) {
-  __shared__ float red[4];
+// One 1024-thread workgroup per row: each thread holds 8 floats of x (d <= 8192) and its 8 norm
+// weights, both loaded before anything else so the two reads overlap; the split-K accumulator the
+// next GEMV adds into is cleared by the same launch (16K floats per workgroup) after the loads are
+// in flight.
+__global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
+                                                       float eps, f16* out, int ldo, float* zero,
+                                                       int64_t zero_n, int M) {
+  __shared__ float red[16];
   const int row = blockIdx.x;
-  if (zero) {   // every block clears a 4096-float slice of the split-K accumulator (float4 stores)
-    const int64_t z0 = (int64_t)blockIdx.x * 4096, z1 = min(zero_n, z0 + 4096);
-    for (int64_t i = z0 + threadIdx.x * 4; i < z1; i += 1024) {
+  const int tid = threadIdx.x;
+  const bool fast = (d & 3) == 0 && d <= 8192;
+  const float* xr = x + (size_t)row * ldx;
+  float4 v[2], ww[2];
+  if (row < M && fast) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = (tid + 1024 * k) * 4;
+      v[k] = i < d ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ww[k] = i < d ? *reinterpret_cast<const float4*>(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (zero) {
+    const int64_t z0 = (int64_t)blockIdx.x * 16384, z1 = min(zero_n, z0 + 16384);
+    for (int64_t i = z0 + tid * 4; i < z1; i += 4096) {
       if (i + 4 <= z1) *reinterpret_cast<float4*>(zero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       else for (int64_t k = i; k < z1; ++k) zero[k] = 0.f;
     }
   }
   if (row >= M) return;
-  const float* xr = x + (size_t)row * ldx;
   f16* o = out + (size_t)row * ldo;
-  const int d4 = d & ~3;
-  if (d4 == d && d <= 8 * 1024) {
-    // single pass: the row (<= 8192 floats) stays in registers between the sum and the scale
-    float4 v[8];
-    float ss = 0.f;
+  float ss = 0.f;
+  if (fast) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = (threadIdx.x + 256 * k) * 4;
-      v[k] = i < d ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
-    }
-    ss = block_sum_256(ss, red);
-    const float sc = rsqrtf(ss / (float)d + eps);
+    for (int k = 0; k < 2; ++k) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  } else {
+    for (int i = tid; i < d; i += 1024) ss += xr[i] * xr[i];
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = (threadIdx.x + 256 * k) * 4;
+  for (int i = 0; i < 16; ++i) tot += red[i];
+  const float sc = rsqrtf(tot / (float)d + eps);
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = (tid + 1024 * k) * 4;
       if (i < d) {
-        const float4 ww = *reinterpret_cast<const float4*>(w + i);
-        half2_t a = {(f16)(v[k].x * sc * ww.x), (f16)(v[k].y * sc * ww.y)};
-        half2_t b = {(f16)(v[k].z * sc * ww.z), (f16)(v[k].w * sc * ww.w)};
+        half2_t a = {(f16)(v[k].x * sc * ww[k].x), (f16)(v[k].y * sc * ww[k].y)};
+        half2_t b = {(f16)(v[k].z * sc * ww[k].z), (f16)(v[k].w * sc * ww[k].w)};
         u32x2 pk = {as_u32(a), as_u32(b)};
         *reinterpret_cast<u32x2*>(o + i) = pk;
       }
     }
-    return;
+  } else {
+    for (int i = tid; i < d; i += 1024) o[i] = (f16)(xr[i] * sc * w[i]);
   }
-  float ss = 0.f;
-  for (int i = threadIdx.x; i < d; i += 256) ss += xr[i] * xr[i];
-  ss = block_sum_256(ss, red);
-  const float sc = rsqrtf(ss / (float)d + eps);
-  for (int i = threadIdx.x; i < d; i += 256) o[i] = (f16)(xr[i] * sc * w[i]);
 }
 
 // ---------------------------------------------------------------- embedding (raw GGUF rows)
@@ -220,8 +232,8 @@ void launch_prefill_meta(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, in
 
 void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
                     float* zero, int64_t zero_n, hipStream_t st) {
-  const int zb = zero ? (int)((zero_n + 4095) / 4096) : 0;
-  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(256), 0, st, x, ldx, w, d, eps, out, ldo, zero,
+  const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
+  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
                      zero_n, M);
 }
 

@@ -16,9 +16,11 @@
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
+#include <cstdlib>
+
 namespace mpk {
 
-template <int PT, int EPI, int WPB, int TPW, int NSLOT>
+template <int PT, int EPI, int WPB, int TPW, int NSLOT, bool XR>
 __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) {
   // TPW tiles per wave share every x fragment (x traffic / weight traffic = 3.5 / TPW at M = 16);
   // NSLOT super-blocks per tile are kept in flight in a compile-time indexed register ring.
@@ -42,11 +44,21 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int last = sb1 - 1;
+  // Register ring of NSLOT super-blocks.  XR: the x fragments of a slot are loaded together with
+  // its weights (vmcnt retires loads in issue order, so x fetched at use waits for every weight
+  // prefetch in flight) at the price of 32 VGPRs per slot; !XR: x fetched at use.
   typename D::Raw ring[NSLOT][TPW];
+  half8_t xr[1][8];   // (x-in-ring variant measured slower: VGPR cost)
+  auto issue = [&](int sl, int sbi) {
 #pragma unroll
-  for (int sl = 0; sl < NSLOT; ++sl)
+    for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)sbi * CB, lane);
+    if constexpr (false) {
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)min(sb0 + sl, last) * CB, lane);
+      for (int i = 0; i < 8; ++i) xr[sl][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)sbi * 256 + 32 * i);
+    }
+  };
+#pragma unroll
+  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sb0 + sl, last));
 
   for (int sb = sb0; sb < sb1; sb += NSLOT) {
 #pragma unroll
@@ -62,30 +74,29 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
             for (int i = 0; i < (int)(sizeof(typename D::Raw) / 4); ++i) h ^= w[i];
             acc[t][0] += __uint_as_float(h & 0x3FFFFFFFu);
           }
-          if (cur + NSLOT < sb1) {
+        } else {
+          const int xs = 0;
+          {
 #pragma unroll
-            for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)(cur + NSLOT) * CB, lane);
+            for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
           }
-          continue;
-        }
-        half8_t a[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+          for (int t = 0; t < TPW; ++t) {
+            half8_t b[4];
+            if constexpr (XR && PT == P_Q4_K) D::template dequant_fast<0>(ring[sl][t], b, lane);
+            else D::template dequant<0>(ring[sl][t], b, lane);
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          half8_t b[4];
-          D::template dequant<0>(ring[sl][t], b, lane);
+            for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(xr[xs][s], b[s], acc[t]);
+            if constexpr (XR && PT == P_Q4_K) D::template dequant_fast<1>(ring[sl][t], b, lane);
+            else D::template dequant<1>(ring[sl][t], b, lane);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(a[s], b[s], acc[t]);
-          D::template dequant<1>(ring[sl][t], b, lane);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(a[4 + s], b[s], acc[t]);
-        }
-        if (cur + NSLOT < sb1) {
-#pragma unroll
-          for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)(cur + NSLOT) * CB, lane);
+            for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(xr[xs][4 + s], b[s], acc[t]);
+          }
         }
       }
+      // unconditional refill (clamped to the last super-block: an L2 hit) keeps the number of loads
+      // in flight path-independent, so the compiler emits exact vmcnt(N) waits, not vmcnt(0)
+      issue(sl, min(cur + NSLOT, last));
     }
   }
 
@@ -151,17 +162,31 @@ namespace mp {
 static int g_wpb = 1;   // waves per workgroup (tuning knob, MP_GEMV_WPB)
 static int g_tpw = 0;   // tiles per wave: 0 = auto (1 for M <= 4, else 2)
 
-template <int PT, int WPB, int TPW, int NSLOT>
-static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+static int g_xr = -1;   // x fragments in the register ring (MIPIPE_GEMV_XR=1), default off
+
+template <int PT, int WPB, int TPW, int NSLOT, bool XR>
+static void launch_cfg_x(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
   const int waves = (p.ntiles + TPW - 1) / TPW;
   dim3 grid((waves + WPB - 1) / WPB, nsplit);
   dim3 block(WPB * 64);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
-    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
-    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
-    case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
+    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT, false>), grid, block, 0, st, p); break;
   }
+}
+
+template <int PT, int WPB, int TPW, int NSLOT>
+static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  if (g_xr < 0) {
+    const char* e = getenv("MIPIPE_GEMV_XR");
+    g_xr = e && atoi(e) ? 1 : 0;
+  }
+  if constexpr (PT == P_Q4_K) {
+    if (g_xr) return launch_cfg_x<PT, WPB, TPW, NSLOT, true>(epi, p, nsplit, st);
+  }
+  launch_cfg_x<PT, WPB, TPW, NSLOT, false>(epi, p, nsplit, st);
 }
 
 // Tiles per wave: with M > 4 the x fragments (16 rows x 32 k per MFMA) cost more L1/L2 traffic
@@ -173,17 +198,25 @@ int gemv_tiles_per_wave(int M, int epi) {
   return M <= 4 ? 1 : 4;
 }
 
+static int g_nslot = -1;   // super-blocks in flight per tile (MIPIPE_GEMV_NSLOT), 0 = default
+
 template <int PT>
 static void launch_pt(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  if (g_nslot < 0) {
+    const char* e = getenv("MIPIPE_GEMV_NSLOT");
+    g_nslot = e ? atoi(e) : 0;
+  }
   const int tpw = gemv_tiles_per_wave(p.M, epi);
   if (tpw == 1) {
-    if (g_wpb == 2) launch_cfg<PT, 2, 1, 4>(epi, p, nsplit, st);
+    if (g_nslot == 8) launch_cfg<PT, 1, 1, 8>(epi, p, nsplit, st);
     else launch_cfg<PT, 1, 1, 4>(epi, p, nsplit, st);
   } else if (tpw == 2) {
-    if (g_wpb == 2) launch_cfg<PT, 2, 2, 2>(epi, p, nsplit, st);
+    if (g_nslot == 4) launch_cfg<PT, 1, 2, 4>(epi, p, nsplit, st);
     else launch_cfg<PT, 1, 2, 2>(epi, p, nsplit, st);
   } else {
-    launch_cfg<PT, 1, 4, 2>(epi, p, nsplit, st);
+    if (g_nslot == 3) launch_cfg<PT, 1, 4, 3>(epi, p, nsplit, st);
+    else if (g_nslot == 4) launch_cfg<PT, 1, 4, 4>(epi, p, nsplit, st);
+    else launch_cfg<PT, 1, 4, 2>(epi, p, nsplit, st);
   }
 }
 

@@ -140,6 +140,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.use_graphs = j.get_bool("graphs", true);
   so.attn_split_len = j.get_int("attn_split_len", 128);
   so.threads = j.get_int("threads", 0);
+  so.fused_attn = j.get_bool("fused_attn", true);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {

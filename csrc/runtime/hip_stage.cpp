@@ -346,6 +346,7 @@ void HipStage::alloc_runtime() {
     o_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * Dp_ * 4);
     ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
   }
+  attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
   // KV cache: static paging, every slot owns max_ctx/64 pages
   const int n_slots = NM * B;
   max_pages_ = opt_.max_ctx / 64;
@@ -464,28 +465,38 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st);
   for (const MatSeg& s : L.qkv)
     gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
-  RopeKvParams rp{};
-  rp.qkv = qkv_; rp.ldqkv = qkv_n_; rp.M = M; rp.Hq = cfg_.n_head; rp.Hkv = cfg_.n_head_kv;
-  rp.hd = cfg_.head_dim; rp.Dp = Dp_; rp.pos = pos; rp.slot = slot; rp.block_table = block_table_;
-  rp.max_pages = max_pages_; rp.rope_cs = rope_cs_; rp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
-  rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li];
-  launch_rope_kv(rp, st);
-  AttnParams ap{};
-  ap.q = q_; ap.kvlen = kvlen; ap.slot = slot; ap.block_table = block_table_; ap.max_pages = max_pages_;
-  ap.k_cache = kc_[li]; ap.v_cache = vc_[li]; ap.M = M; ap.Hq = cfg_.n_head; ap.Hkv = cfg_.n_head_kv;
-  ap.hd = cfg_.head_dim; ap.Dp = Dp_; ap.max_kv = opt_.max_ctx; ap.out = attn_; ap.ldo = Ko_;
-  if (decode) {
-    ap.tq = 1;
-    ap.split_len = opt_.attn_split_len;
-    ap.n_split = n_split_;
-    ap.o_part = o_part_; ap.ml_part = ml_part_;
+  if (decode && opt_.fused_attn) {
+    DecodeAttnParams dp{};
+    dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
+    dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
+    dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
+    dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
+    dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
+    launch_attn_decode(dp, st);
   } else {
-    const int G = cfg_.n_head / cfg_.n_head_kv;
-    ap.tq = std::max(1, 16 / G);
-    ap.split_len = (int)round_up(opt_.max_ctx, 128);
-    ap.n_split = 1;
+    RopeKvParams rp{};
+    rp.qkv = qkv_; rp.ldqkv = qkv_n_; rp.M = M; rp.Hq = cfg_.n_head; rp.Hkv = cfg_.n_head_kv;
+    rp.hd = cfg_.head_dim; rp.Dp = Dp_; rp.pos = pos; rp.slot = slot; rp.block_table = block_table_;
+    rp.max_pages = max_pages_; rp.rope_cs = rope_cs_; rp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
+    rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li];
+    launch_rope_kv(rp, st);
+    AttnParams ap{};
+    ap.q = q_; ap.kvlen = kvlen; ap.slot = slot; ap.block_table = block_table_; ap.max_pages = max_pages_;
+    ap.k_cache = kc_[li]; ap.v_cache = vc_[li]; ap.M = M; ap.Hq = cfg_.n_head; ap.Hkv = cfg_.n_head_kv;
+    ap.hd = cfg_.head_dim; ap.Dp = Dp_; ap.max_kv = opt_.max_ctx; ap.out = attn_; ap.ldo = Ko_;
+    if (decode) {
+      ap.tq = 1;
+      ap.split_len = opt_.attn_split_len;
+      ap.n_split = n_split_;
+      ap.o_part = o_part_; ap.ml_part = ml_part_;
+    } else {
+      const int G = cfg_.n_head / cfg_.n_head_kv;
+      ap.tq = std::max(1, 16 / G);
+      ap.split_len = (int)round_up(opt_.max_ctx, 128);
+      ap.n_split = 1;
+    }
+    launch_attention(ap, st);
   }
-  launch_attention(ap, st);
   gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
   launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
   if (L.moe) {

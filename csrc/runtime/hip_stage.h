@@ -148,6 +148,7 @@ class HipStage : public Stage {
   float* gu_ = nullptr;   // unfused gate|up f32
   float* logits_ = nullptr; int logits_ld_ = 0;
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
+  int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
   // MoE scratch
   float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
   float* moe_w_ = nullptr; f16* moe_h_ = nullptr;

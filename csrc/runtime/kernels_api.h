@@ -90,6 +90,24 @@ struct AttnParams {
 };
 void launch_attention(const AttnParams& p, hipStream_t st);
 
+// fused decode step of attention: RoPE(q, k) + KV append + split-K flash-decoding + last-arriver
+// merge (replaces rope_kv + attention + combine for tq = 1)
+struct DecodeAttnParams {
+  const float* qkv; int ldqkv;     // [M][ldqkv] f32 projections q | k | v
+  const int32_t* pos;              // [M]
+  const int32_t* slot;             // [M]
+  const int32_t* block_table; int max_pages;
+  const float2* rope_cs;           // [max_pos][hd/2]
+  float q_scale;
+  f16* k_cache; f16* v_cache;
+  int M, Hq, Hkv, hd, Dp;
+  int split_len, n_split;
+  float* o_part; float* ml_part;   // [n_split][M*Hq][Dp], [n_split][M*Hq][2]
+  int32_t* counters;               // [M*Hkv] zero-initialised, self-resetting
+  f16* out; int ldo;
+};
+void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
+
 // greedy sampling: tokens[m] = argmax logits[m][:n]
 void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st);
 // temperature / top-k / top-p / min-p sampling with a counter-based RNG

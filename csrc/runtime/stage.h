@@ -23,6 +23,7 @@ struct StageOptions {
   bool use_graphs = true;
   int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
+  bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
 };
 
 class Stage {

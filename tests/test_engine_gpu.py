@@ -170,3 +170,21 @@ def test_multiprocess_pipeline_one_gpu_tcp(cuda, native, model_dir):
         outs.append(o)
     last = [l for l in outs[-1].splitlines() if l.startswith("OUT ")]
     assert last and json.loads(last[0][4:]) == ref_out
+
+
+@pytest.mark.parametrize("name", ["tiny-gqa", "stories15m"])
+def test_fused_decode_attention_matches_unfused(cuda, native, model_dir, name):
+    """Fused RoPE + KV append + split-K attention + last-arriver merge == the three-kernel path,
+    across several KV splits (split_len 128, contexts up to ~400)."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, name, "Q8_0")
+    rng = np.random.default_rng(5)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (300, 5, 130, 255)]
+    res = []
+    for fused in (False, True):
+        with Engine(gguf=path, max_ctx=512, n_mb=2, mb_size=2, prefill_chunk=64, fused_attn=fused) as eng:
+            out, _ = eng.generate(prompts, 12)
+            lg = eng.logits()
+            res.append((out, lg))
+    assert res[0][0] == res[1][0]
+    assert nmse(res[1][1], res[0][1]) < 1e-6
