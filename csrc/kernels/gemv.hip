@@ -26,13 +26,18 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
   // NSLOT super-blocks per tile are kept in flight in a compile-time indexed register ring.
   using D = Deq<PT>;
   constexpr int CB = D::CB;
+  // WPB waves of a workgroup share the same TPW tiles and split the workgroup's K range among
+  // themselves (intra-workgroup split-K, reduced through LDS before the epilogue): more waves per
+  // SIMD for the same tiles, no extra x traffic and no atomics.
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int tile0 = (blockIdx.x * WPB + wave) * TPW;
+  const int tile0 = blockIdx.x * TPW;
   if (tile0 >= p.ntiles) return;
-  const int sb0 = blockIdx.y * p.sb_per_split;
-  const int sb1 = min(sb0 + p.sb_per_split, p.nsb);
-  if (sb0 >= sb1) return;
+  const int sbA = blockIdx.y * p.sb_per_split;
+  const int sbB = min(sbA + p.sb_per_split, p.nsb);
+  if (sbA >= sbB) return;
+  const int sb0 = sbA + ((sbB - sbA) * wave) / WPB;
+  const int sb1 = sbA + ((sbB - sbA) * (wave + 1)) / WPB;
   const int g = lane >> 4, r = lane & 15;
   const uint8_t* wt[TPW];
 #pragma unroll
@@ -58,7 +63,8 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
     }
   };
 #pragma unroll
-  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sb0 + sl, last));
+  // (a wave with an empty K share still loads a valid super-block of its workgroup's range)
+  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(max(sb0, min(sb0 + sl, last)), sbB - 1));
 
   for (int sb = sb0; sb < sb1; sb += NSLOT) {
 #pragma unroll
@@ -74,9 +80,27 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
             for (int i = 0; i < (int)(sizeof(typename D::Raw) / 4); ++i) h ^= w[i];
             acc[t][0] += __uint_as_float(h & 0x3FFFFFFFu);
           }
+        } else if constexpr (EPI == 4) {   // probe: weight + x loads, no dequant / MFMA
+#pragma unroll
+          for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&ring[sl][t]);
+            uint32_t h = 0;
+#pragma unroll
+            for (int i = 0; i < (int)(sizeof(typename D::Raw) / 4); ++i) h ^= w[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) h ^= __builtin_bit_cast(u32x4, xr[0][i]).x;
+            acc[t][0] += __uint_as_float(h & 0x3FFFFFFFu);
+          }
         } else {
           const int xs = 0;
-          {
+          if constexpr (EPI == 5) {   // probe: dequant + MFMA on a constant x (no x loads)
+            if (cur == sb0) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + 32 * i);
+            }
+          } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
           }
@@ -98,6 +122,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
       // in flight path-independent, so the compiler emits exact vmcnt(N) waits, not vmcnt(0)
       issue(sl, min(cur + NSLOT, last));
     }
+  }
+  if constexpr (WPB > 1) {
+    __shared__ f32x4 red[WPB - 1][TPW][64];
+    if (wave > 0) {
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) red[wave - 1][t][lane] = acc[t];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int w = 0; w < WPB - 1; ++w)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t] += red[w][t][lane];
   }
 
   // lane holds C[m = 4g + i][n = 16*tile + r]
@@ -166,14 +203,15 @@ static int g_xr = -1;   // x fragments in the register ring (MIPIPE_GEMV_XR=1), 
 
 template <int PT, int WPB, int TPW, int NSLOT, bool XR>
 static void launch_cfg_x(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
-  const int waves = (p.ntiles + TPW - 1) / TPW;
-  dim3 grid((waves + WPB - 1) / WPB, nsplit);
+  dim3 grid((p.ntiles + TPW - 1) / TPW, nsplit);
   dim3 block(WPB * 64);
   switch (epi) {
     case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
     case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
     case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
     case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT, false>), grid, block, 0, st, p); break;
+    case 4: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 4, WPB, TPW, NSLOT, false>), grid, block, 0, st, p); break;
+    case 5: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 5, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
   }
 }
 
@@ -198,29 +236,27 @@ int gemv_tiles_per_wave(int M, int epi) {
   return M <= 4 ? 1 : 4;
 }
 
-static int g_nslot = -1;   // super-blocks in flight per tile (MIPIPE_GEMV_NSLOT), 0 = default
+template <int PT, int TPW, int NSLOT>
+static void launch_ks(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  if (g_wpb == 4) launch_cfg<PT, 4, TPW, NSLOT>(epi, p, nsplit, st);
+  else if (g_wpb == 2) launch_cfg<PT, 2, TPW, NSLOT>(epi, p, nsplit, st);
+  else launch_cfg<PT, 1, TPW, NSLOT>(epi, p, nsplit, st);
+}
 
 template <int PT>
 static void launch_pt(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
-  if (g_nslot < 0) {
-    const char* e = getenv("MIPIPE_GEMV_NSLOT");
-    g_nslot = e ? atoi(e) : 0;
+  static bool env_done = false;
+  if (!env_done) {
+    env_done = true;
+    if (const char* e = getenv("MIPIPE_GEMV_KS")) g_wpb = atoi(e);
   }
   const int tpw = gemv_tiles_per_wave(p.M, epi);
-  if (tpw == 1) {
-    if (g_nslot == 8) launch_cfg<PT, 1, 1, 8>(epi, p, nsplit, st);
-    else launch_cfg<PT, 1, 1, 4>(epi, p, nsplit, st);
-  } else if (tpw == 2) {
-    if (g_nslot == 4) launch_cfg<PT, 1, 2, 4>(epi, p, nsplit, st);
-    else launch_cfg<PT, 1, 2, 2>(epi, p, nsplit, st);
-  } else {
-    if (g_nslot == 3) launch_cfg<PT, 1, 4, 3>(epi, p, nsplit, st);
-    else if (g_nslot == 4) launch_cfg<PT, 1, 4, 4>(epi, p, nsplit, st);
-    else launch_cfg<PT, 1, 4, 2>(epi, p, nsplit, st);
-  }
+  if (tpw == 1) launch_ks<PT, 1, 4>(epi, p, nsplit, st);
+  else if (tpw == 2) launch_ks<PT, 2, 2>(epi, p, nsplit, st);
+  else launch_ks<PT, 4, 2>(epi, p, nsplit, st);
 }
 
-void set_gemv_wpb(int w) { g_wpb = (w == 1 || w == 2) ? w : 1; }
+void set_gemv_wpb(int w) { g_wpb = (w == 1 || w == 2 || w == 4) ? w : 1; }
 void set_gemv_tpw(int t) { g_tpw = (t == 1 || t == 2 || t == 4) ? t : 0; }
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {

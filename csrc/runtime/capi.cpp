@@ -139,6 +139,17 @@ const char* mp_model_config_json(const char* gguf_path) {
 }
 
 // ------------------------------------------------------------------ kernel ops (tests)
+int mp_op_gemm(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+               int ldy, void* H, int ldh, int n_valid, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  launch_gemm(ptype, epi, p, (hipStream_t)stream);
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
                int ldy, void* H, int ldh, int n_valid, int nsplit, void* stream) {
   API_TRY
@@ -312,6 +323,20 @@ const char* mp_engine_info(void* h) {
   g_str = static_cast<Engine*>(h)->info().dump();
   return g_str.c_str();
   API_CATCH(nullptr)
+}
+const char* mp_engine_health(void* h) {
+  API_TRY
+  g_str = static_cast<Engine*>(h)->health().dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+int mp_engine_trace(void* h, int on, const char* path) {
+  API_TRY
+  Engine* e = static_cast<Engine*>(h);
+  if (path && *path) e->write_trace(path);
+  else e->enable_trace(on != 0);
+  return 0;
+  API_CATCH(-1)
 }
 // Generate for a batch of prompts. prompts: concatenated token ids, lens[n]. out: [n][n_predict]
 // returns JSON stats string

@@ -141,6 +141,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.attn_split_len = j.get_int("attn_split_len", 128);
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
+  so.prefill_gemm = j.get_bool("prefill_gemm", true);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {
@@ -175,6 +176,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     workers_.push_back(std::move(w));
   }
   build_links(j);
+  for (auto& l : links_) l->set_timeout(j.get_num("link_timeout_s", 600.0));
   rounds_cap_ = max_ctx_ + 2;
   if (cpu_) {
     out_vec_.resize((size_t)rounds_cap_ * M_ * B_);
@@ -501,27 +503,30 @@ void Engine::run_all(const std::vector<Item>& items) {
     try {
       run_items(*workers_[0], items);
     } catch (...) {
+      failed_ = true;
       for (auto& l : links_) l->abort();
       throw;
     }
   } else {
     std::vector<std::thread> th;
     std::vector<std::exception_ptr> errs(workers_.size());
+    std::atomic<int> first_err{-1};   // the root cause; the others are usually "link aborted"
     for (size_t i = 0; i < workers_.size(); ++i)
       th.emplace_back([&, i] {
         try {
           run_items(*workers_[i], items);
         } catch (...) {
           errs[i] = std::current_exception();
+          int expect = -1;
+          first_err.compare_exchange_strong(expect, (int)i);
           for (auto& l : links_) l->abort();
         }
       });
     for (auto& t : th) t.join();
-    for (auto& e : errs)
-      if (e) {
-        failed_ = true;
-        std::rethrow_exception(e);
-      }
+    if (first_err >= 0) {
+      failed_ = true;
+      std::rethrow_exception(errs[first_err]);
+    }
   }
   sync_all();
   if (trace_) collect_trace();

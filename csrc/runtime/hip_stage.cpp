@@ -415,6 +415,13 @@ void HipStage::set_sampling(float temp, int top_k, float top_p, float min_p, uin
 
 void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
                     int n_valid, bool allow_split, hipStream_t st) {
+  if (M > 16 && opt_.prefill_gemm) {   // prompt chunks: MFMA GEMM, weights read once per 64 rows
+    GemvParams p{};
+    p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
+    p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
+    launch_gemm(m.ptype, epi, p, st);
+    return;
+  }
   for (int r0 = 0; r0 < M; r0 += 16) {
     GemvParams p{};
     p.W = m.d;

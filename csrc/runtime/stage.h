@@ -24,6 +24,7 @@ struct StageOptions {
   int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
+  bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
 };
 
 class Stage {

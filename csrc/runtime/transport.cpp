@@ -72,7 +72,7 @@ void LocalLink::send(const void* buf, size_t bytes, hipStream_t st) {
   bool wait_freed;
   {
     std::unique_lock<std::mutex> l(mu_);
-    if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !free_.empty(); }))
+    if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !free_.empty(); }))
       throw std::runtime_error("LocalLink: send timed out (peer stalled)");
     if (aborted_) throw std::runtime_error("LocalLink: aborted");
     slot = free_.front();
@@ -95,7 +95,7 @@ void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
   Msg m;
   {
     std::unique_lock<std::mutex> l(mu_);
-    if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !q_.empty(); }))
+    if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !q_.empty(); }))
       throw std::runtime_error("LocalLink: recv timed out (peer stalled)");
     if (aborted_) throw std::runtime_error("LocalLink: aborted");
     m = q_.front();
@@ -238,6 +238,13 @@ void TcpLink::abort() {
   if (fd_ >= 0) { shutdown(fd_, SHUT_RDWR); }
 }
 
+void TcpLink::set_timeout(double s) {
+  timeout_s = s;
+  timeval tv{(long)s, (long)((s - (long)s) * 1e6)};
+  setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+}
+
 void TcpLink::send(const void* buf, size_t bytes, hipStream_t st) {
   const void* src = buf;
   if (st) {
@@ -275,7 +282,7 @@ namespace mp {
 void HostLink::send(const void* buf, size_t bytes, hipStream_t) {
   std::vector<uint8_t> m((const uint8_t*)buf, (const uint8_t*)buf + bytes);
   std::unique_lock<std::mutex> l(mu_);
-  if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || q_.size() < max_q_; }))
+  if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || q_.size() < max_q_; }))
     throw std::runtime_error("HostLink: send timed out (peer stalled)");
   if (aborted_) throw std::runtime_error("HostLink: aborted");
   q_.push_back(std::move(m));
@@ -286,7 +293,7 @@ void HostLink::send(const void* buf, size_t bytes, hipStream_t) {
 
 void HostLink::recv(void* buf, size_t bytes, hipStream_t) {
   std::unique_lock<std::mutex> l(mu_);
-  if (!cv_.wait_for(l, std::chrono::seconds(600), [&] { return aborted_ || !q_.empty(); }))
+  if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !q_.empty(); }))
     throw std::runtime_error("HostLink: recv timed out (peer stalled)");
   if (aborted_) throw std::runtime_error("HostLink: aborted");
   if (q_.front().size() != bytes) throw std::runtime_error("HostLink: message size mismatch");

@@ -28,6 +28,9 @@ class Link {
   virtual void recv(void* buf, size_t bytes, hipStream_t st) = 0;
   virtual const char* kind() const = 0;
   virtual void abort() {}
+  // blocking waits give up after this long (a dead or stalled peer surfaces as an error)
+  virtual void set_timeout(double s) { timeout_s = s; }
+  double timeout_s = 600;
   uint64_t bytes_sent = 0, msgs_sent = 0;
 };
 
@@ -109,6 +112,7 @@ class TcpLink : public Link {
   void recv(void* buf, size_t bytes, hipStream_t st) override;
   const char* kind() const override { return "tcp"; }
   void abort() override;
+  void set_timeout(double s) override;
 
  private:
   int fd_ = -1;

@@ -42,6 +42,8 @@ _SIGS = {
     "mp_model_config_json": ([c_char_p], c_char_p),
     "mp_op_gemv": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                     c_int, c_int, c_int, c_void_p], c_int),
+    "mp_op_gemm": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                    c_int, c_int, c_void_p], c_int),
     "mp_op_unpack": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_rmsnorm": ([c_void_p, c_int, c_void_p, c_int, c_float, c_void_p, c_int, c_int, c_void_p], c_int),
     "mp_op_embed": ([c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
@@ -61,6 +63,8 @@ _SIGS = {
     "mp_engine_create": ([c_char_p], c_void_p),
     "mp_engine_destroy": ([c_void_p], None),
     "mp_engine_info": ([c_void_p], c_char_p),
+    "mp_engine_health": ([c_void_p], c_char_p),
+    "mp_engine_trace": ([c_void_p, c_int, c_char_p], c_int),
     "mp_engine_generate": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p], c_char_p),
     "mp_engine_bench": ([c_void_p, c_int, c_int, c_int], c_char_p),
     "mp_engine_start": ([c_void_p, c_void_p, c_void_p, c_int], c_int),

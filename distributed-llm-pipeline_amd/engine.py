@@ -4,8 +4,10 @@
     out, stats = eng.generate([[1, 15, 27], [1, 99]], n_predict=32)
 
 Config keys mirror the C++ Engine (see engine.h): gguf | synthetic+ftype, mode ("local" or "mp"),
-stages, devices, link ("local" | "rccl"), n_mb, mb_size, max_ctx, prefill_chunk, split
-("even" | "mem" | "cost"), graphs, attn_split_len, verbose, log_file.
+stages, devices, link ("local" | "rccl" | "tcp"), backend ("hip" | "cpu"), n_mb, mb_size, max_ctx,
+prefill_chunk, split ("even" | "mem" | "cost"), graphs, fused_attn, prefill_gemm, attn_split_len,
+temp/top_k/top_p/min_p/seed (sampling), world/rank/hosts/next_host/base_port/rccl_ids (mp mode),
+threads (CPU backend), trace, watchdog_s, link_timeout_s, fault (fault injection), verbose, log_file.
 """
 from __future__ import annotations
 
@@ -73,6 +75,17 @@ class Engine:
 
     def bench(self, prompt_len: int, warmup: int, steps: int):
         return N.jcall(N.lib().mp_engine_bench, self._h, prompt_len, warmup, steps, what="bench")
+
+    def health(self) -> dict:
+        """Per-stage heartbeat (items done), link byte counters, ok=False after a pipeline fault."""
+        return N.jcall(N.lib().mp_engine_health, self._h, what="engine health")
+
+    def trace(self, on: bool = True):
+        N.check(N.lib().mp_engine_trace(self._h, int(on), None), "trace")
+
+    def write_trace(self, path: str):
+        """Chrome-trace JSON (chrome://tracing, Perfetto) of compute/send/recv spans per stage."""
+        N.check(N.lib().mp_engine_trace(self._h, 1, N.cstr(path)), "write trace")
 
     def logits(self, rows: int = 1, vocab: int | None = None):
         vocab = vocab or self.info["model"]["vocab"]

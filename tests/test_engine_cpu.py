@@ -141,3 +141,43 @@ def test_cpu_multiprocess_tcp_pipeline(native, model_dir, world):
         outs.append(o)
     last = [l for l in outs[-1].splitlines() if l.startswith("OUT ")]
     assert last and json.loads(last[0][4:]) == ref_out
+
+
+def test_fault_injection_fail_and_health(native, model_dir):
+    """A stage that throws mid-run aborts the links; the error surfaces with its cause and the
+    engine health turns not-ok."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=2, mb_size=1, stages=2, split="even",
+                fault={"stage": 1, "fail_at": 5}) as eng:
+        assert eng.health()["ok"]
+        with pytest.raises(RuntimeError, match="injected fault"):
+            eng.generate([[3, 4, 5], [6, 7]], 8)
+        assert not eng.health()["ok"]
+
+
+def test_fault_injection_dropped_message_times_out(native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=1, mb_size=1, stages=2, split="even",
+                link_timeout_s=1.5, fault={"stage": 0, "drop_send_at": 3}) as eng:
+        with pytest.raises(RuntimeError, match="timed out|aborted"):
+            eng.generate([[3, 4, 5]], 8)
+
+
+def test_fault_delay_and_trace(native, model_dir, tmp_path):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=2, mb_size=1, stages=2, split="even",
+                fault={"stage": 0, "delay_ms": 5}) as eng:
+        eng.trace(True)
+        out, _ = eng.generate([[3, 4, 5], [6, 7]], 6)
+        h = eng.health()
+        eng.write_trace(str(tmp_path / "t.json"))
+    assert h["ok"] and all(s["items_done"] > 0 for s in h["stages"])
+    assert h["stages"][0]["bytes_sent"] > 0
+    ev = json.load(open(tmp_path / "t.json"))["traceEvents"]
+    spans = [e for e in ev if e["ph"] == "X"]
+    assert {e["pid"] for e in spans} == {0, 1}
+    dec0 = [e for e in spans if e["pid"] == 0 and e["name"].startswith("decode")]
+    assert dec0 and all(e["dur"] >= 0 for e in dec0)

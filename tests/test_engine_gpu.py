@@ -188,3 +188,17 @@ def test_fused_decode_attention_matches_unfused(cuda, native, model_dir, name):
             res.append((out, lg))
     assert res[0][0] == res[1][0]
     assert nmse(res[1][1], res[0][1]) < 1e-6
+
+
+def test_prefill_gemm_matches_gemv_path(cuda, native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    rng = np.random.default_rng(9)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (200, 33, 70)]
+    res = []
+    for pg in (False, True):
+        with Engine(gguf=path, max_ctx=512, n_mb=1, mb_size=3, prefill_chunk=128, prefill_gemm=pg) as eng:
+            out, _ = eng.generate(prompts, 8)
+            res.append((out, eng.logits()))
+    assert res[0][0] == res[1][0]
+    assert nmse(res[1][1], res[0][1]) < 1e-5

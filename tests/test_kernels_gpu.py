@@ -227,3 +227,29 @@ def test_rope_kv_attention(cuda, native, hd, Hq, Hkv, mode):
         idx = torch.tensor([0, 1, 63, 64, 150, 299])
         ref = _ref_attention(q.float().cpu()[idx][:, :, :hd] * math.sqrt(hd), kref, vref, kvlen[idx])
         torch.testing.assert_close(out.view(S, Hq, hd)[idx], ref, rtol=5e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q5_K, Q.Q6_K, Q.Q8_0, Q.F16])
+@pytest.mark.parametrize("M", [17, 64, 100, 256])
+def test_gemm_prefill(cuda, native, qt, M):
+    """Prefill MFMA dequant-GEMM (64x64 tiles, LDS-staged X) vs torch fp32: STORE, ADD, SwiGLU."""
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
+    n, k = 208, 1280                     # 13 tiles (partial workgroup of 4), 5 super-blocks
+    raw, deq = _weights(qt, n, k, 300 + qt + M)
+    w = PackedWeight(raw, qt, n, k)
+    x = torch.randn(M, k)
+    xh = torch.zeros(M, w.k_pad, dtype=torch.float16)
+    xh[:, :k] = x.half()
+    ref = xh[:, :k].float() @ deq.T
+    y = gemm(w, xh.cuda(), EPI_STORE)
+    assert nmse(y.cpu(), ref) < 1e-5
+    base = torch.randn(M, n)
+    y2 = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda())
+    assert nmse(y2.cpu(), ref + base) < 1e-5
+    if qt in (Q.Q4_K, Q.Q8_0):
+        # interleaved gate/up rows: tile rows 0-7 gate, 8-15 up of the same 8 outputs
+        h = gemm(w, xh.cuda(), EPI_SWIGLU)
+        gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
+        g, u = ref[:, gi], ref[:, gi + 8]
+        href = torch.nn.functional.silu(g) * u
+        assert nmse(h.float().cpu(), href) < 1e-4

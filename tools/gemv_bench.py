@@ -31,14 +31,14 @@ def main():
     ap.add_argument("--splits", default="auto")
     ap.add_argument("--iters", type=int, default=24)
     ap.add_argument("--target", type=int, default=2048)
-    ap.add_argument("--probe", action="store_true", help="bandwidth probe: same loads, no dequant/MFMA")
+    ap.add_argument("--probe", type=int, default=0, help="3: loads only, 4: weight+x loads, 5: dequant+MFMA without x loads")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for sname in a.shapes.split(","):
         n, k, epi = SHAPES[sname]
         if a.probe:
-            epi = 3
+            epi = a.probe
         for tname in a.types.split(","):
             qt = TYPES[tname]
             if sname.endswith("head") and tname == "Q4_K":
