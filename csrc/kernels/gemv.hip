@@ -230,8 +230,23 @@ static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st)
 // Tiles per wave: with M > 4 the x fragments (16 rows x 32 k per MFMA) cost more L1/L2 traffic
 // than the weights themselves (3.5x at M = 16); sharing them across tiles pays.  Measured on
 // MI355X (tools/gemv_bench.py, 70B shapes): M = 16 gate/up 115 -> 67 us with 4 tiles per wave.
+void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, hipStream_t st);
+
+// kernel version (MIPIPE_GEMV_V: 1 = per-wave x loads, 2 = workgroup-shared x in LDS, default 2)
+// and waves per workgroup of v2 (MIPIPE_GEMV_NW: 4 or 8)
+static int g_ver = -1, g_nw = 8;
+static int gemv_version() {
+  if (g_ver < 0) {
+    const char* e = getenv("MIPIPE_GEMV_V");
+    g_ver = e ? atoi(e) : 2;
+    if (const char* w = getenv("MIPIPE_GEMV_NW")) g_nw = atoi(w) == 4 ? 4 : 8;
+  }
+  return g_ver;
+}
+
 int gemv_tiles_per_wave(int M, int epi) {
   (void)epi;
+  if (gemv_version() == 2) return 1;   // v2: one tile per wave, x shared through LDS
   if (g_tpw) return g_tpw;
   return M <= 4 ? 1 : 4;
 }
@@ -263,6 +278,7 @@ void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   if (nsplit < 1) nsplit = 1;
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
+  if (gemv_version() == 2 && epi < 3 && p.M <= 16) return launch_gemv2(ptype, epi, p, nsplit, g_nw, st);
   switch (ptype) {
     case P_Q4_K: launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
     case P_Q5_K: launch_pt<P_Q5_K>(epi, p, nsplit, st); break;

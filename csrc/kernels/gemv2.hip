@@ -1,0 +1,162 @@
+// Decode GEMV v2: workgroup-shared activations.
+//
+// Measured on MI355X (tools/gemv_bench.py probes, 70B gate/up, 264 MB Q4_K): weight loads alone
+// stream at 6-6.6 TB/s; dequant + MFMA alone (no x loads) at ~4.9 TB/s with one tile per wave;
+// but per-wave x fragment loads (8 x 1 KB wave-instructions per super-block, 16 rows at M = 16)
+// tripled the time at one tile per wave: the texture-address path, not HBM, was the limit.
+// v2 therefore keeps one 16-row weight tile per wave (best VALU/MFMA issue: several waves per
+// SIMD) and stages x ONCE per workgroup of NW waves into LDS (one 16 B load per thread per
+// super-block for 16 rows), from which every wave reads its A fragments with ds_read_b128.
+//
+//   grid (ceil(ntiles / NW), nsplit)   block NW * 64
+//   wave w of workgroup b: tile b*NW + w, super-blocks [sbA, sbB) of split blockIdx.y
+//
+// Ordering: x(sb+1) is issued BEFORE the weight refill of the current step, so waiting for it
+// (vmcnt) never drains the weight prefetches issued after it (vmcnt retires in issue order).
+#include "kcommon.h"
+#include "dequant.h"
+#include "../runtime/kernels_api.h"
+
+namespace mpk {
+using namespace mp;
+
+constexpr int G2_LDX = 256 + 8;   // padded f16 row in LDS (528 B): 16 rows of a fragment read hit distinct banks
+
+template <int PT, int EPI, int NW, int NSLOT>
+__global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB;
+  constexpr int NT = NW * 64;
+  __shared__ __attribute__((aligned(16))) f16 xs[2][16 * G2_LDX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int tile = blockIdx.x * NW + wave;
+  const int sbA = blockIdx.y * p.sb_per_split;
+  const int sbB = min(sbA + p.sb_per_split, p.nsb);
+  if (sbA >= sbB) return;   // uniform over the workgroup
+  const uint8_t* wt = p.W + (size_t)min(tile, p.ntiles - 1) * p.nsb * CB;
+  const int M = p.M;
+
+  // x staging: 16 rows x 256 k per super-block = 512 chunks of 16 B; thread t owns chunks t, t+NT..
+  // The x chunks of super-block j are loaded TOGETHER with its weights (register rings of NSLOT),
+  // NSLOT steps ahead, and copied to LDS one step before use: every vmcnt wait then leaves the
+  // loads of the NSLOT-1 later super-blocks in flight.
+  constexpr int XCH = (512 + NT - 1) / NT;
+  u32x4 xv[NSLOT][XCH];
+  typename D::Raw ring[NSLOT];
+  const int last = sbB - 1;
+  auto issue = [&](const int sl, const int sb) {
+    D::load(ring[sl], wt + (size_t)sb * CB, lane);
+#pragma unroll
+    for (int j = 0; j < XCH; ++j) {
+      const int c = tid + NT * j;
+      if (c < 512) {
+        const int row = c >> 5, col = (c & 31) * 8;
+        xv[sl][j] = row < M ? *reinterpret_cast<const u32x4*>(p.X + (size_t)row * p.ldx + (size_t)sb * 256 + col)
+                            : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  auto store_x = [&](const int sl, const int buf) {
+#pragma unroll
+    for (int j = 0; j < XCH; ++j) {
+      const int c = tid + NT * j;
+      if (c < 512) {
+        const int row = c >> 5, col = (c & 31) * 8;
+        *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + col]) = xv[sl][j];
+      }
+    }
+  };
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sbA + sl, last));
+  store_x(0, 0);
+  __syncthreads();
+
+  // rows >= M are zero in LDS (their outputs are never stored)
+  const f16* xrow0 = &xs[0][r * G2_LDX + 8 * g];
+  const f16* xrow1 = &xs[1][r * G2_LDX + 8 * g];
+  // one super-block; all loads unconditional (clamped to the range): path-independent vmcnt
+  auto step = [&](const int sl, const int cur) {
+    const int buf = (cur - sbA) & 1;
+    const f16* xr = buf ? xrow1 : xrow0;
+    half8_t b[4];
+    D::template dequant<0>(ring[sl], b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 32 * s), b[s], acc);
+    D::template dequant<1>(ring[sl], b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 128 + 32 * s), b[s], acc);
+    store_x((sl + 1) % NSLOT, buf ^ 1);            // x(cur + 1), loaded NSLOT - 1 steps ago
+    issue(sl, min(cur + NSLOT, last));
+    __syncthreads();
+  };
+  int sb = sbA;
+  for (; sb + NSLOT <= sbB; sb += NSLOT) {
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) step(sl, sb + sl);
+  }
+#pragma unroll
+  for (int sl = 0; sl < NSLOT - 1; ++sl)   // tail (< NSLOT super-blocks; uniform over the workgroup)
+    if (sb + sl < sbB) step(sl, sb + sl);
+  if (tile >= p.ntiles) return;
+  // lane holds C[m = 4g + i][n = 16*tile + r]
+  if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float other = __shfl_xor(acc[i], 8);
+      const int m = 4 * g + i;
+      const int o = tile * 8 + r;
+      if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[i]) * other);
+    }
+  } else {
+    const int n = tile * 16 + r;
+    if (n < p.n_valid) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 4 * g + i;
+        if (m < M) {
+          float* dst = p.Y + (size_t)m * p.ldy + n;
+          if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i]);
+          else *dst = acc[i];
+        }
+      }
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+template <int PT, int NW, int NSLOT>
+static void gemv2_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+  dim3 grid((p.ntiles + NW - 1) / NW, nsplit);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI_STORE, NW, NSLOT>), grid, dim3(NW * 64), 0, st, p); break;
+    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI_ATOMIC, NW, NSLOT>), grid, dim3(NW * 64), 0, st, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI_SWIGLU, NW, NSLOT>), grid, dim3(NW * 64), 0, st, p); break;
+  }
+}
+
+template <int PT>
+static void gemv2_pt(int epi, const GemvParams& p, int nsplit, int nw, hipStream_t st) {
+  if (nw == 8) gemv2_cfg<PT, 8, 4>(epi, p, nsplit, st);
+  else gemv2_cfg<PT, 4, 4>(epi, p, nsplit, st);
+}
+
+// p.sb_per_split must be set by the caller (launch_gemv does)
+void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, hipStream_t st) {
+  switch (ptype) {
+    case P_Q4_K: gemv2_pt<P_Q4_K>(epi, p, nsplit, nw, st); break;
+    case P_Q5_K: gemv2_pt<P_Q5_K>(epi, p, nsplit, nw, st); break;
+    case P_Q6_K: gemv2_pt<P_Q6_K>(epi, p, nsplit, nw, st); break;
+    case P_Q8_0: gemv2_pt<P_Q8_0>(epi, p, nsplit, nw, st); break;
+    case P_Q4_0: gemv2_pt<P_Q4_0>(epi, p, nsplit, nw, st); break;
+    case P_F16: gemv2_pt<P_F16>(epi, p, nsplit, nw, st); break;
+  }
+}
+
+}  // namespace mp
