@@ -226,6 +226,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
 
   const int start = z * p.split_len;
   const int end = min(start + p.split_len, kvlen);
+  // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
+  // single active split writes the output directly, so short contexts pay no merge round trip
+  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
+  if (z >= n_act) return;
 
   // 1. append the new token's K (rotated) and V to the cache (the split that will read it)
   if (start <= pos && pos < end) {
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     }
     const int hh = kvh * G + r;
     const size_t rid = (size_t)t * p.Hq + hh;
-    if (p.n_split == 1) {
+    if (n_act == 1) {
       if (d < p.hd) p.out[(size_t)t * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
     } else {
       st_sc1(p.o_part + ((size_t)z * stride + rid) * DP + d, O);
@@ -369,14 +373,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
       }
     }
   }
-  if (p.n_split == 1) return;
+  if (n_act == 1) return;
   // 4. last arriver of this (token, kv head) merges the splits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const int old = __hip_atomic_fetch_add(p.counters + (size_t)t * p.Hkv + kvh, 1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-    sm_last = old == p.n_split - 1;
+    sm_last = old == n_act - 1;
   }
   __syncthreads();
   if (!sm_last) return;
@@ -385,9 +389,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     const int hh = kvh * G + r;
     const size_t rid = (size_t)t * p.Hq + hh;
     float M = -INFINITY;
-    for (int zz = 0; zz < p.n_split; ++zz) M = fmaxf(M, ld_sc1(p.ml_part + (zz * stride + rid) * 2));
+    for (int zz = 0; zz < n_act; ++zz) M = fmaxf(M, ld_sc1(p.ml_part + (zz * stride + rid) * 2));
     float L = 0.f, O = 0.f;
-    for (int zz = 0; zz < p.n_split; ++zz) {
+    for (int zz = 0; zz < n_act; ++zz) {
       const float mz = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
       if (mz == -INFINITY) continue;
       const float f = __expf(mz - M);

@@ -213,6 +213,8 @@ void CpuStage::alloc_runtime() {
     pos_.emplace_back(std::max(B, 16), 0);
   }
   prompt_.assign((size_t)n_slots * opt_.max_ctx, 0);
+  if (spec_.last())
+    for (int mb = 0; mb < NM; ++mb) last_h_.emplace_back((size_t)B * d, 0.f);
   if (spec_.last()) logits_.assign((size_t)B * cfg_.vocab, 0.f);
   xn_.resize((size_t)rows * d);
   qkv_.resize((size_t)rows * (cfg_.q_dim() + 2 * cfg_.kv_dim()));
@@ -400,20 +402,40 @@ void CpuStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt) {
   for (int m = 0; m < M; ++m) tok_out[m] = sample_row(logits_.data() + (size_t)m * cfg_.vocab, salt, m);
 }
 
-void CpuStage::prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens, bool last_chunk, hipStream_t) {
-  if (T > opt_.prefill_chunk) throw std::runtime_error("prefill chunk too large");
-  if (p0 + T > opt_.max_ctx) throw std::runtime_error("prompt exceeds context");
-  const int d = cfg_.d_model, sl = mb * opt_.mb_size + b;
+void CpuStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t) {
+  const int d = cfg_.d_model;
   float* x = act_[mb].data();
-  if (spec_.first())
-    for (int t = 0; t < T; ++t) {
-      if (tokens[t] < 0 || tokens[t] >= cfg_.vocab) throw std::runtime_error("token id out of range");
-      dequant_row(embd_.type, embd_.data + (size_t)tokens[t] * embd_.rb, x + (size_t)t * d, d);
+  std::vector<int32_t> pos, slot;
+  for (const PrefillSeg& s : segs) {
+    if (s.p0 + s.T > opt_.max_ctx) throw std::runtime_error("prompt exceeds context");
+    const int sl = mb * opt_.mb_size + s.b;
+    for (int t = 0; t < s.T; ++t) {
+      const int row = (int)pos.size();
+      pos.push_back(s.p0 + t);
+      slot.push_back(sl);
+      if (spec_.first()) {
+        const int32_t tok = prompt_[(size_t)sl * opt_.max_ctx + s.p0 + t];
+        if (tok < 0 || tok >= cfg_.vocab) throw std::runtime_error("token id out of range");
+        dequant_row(embd_.type, embd_.data + (size_t)tok * embd_.rb, x + (size_t)row * d, d);
+      }
     }
-  std::vector<int32_t> pos(T), slot(T, sl);
-  for (int t = 0; t < T; ++t) pos[t] = p0 + t;
+  }
+  const int T = (int)pos.size();
+  if (T > opt_.prefill_chunk) throw std::runtime_error("prefill chunk too large");
+  // rows carry their own slot and position, so the packed chunk runs as one batch (the causal
+  // mask per row is its position; other sequences' rows are in other slots)
   for (size_t li = 0; li < layers_.size(); ++li) layer_forward((int)li, T, x, pos.data(), slot.data());
-  if (spec_.last() && last_chunk) head(1, x + (size_t)(T - 1) * d, tok_[mb].data() + b, 1000003ULL + sl);
+  if (spec_.last()) {
+    int row = 0;
+    for (const PrefillSeg& s : segs) {
+      row += s.T;
+      if (s.last) std::memcpy(last_h_[mb].data() + (size_t)s.b * d, x + (size_t)(row - 1) * d, (size_t)d * 4);
+    }
+  }
+}
+
+void CpuStage::prefill_finish(int mb, hipStream_t) {
+  if (spec_.last()) head(opt_.mb_size, last_h_[mb].data(), tok_[mb].data(), 1000003ULL + (uint64_t)mb);
 }
 
 void CpuStage::decode(int mb, hipStream_t) {

@@ -40,7 +40,8 @@ class CpuStage : public Stage {
   int32_t* tokens(int mb) override { return tok_[mb].data(); }
   int32_t* prompt_buf() override { return prompt_.data(); }
   void set_positions(int mb, const std::vector<int32_t>& pos) override;
-  void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens, bool last_chunk, hipStream_t st) override;
+  void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
+  void prefill_finish(int mb, hipStream_t st) override;
   void decode(int mb, hipStream_t st) override;
   const float* logits_ptr() const override { return logits_.data(); }
   int logits_ld() const override { return cfg_.vocab; }
@@ -80,6 +81,7 @@ class CpuStage : public Stage {
   std::vector<std::vector<float>> act_;
   std::vector<std::vector<int32_t>> tok_, pos_;
   std::vector<int32_t> prompt_;
+  std::vector<std::vector<float>> last_h_;   // last stage: [mb][B][d] final prompt rows
   std::vector<float> logits_;
   // scratch
   std::vector<float> xn_, qkv_, att_, h_, gu_;

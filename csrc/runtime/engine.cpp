@@ -138,10 +138,11 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.max_ctx = max_ctx_;
   so.prefill_chunk = chunk_;
   so.use_graphs = j.get_bool("graphs", true);
-  so.attn_split_len = j.get_int("attn_split_len", 128);
+  so.attn_split_len = j.get_int("attn_split_len", 0);   // 0 = auto
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
+  packed_prefill_ = j.get_bool("packed_prefill", true);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {
@@ -374,16 +375,16 @@ void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
     switch (it.kind) {
       case Item::PREFILL: {
         if (!first) recv(mb, st.act(mb), (size_t)it.T * d4, "act");
-        span(w, nullptr, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T), [&] {
-          st.prefill_chunk(mb, it.b, it.p0, it.T,
-                           first ? st.prompt_buf() + (size_t)(mb * B_ + it.b) * max_ctx_ + it.p0 : nullptr,
-                           it.last_chunk, nullptr);
-        });
+        span(w, nullptr, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T),
+             [&] { st.prefill(mb, it.segs, nullptr); });
         if (!last) send(mb, st.act(mb), (size_t)it.T * d4, "act");
         break;
       }
       case Item::PREFILL_END: {
-        if (last) std::memcpy(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4);
+        if (last) {
+          span(w, nullptr, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, nullptr); });
+          std::memcpy(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4);
+        }
         if (S_ > 1) {
           if (last) send(mb, st.tokens(mb), (size_t)B_ * 4, "tok");
           if (first) w.ring_pending[mb] = true;
@@ -458,17 +459,17 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         const size_t bytes = (size_t)it.T * d4;
         if (!first) recv_into(mb, st.act(mb), bytes);
         else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
-        const int slot = mb * B_ + it.b;
-        span(w, cs, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T), [&] {
-          st.prefill_chunk(mb, it.b, it.p0, it.T, first ? st.prompt_buf() + (size_t)slot * max_ctx_ + it.p0 : nullptr,
-                           it.last_chunk, cs);
-        });
+        span(w, cs, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T),
+             [&] { st.prefill(mb, it.segs, cs); });
         if (!last) send_from(mb, st.act(mb), bytes);
         break;
       }
       case Item::PREFILL_END: {
-        if (last) HIP_OK(hipMemcpyAsync(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4,
-                                        hipMemcpyDeviceToHost, cs));
+        if (last) {
+          span(w, cs, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, cs); });
+          HIP_OK(hipMemcpyAsync(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4, hipMemcpyDeviceToHost,
+                                cs));
+        }
         if (S_ > 1) {
           if (last) send_from(mb, st.tokens(mb), (size_t)B_ * 4);
           if (first) post_ring_recv(w, mb);
@@ -664,17 +665,31 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
       }
     }
   }
+  // packed prefill: the prompts of a micro-batch are cut into chunks of up to chunk_ rows that may
+  // hold several sequences, so each projection reads its weights once per chunk (not per sequence)
   for (int mb = 0; mb < M_; ++mb) {
+    Item it{Item::PREFILL};
+    it.mb = mb;
+    auto flush = [&] {
+      if (it.T > 0) items.push_back(it);
+      it.segs.clear();
+      it.T = 0;
+    };
     for (int b = 0; b < B_; ++b) {
       const size_t i = (size_t)mb * B_ + b;
       if (i >= prompts.size()) continue;
       const int n = (int)prompts[i].size();
-      for (int p0 = 0; p0 < n; p0 += chunk_) {
-        Item it{Item::PREFILL};
-        it.mb = mb; it.b = b; it.p0 = p0; it.T = std::min(chunk_, n - p0); it.last_chunk = p0 + it.T >= n;
-        items.push_back(it);
+      for (int p0 = 0; p0 < n;) {
+        const int take = std::min(chunk_ - it.T, n - p0);
+        PrefillSeg sg;
+        sg.b = b; sg.p0 = p0; sg.T = take; sg.last = p0 + take >= n;
+        it.segs.push_back(sg);
+        it.T += take;
+        p0 += take;
+        if (it.T == chunk_ || !packed_prefill_) flush();
       }
     }
+    flush();
     Item e{Item::PREFILL_END};
     e.mb = mb;
     items.push_back(e);

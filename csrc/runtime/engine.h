@@ -34,8 +34,9 @@ class GgufFile;
 
 struct Item {
   enum Kind { PREFILL, PREFILL_END, DECODE } kind;
-  int mb = 0, b = 0, p0 = 0, T = 0;
-  bool last_chunk = false;
+  int mb = 0;
+  int T = 0;                      // PREFILL: total rows of the packed chunk
+  std::vector<PrefillSeg> segs;   // PREFILL: sequences (segments) packed into the chunk
   int round = 0;
 };
 
@@ -127,6 +128,7 @@ class Engine {
   std::vector<int32_t> out_vec_;                   // CPU backend storage of out_host_
   bool cpu_ = false;
   bool trace_ = false, failed_ = false;
+  bool packed_prefill_ = true;   // several sequences per prefill chunk (config "packed_prefill")
   double trace_t0_ = 0, watchdog_s_ = 600;
   std::vector<std::string> trace_events_;
   Json fault_;

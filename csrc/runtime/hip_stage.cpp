@@ -339,7 +339,15 @@ void HipStage::alloc_runtime() {
     logits_ld_ = (int)round_up(cfg_.vocab, 16);
     logits_ = (float*)zalloc((size_t)B * logits_ld_ * 4);
   }
-  const int split = std::max(128, (int)round_up(opt_.attn_split_len, 128));
+  int split = opt_.attn_split_len;
+  if (split <= 0) {
+    // auto: enough (sequence, kv head, split) workgroups to cover the CUs, but >= 256 keys per
+    // split (a split merge costs a publish/acquire round trip; short contexts use one split)
+    const int pairs = std::max(1, B * Hkv);
+    const int want = std::max(1, std::min((256 + pairs - 1) / pairs, (opt_.max_ctx + 255) / 256));
+    split = (opt_.max_ctx + want - 1) / want;
+  }
+  split = std::max(128, (int)round_up(split, 128));
   opt_.attn_split_len = split;
   n_split_ = (int)((opt_.max_ctx + split - 1) / split);
   if (n_split_ > 1) {
@@ -391,6 +399,8 @@ void HipStage::alloc_runtime() {
   pf_kvlen_ = (int32_t*)zalloc((size_t)opt_.prefill_chunk * 4);
   pf_slot_ = (int32_t*)zalloc((size_t)opt_.prefill_chunk * 4);
   prompt_dev_ = (int32_t*)zalloc((size_t)n_slots * opt_.max_ctx * 4);
+  if (spec_.last())
+    for (int mb = 0; mb < NM; ++mb) last_h_.push_back((float*)zalloc((size_t)B * d * 4));
   HIP_OK(hipDeviceSynchronize());
   MP_LOGI("stage %d: layers %d-%d offloaded to GPU %d (%s), weights %.2f GiB, KV %.2f GiB (%d slots x %d ctx)",
           spec_.stage, spec_.layer_begin, spec_.layer_end - 1, spec_.device,
@@ -502,7 +512,20 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       ap.split_len = (int)round_up(opt_.max_ctx, 128);
       ap.n_split = 1;
     }
-    launch_attention(ap, st);
+    if (!decode && segs_ && segs_->size() > 1) {
+      // packed prefill: a row group of the attention kernel must belong to one sequence
+      int row = 0;
+      for (const PrefillSeg& s : *segs_) {
+        AttnParams a = ap;
+        a.q = q_ + (size_t)row * cfg_.n_head * Dp_;
+        a.kvlen = kvlen + row; a.slot = slot + row; a.M = s.T;
+        a.out = attn_ + (size_t)row * Ko_;
+        launch_attention(a, st);
+        row += s.T;
+      }
+    } else {
+      launch_attention(ap, st);
+    }
   }
   gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
   launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
@@ -536,18 +559,37 @@ void HipStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipS
   }
 }
 
-void HipStage::prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk,
-                             hipStream_t st) {
-  if (T > opt_.prefill_chunk) throw std::runtime_error("prefill chunk too large");
-  if (p0 + T > opt_.max_ctx) throw std::runtime_error("prompt exceeds context");
-  const int sl = slot_of(mb, b);
-  launch_prefill_meta(pf_pos_, pf_kvlen_, pf_slot_, p0, T, sl, st);
+void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) {
+  const int d = cfg_.d_model;
   float* x = act_[mb];
-  if (spec_.first()) launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tokens_dev, T, x,
-                                  cfg_.d_model, st);
+  int T = 0;
+  for (const PrefillSeg& s : segs) {
+    if (s.p0 + s.T > opt_.max_ctx) throw std::runtime_error("prompt exceeds context");
+    const int sl = slot_of(mb, s.b);
+    launch_prefill_meta(pf_pos_ + T, pf_kvlen_ + T, pf_slot_ + T, s.p0, s.T, sl, st);
+    if (spec_.first())
+      launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, d, prompt_dev_ + (size_t)sl * opt_.max_ctx + s.p0,
+                   s.T, x + (size_t)T * d, d, st);
+    T += s.T;
+  }
+  if (T > opt_.prefill_chunk) throw std::runtime_error("prefill chunk too large");
+  segs_ = &segs;
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, T, x, pf_pos_, pf_kvlen_, pf_slot_, false, st);
-  if (spec_.last() && last_chunk) head(1, x + (size_t)(T - 1) * cfg_.d_model, tok_[mb] + b, 1000003ULL + sl, st);
+  segs_ = nullptr;
+  if (spec_.last()) {
+    int row = 0;
+    for (const PrefillSeg& s : segs) {
+      row += s.T;
+      if (s.last)
+        HIP_OK(hipMemcpyAsync(last_h_[mb] + (size_t)s.b * d, x + (size_t)(row - 1) * d, (size_t)d * 4,
+                              hipMemcpyDeviceToDevice, st));
+    }
+  }
+}
+
+void HipStage::prefill_finish(int mb, hipStream_t st) {
+  if (spec_.last()) head(opt_.mb_size, last_h_[mb], tok_[mb], 1000003ULL + (uint64_t)mb, st);
 }
 
 void HipStage::decode_eager(int mb, hipStream_t st) {

@@ -90,11 +90,9 @@ class HipStage : public Stage {
   // positions of micro-batch mb (host values) before decode; kvlen = pos + 1
   void set_positions(int mb, const std::vector<int32_t>& pos) override;
 
-  // Prefill T tokens of sequence (mb, b) starting at position p0.  First stage: tokens_dev holds
-  // the T token ids (device); otherwise act(mb) holds the incoming activations.  On the last
-  // stage and `last_chunk`, the next token is written to tokens(mb)[b].
-  void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens_dev, bool last_chunk,
-                     hipStream_t st) override;
+  // packed prefill chunk (see Stage::prefill) and the head over the kept last rows
+  void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
+  void prefill_finish(int mb, hipStream_t st) override;
 
   // One decode step for micro-batch mb (graph replay if captured).
   void decode(int mb, hipStream_t st) override;
@@ -164,6 +162,8 @@ class HipStage : public Stage {
   // prefill metadata
   int32_t* pf_pos_ = nullptr; int32_t* pf_kvlen_ = nullptr; int32_t* pf_slot_ = nullptr;
   int32_t* prompt_dev_ = nullptr;
+  std::vector<float*> last_h_;                       // last stage: [mb][B][d] final prompt rows
+  const std::vector<PrefillSeg>* segs_ = nullptr;    // segments of the prefill in progress
   // graphs
   std::vector<hipGraphExec_t> graphs_;
 };

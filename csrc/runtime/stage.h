@@ -21,10 +21,17 @@ struct StageOptions {
   int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
   int prefill_chunk = 256;  // max tokens per prefill chunk
   bool use_graphs = true;
-  int attn_split_len = 128; // decode flash-decoding split length (multiple of 128)
+  int attn_split_len = 0;   // decode flash-decoding split length (multiple of 128; 0 = auto)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
+};
+
+struct PrefillSeg {
+  int b = 0;          // sequence row within the micro-batch
+  int p0 = 0;         // first position of this segment
+  int T = 0;          // tokens
+  bool last = false;  // ends the prompt
 };
 
 class Stage {
@@ -43,8 +50,14 @@ class Stage {
   virtual int32_t* tokens(int mb) = 0;     // [mb_size]
   virtual int32_t* prompt_buf() = 0;       // [n_slots][max_ctx] token ids (first stage)
   virtual void set_positions(int mb, const std::vector<int32_t>& pos) = 0;
-  virtual void prefill_chunk(int mb, int b, int p0, int T, const int32_t* tokens, bool last_chunk,
-                             hipStream_t st) = 0;
+  // Packed prefill: one chunk = segments of several sequences of micro-batch mb (rows stacked in
+  // segment order, sum of T <= prefill_chunk).  The projections run as ONE GEMM over all rows
+  // (weights read once per chunk, not per sequence); attention runs per segment.  The first
+  // stage embeds the tokens from prompt_buf(); for a segment with `last` set, the last stage
+  // keeps the final row's hidden state for prefill_finish().
+  virtual void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) = 0;
+  // last stage: LM head + sampling over the kept rows -> tokens(mb)[b] for every sequence of mb
+  virtual void prefill_finish(int mb, hipStream_t st) = 0;
   virtual void decode(int mb, hipStream_t st) = 0;
   virtual const float* logits_ptr() const = 0;   // last computed logits (device/host)
   virtual int logits_ld() const = 0;
