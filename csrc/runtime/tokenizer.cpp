@@ -1,4 +1,5 @@
 #include "tokenizer.h"
+#include "unicode_tables.h"
 
 #include <algorithm>
 #include <climits>
@@ -52,43 +53,10 @@ std::string utf8_encode(uint32_t cp) {
 
 // ------------------------------------------------------------------ Unicode categories (compact)
 namespace {
-struct Range { uint32_t a, b; };
-// \p{L}: letters of the major scripts (Latin, Greek, Cyrillic, Armenian, Hebrew, Arabic, Indic,
-// Thai, Georgian, Hangul, Kana, CJK, fullwidth Latin, ...).
-const Range kLetters[] = {
-    {0x41, 0x5A}, {0x61, 0x7A}, {0xAA, 0xAA}, {0xB5, 0xB5}, {0xBA, 0xBA}, {0xC0, 0xD6}, {0xD8, 0xF6},
-    {0xF8, 0x2C1}, {0x2C6, 0x2D1}, {0x2E0, 0x2E4}, {0x2EC, 0x2EC}, {0x2EE, 0x2EE}, {0x370, 0x374}, {0x376, 0x377},
-    {0x37A, 0x37D}, {0x37F, 0x37F}, {0x386, 0x386}, {0x388, 0x3FF}, {0x400, 0x481}, {0x48A, 0x52F},
-    {0x531, 0x556}, {0x559, 0x559}, {0x560, 0x588}, {0x5D0, 0x5EA}, {0x5EF, 0x5F2}, {0x620, 0x64A},
-    {0x66E, 0x66F}, {0x671, 0x6D3}, {0x6D5, 0x6D5}, {0x6E5, 0x6E6}, {0x6EE, 0x6EF}, {0x6FA, 0x6FC},
-    {0x6FF, 0x6FF}, {0x710, 0x710}, {0x712, 0x72F}, {0x74D, 0x7A5}, {0x904, 0x939}, {0x93D, 0x93D},
-    {0x950, 0x950}, {0x958, 0x961}, {0x971, 0x980}, {0x985, 0x9B9}, {0xA05, 0xA39}, {0xA85, 0xAB9},
-    {0xB05, 0xB39}, {0xB83, 0xBB9}, {0xC05, 0xC39}, {0xC85, 0xCB9}, {0xD05, 0xD3A}, {0xD85, 0xDC6},
-    {0xE01, 0xE30}, {0xE32, 0xE33}, {0xE40, 0xE46}, {0xE81, 0xEB0}, {0xF00, 0xF00}, {0xF40, 0xF6C},
-    {0x1000, 0x102A}, {0x10A0, 0x10FF}, {0x1100, 0x1248}, {0x1250, 0x135A}, {0x13A0, 0x13F5},
-    {0x1401, 0x166C}, {0x1780, 0x17B3}, {0x1820, 0x1878}, {0x1E00, 0x1F15}, {0x1F18, 0x1FFC},
-    {0x2071, 0x2071}, {0x207F, 0x207F}, {0x2090, 0x209C}, {0x2102, 0x2102}, {0x2107, 0x2107},
-    {0x210A, 0x2113}, {0x2115, 0x2115}, {0x2119, 0x211D}, {0x2124, 0x2124}, {0x2126, 0x2126},
-    {0x2128, 0x2128}, {0x212A, 0x212D}, {0x212F, 0x2139}, {0x2C00, 0x2CE4}, {0x2D00, 0x2D25},
-    {0x3005, 0x3006}, {0x3031, 0x3035}, {0x303B, 0x303C}, {0x3041, 0x3096}, {0x309D, 0x309F},
-    {0x30A1, 0x30FA}, {0x30FC, 0x30FF}, {0x3105, 0x312F}, {0x3131, 0x318E}, {0x31A0, 0x31BF},
-    {0x31F0, 0x31FF}, {0x3400, 0x4DBF}, {0x4E00, 0x9FFF}, {0xA000, 0xA48C}, {0xA4D0, 0xA4FD},
-    {0xA500, 0xA60C}, {0xA640, 0xA66E}, {0xA680, 0xA69D}, {0xA722, 0xA788}, {0xA78B, 0xA7CA},
-    {0xAC00, 0xD7A3}, {0xF900, 0xFA6D}, {0xFB00, 0xFB06}, {0xFB1D, 0xFB4F}, {0xFB50, 0xFDFB},
-    {0xFE70, 0xFEFC}, {0xFF21, 0xFF3A}, {0xFF41, 0xFF5A}, {0xFF66, 0xFFDC}, {0x10000, 0x1FFFF},
-    {0x20000, 0x3134F},
-};
-// \p{N}: Nd + Nl + No of common scripts
-const Range kNumbers[] = {
-    {0x30, 0x39}, {0xB2, 0xB3}, {0xB9, 0xB9}, {0xBC, 0xBE}, {0x660, 0x669}, {0x6F0, 0x6F9}, {0x7C0, 0x7C9},
-    {0x966, 0x96F}, {0x9E6, 0x9EF}, {0xA66, 0xA6F}, {0xAE6, 0xAEF}, {0xB66, 0xB6F}, {0xBE6, 0xBF2},
-    {0xC66, 0xC6F}, {0xCE6, 0xCEF}, {0xD66, 0xD78}, {0xE50, 0xE59}, {0xED0, 0xED9}, {0xF20, 0xF33},
-    {0x1040, 0x1049}, {0x1369, 0x137C}, {0x17E0, 0x17E9}, {0x1810, 0x1819}, {0x2070, 0x2070},
-    {0x2074, 0x2079}, {0x2080, 0x2089}, {0x2150, 0x2182}, {0x2185, 0x2189}, {0x2460, 0x249B},
-    {0x24EA, 0x24FF}, {0x2776, 0x2793}, {0x2CFD, 0x2CFD}, {0x3007, 0x3007}, {0x3021, 0x3029},
-    {0x3038, 0x303A}, {0x3192, 0x3195}, {0x3220, 0x3229}, {0x3248, 0x324F}, {0x3251, 0x325F},
-    {0x3280, 0x3289}, {0x32B1, 0x32BF}, {0xA620, 0xA629}, {0xFF10, 0xFF19},
-};
+using uc::Range;
+using uc::kLetters;
+using uc::kNumbers;
+using uc::kSpaces;
 template <size_t N>
 bool in_ranges(const Range (&r)[N], uint32_t cp) {
   size_t lo = 0, hi = N;
@@ -104,11 +72,7 @@ bool in_ranges(const Range (&r)[N], uint32_t cp) {
 
 bool uc_is_letter(uint32_t cp) { return cp >= 0x41 && in_ranges(kLetters, cp); }
 bool uc_is_number(uint32_t cp) { return cp >= 0x30 && in_ranges(kNumbers, cp); }
-bool uc_is_space(uint32_t cp) {
-  return cp == 0x20 || (cp >= 0x09 && cp <= 0x0D) || cp == 0x85 || cp == 0xA0 || cp == 0x1680 ||
-         (cp >= 0x2000 && cp <= 0x200A) || cp == 0x2028 || cp == 0x2029 || cp == 0x202F || cp == 0x205F ||
-         cp == 0x3000;
-}
+bool uc_is_space(uint32_t cp) { return cp >= 0x09 && in_ranges(kSpaces, cp); }
 
 // ------------------------------------------------------------------ Llama-3 pre-tokenizer
 // (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+
