@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--link", default="rccl", choices=["rccl", "tcp"], help="stage-to-stage transport (N > 1)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra engine option (A/B runs), e.g. --set fused_norm=false")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -71,6 +73,9 @@ def main():
     max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
     cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
                prefill_chunk=256, graphs=not args.no_graphs, split="cost", seed=1234)
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        cfg[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
     if world > 1:
         cfg.update(mode="mp", world=world, rank=rank, device=local_rank, link=args.link)
         if args.link == "rccl":

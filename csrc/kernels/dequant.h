@@ -70,7 +70,27 @@ template <> struct Deq<P_Q4_K> {
     r.q1 = ld16_nt(c + 1024 + lane * 16);
     r.hdr = ld16(c + 2048 + (lane & 15) * 16);
   }
-  // EXPERIMENT (timing only, drops the min term): B = fma(x_magic, S, T), T = -offset*S exact
+  // Min-free dequant: B = fma(x_magic, S, T) with T = -offset * S EXACT (power-of-two multiple of
+  // an f16), i.e. B = q * S rounded once; the "- dmin * m" term of every 32-weight sub-block is
+  // left to one extra MFMA per 4 super-blocks against the sub-block sums of x (mins() below):
+  // 2 VALU ops per f16 pair instead of 3.
+  // mins of the 8 sub-blocks of this super-block as the B fragment of that MFMA: -dmin * m_j
+  __device__ static __forceinline__ half8_t mins(const Raw& r) {
+    const half2_t dm = as_h2(r.hdr.x);
+    const uint32_t S0 = r.hdr.y, S1 = r.hdr.z, S2 = r.hdr.w;
+    (void)S0;
+    const uint32_t m03 = S1 & 0x3F3F3F3Fu;
+    const uint32_t m47 = ((S2 >> 4) & 0x0F0F0F0Fu) | ((S1 >> 2) & 0x30303030u);
+    const half2_t nd = -h2hi(dm), c = h2hi(dm) * h2c(1024.f);   // exact: power-of-two multiple
+    const Consts k = make_consts();
+    auto cv = [&](uint32_t v) { return as_u32(__builtin_elementwise_fma(as_h2(and_or(v, 0x00FF00FFu, k.mag_hi)), nd, c)); };
+    // pairs (m0,m2),(m1,m3) -> reorder to m0..m7 in j order
+    const half2_t a02 = as_h2(cv(m03)), a13 = as_h2(cv(m03 >> 8)), b02 = as_h2(cv(m47)), b13 = as_h2(cv(m47 >> 8));
+    half8_t o;
+    o[0] = a02.x; o[1] = a13.x; o[2] = a02.y; o[3] = a13.y;
+    o[4] = b02.x; o[5] = b13.x; o[6] = b02.y; o[7] = b13.y;
+    return o;
+  }
   template <int H>
   __device__ static __forceinline__ void dequant_fast(const Raw& r, half8_t b[4], int lane) {
     const half2_t dm = as_h2(r.hdr.x);
