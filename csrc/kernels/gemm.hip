@@ -70,10 +70,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
       else D::template dequant<1>(raw[cur], b, lane);
 #pragma unroll
       for (int ms = 0; ms < 4; ++ms) {
-        const f16* xr = &xs[cur][(16 * ms + r) * GM_LDX + 128 * h + 8 * g];
+        const f16* xr = &xs[cur][(16 * ms + r) * GM_LDX + t16_xoff(g, 4 * h)];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const half8_t a = *reinterpret_cast<const half8_t*>(xr + 32 * s);
+          const half8_t a = *reinterpret_cast<const half8_t*>(xr + 8 * s);
           acc[ms] = mfma16x16x32(a, b[s], acc[ms]);
         }
       }

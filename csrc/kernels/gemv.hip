@@ -20,7 +20,7 @@
 
 namespace mpk {
 
-template <int PT, int EPI, int WPB, int TPW, int NSLOT, bool XR>
+template <int PT, int EPI, int WPB, int TPW, int NSLOT>
 __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) {
   // TPW tiles per wave share every x fragment (x traffic / weight traffic = 3.5 / TPW at M = 16);
   // NSLOT super-blocks per tile are kept in flight in a compile-time indexed register ring.
@@ -43,24 +43,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
 #pragma unroll
   for (int t = 0; t < TPW; ++t) wt[t] = p.W + (size_t)min(tile0 + t, p.ntiles - 1) * p.nsb * CB;
   // rows m >= M read row M-1 (clamped address, no exec masking); their outputs are never stored
-  const f16* xp = p.X + (size_t)min(r, p.M - 1) * p.ldx + 8 * g;
+  const f16* xp = p.X + (size_t)min(r, p.M - 1) * p.ldx + t16_xoff(g, 0);
 
   f32x4 acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int last = sb1 - 1;
-  // Register ring of NSLOT super-blocks.  XR: the x fragments of a slot are loaded together with
-  // its weights (vmcnt retires loads in issue order, so x fetched at use waits for every weight
-  // prefetch in flight) at the price of 32 VGPRs per slot; !XR: x fetched at use.
+  // Register ring of NSLOT super-blocks; x fragments are fetched at use (an x-in-ring variant
+  // measured slower: 32 VGPRs per slot)
   typename D::Raw ring[NSLOT][TPW];
-  half8_t xr[1][8];   // (x-in-ring variant measured slower: VGPR cost)
+  half8_t xr[1][8];
   auto issue = [&](int sl, int sbi) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) D::load(ring[sl][t], wt[t] + (size_t)sbi * CB, lane);
-    if constexpr (false) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) xr[sl][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)sbi * 256 + 32 * i);
-    }
   };
 #pragma unroll
   // (a wave with an empty K share still loads a valid super-block of its workgroup's range)
@@ -82,7 +77,7 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
           }
         } else if constexpr (EPI == 4) {   // probe: weight + x loads, no dequant / MFMA
 #pragma unroll
-          for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+          for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 8 * i);
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(&ring[sl][t]);
@@ -98,21 +93,19 @@ __global__ __launch_bounds__(WPB * 64) void gemv_kernel(const mp::GemvParams p) 
           if constexpr (EPI == 5) {   // probe: dequant + MFMA on a constant x (no x loads)
             if (cur == sb0) {
 #pragma unroll
-              for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + 32 * i);
+              for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + 8 * i);
             }
           } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+            for (int i = 0; i < 8; ++i) xr[0][i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 8 * i);
           }
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
             half8_t b[4];
-            if constexpr (XR && PT == P_Q4_K) D::template dequant_fast<0>(ring[sl][t], b, lane);
-            else D::template dequant<0>(ring[sl][t], b, lane);
+            D::template dequant<0>(ring[sl][t], b, lane);
 #pragma unroll
             for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(xr[xs][s], b[s], acc[t]);
-            if constexpr (XR && PT == P_Q4_K) D::template dequant_fast<1>(ring[sl][t], b, lane);
-            else D::template dequant<1>(ring[sl][t], b, lane);
+            D::template dequant<1>(ring[sl][t], b, lane);
 #pragma unroll
             for (int s = 0; s < 4; ++s) acc[t] = mfma16x16x32(xr[xs][4 + s], b[s], acc[t]);
           }
@@ -186,7 +179,7 @@ __global__ __launch_bounds__(64) void unpack_kernel(const uint8_t* W, int nsb, f
     else D::template dequant<1>(raw, b, lane);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      f16* o = out + (size_t)(tile * 16 + r) * ldo + sb * 256 + 128 * h + 32 * s + 8 * g;
+      f16* o = out + (size_t)(tile * 16 + r) * ldo + sb * 256 + t16_xoff(g, 4 * h + s);
       *reinterpret_cast<half8_t*>(o) = b[s];
     }
   }
@@ -199,32 +192,18 @@ namespace mp {
 static int g_wpb = 1;   // waves per workgroup (tuning knob, MP_GEMV_WPB)
 static int g_tpw = 0;   // tiles per wave: 0 = auto (1 for M <= 4, else 2)
 
-static int g_xr = -1;   // x fragments in the register ring (MIPIPE_GEMV_XR=1), default off
-
-template <int PT, int WPB, int TPW, int NSLOT, bool XR>
-static void launch_cfg_x(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
+template <int PT, int WPB, int TPW, int NSLOT>
+static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
   dim3 grid((p.ntiles + TPW - 1) / TPW, nsplit);
   dim3 block(WPB * 64);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
-    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
-    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
-    case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT, false>), grid, block, 0, st, p); break;
-    case 4: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 4, WPB, TPW, NSLOT, false>), grid, block, 0, st, p); break;
-    case 5: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 5, WPB, TPW, NSLOT, XR>), grid, block, 0, st, p); break;
+    case EPI_STORE: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_STORE, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case EPI_ATOMIC: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_ATOMIC, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL((mpk::gemv_kernel<PT, EPI_SWIGLU, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 3, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case 4: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 4, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
+    case 5: hipLaunchKernelGGL((mpk::gemv_kernel<PT, 5, WPB, TPW, NSLOT>), grid, block, 0, st, p); break;
   }
-}
-
-template <int PT, int WPB, int TPW, int NSLOT>
-static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
-  if (g_xr < 0) {
-    const char* e = getenv("MIPIPE_GEMV_XR");
-    g_xr = e && atoi(e) ? 1 : 0;
-  }
-  if constexpr (PT == P_Q4_K) {
-    if (g_xr) return launch_cfg_x<PT, WPB, TPW, NSLOT, true>(epi, p, nsplit, st);
-  }
-  launch_cfg_x<PT, WPB, TPW, NSLOT, false>(epi, p, nsplit, st);
 }
 
 // Tiles per wave: with M > 4 the x fragments (16 rows x 32 k per MFMA) cost more L1/L2 traffic

@@ -24,14 +24,12 @@ using namespace mp;
 
 constexpr int G2_LDX = 256 + 8;   // padded f16 row in LDS (528 B): 16 rows of a fragment read hit distinct banks
 
-template <int PT, int EPI, int NW, int NSLOT, bool FAST>
+template <int PT, int EPI, int NW, int NSLOT>
 __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int NT = NW * 64;
   __shared__ __attribute__((aligned(16))) f16 xs[2][16 * G2_LDX];
-  // FAST (Q4_K): per-32 sub-block sums of the x rows for the min MFMA, ring of 8 super-blocks
-  __shared__ __attribute__((aligned(16))) f16 xsum[FAST ? 8 : 1][16][8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int tile = blockIdx.x * NW + wave;
@@ -61,7 +59,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
       }
     }
   };
-  auto store_x = [&](const int sl, const int buf, const int sbi) {
+  auto store_x = [&](const int sl, const int buf) {
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       const int c = tid + NT * j;
@@ -69,58 +67,30 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
         const int row = c >> 5, col = (c & 31) * 8;
         *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + col]) = xv[sl][j];
       }
-      if constexpr (FAST) {
-        // 4 consecutive chunks = one 32-wide sub-block of one row (c and tid share the low bits)
-        const half8_t hv = __builtin_bit_cast(half8_t, xv[sl][j]);
-        float t = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t += (float)hv[e];
-        t += __shfl_xor(t, 1);
-        t += __shfl_xor(t, 2);
-        if (c < 512 && (c & 3) == 0) xsum[(sbi - sbA) & 7][c >> 5][(c & 31) >> 2] = (f16)t;
-      }
     }
   };
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sbA + sl, last));
-  store_x(0, 0, sbA);
+  store_x(0, 0);
   __syncthreads();
-  half8_t bmin = {};   // FAST: this lane's min fragment of the current group of 4 super-blocks
 
   // rows >= M are zero in LDS (their outputs are never stored)
-  const f16* xrow0 = &xs[0][r * G2_LDX + 8 * g];
-  const f16* xrow1 = &xs[1][r * G2_LDX + 8 * g];
+  const f16* xrow0 = &xs[0][r * G2_LDX + t16_xoff(g, 0)];
+  const f16* xrow1 = &xs[1][r * G2_LDX + t16_xoff(g, 0)];
   // one super-block; all loads unconditional (clamped to the range): path-independent vmcnt
   auto step = [&](const int sl, const int cur) {
     const int buf = (cur - sbA) & 1;
     const f16* xr = buf ? xrow1 : xrow0;
     half8_t b[4];
-    if constexpr (FAST) {
-      const int gi = (cur - sbA) & 3;             // position in the group of 4 super-blocks
-      const half8_t mv = D::mins(ring[sl]);
-      if (g == gi) bmin = mv;
-      D::template dequant_fast<0>(ring[sl], b, lane);
-    } else {
-      D::template dequant<0>(ring[sl], b, lane);
-    }
+    D::template dequant<0>(ring[sl], b, lane);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 32 * s), b[s], acc);
-    if constexpr (FAST) D::template dequant_fast<1>(ring[sl], b, lane);
-    else D::template dequant<1>(ring[sl], b, lane);
+    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 8 * s), b[s], acc);
+    D::template dequant<1>(ring[sl], b, lane);
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 128 + 32 * s), b[s], acc);
-    if constexpr (FAST) {
-      const int gi = (cur - sbA) & 3;
-      if (gi == 3 || cur == sbB - 1) {   // flush the group: sum_j xsum[m][j] * (-dmin m_j)[n]
-        const half8_t a = *reinterpret_cast<const half8_t*>(&xsum[(cur - gi + g - sbA) & 7][r][0]);
-        acc = mfma16x16x32(a, bmin, acc);
-        bmin = half8_t{};
-      }
-    }
-    store_x((sl + 1) % NSLOT, buf ^ 1, min(cur + 1, last));   // x(cur + 1), loaded NSLOT - 1 steps ago
+    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 32 + 8 * s), b[s], acc);
+    store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
     issue(sl, min(cur + NSLOT, last));
     __syncthreads();
   };
@@ -162,33 +132,18 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 
 namespace mp {
 
-template <int PT, int EPI, int NW, bool FAST>
+template <int PT, int EPI, int NW>
 static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
-  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 4, FAST>), dim3((p.ntiles + NW - 1) / NW, nsplit),
-                     dim3(NW * 64), 0, st, p);
+  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 4>), dim3((p.ntiles + NW - 1) / NW, nsplit), dim3(NW * 64), 0,
+                     st, p);
 }
-
-static int g_fast = -1;   // min-MFMA dequant for Q4_K (MIPIPE_GEMV_FAST, default off: measured 20-30% slower, profiles/r1d_gemv_fast.txt)
 
 template <int PT, int NW>
 static void gemv2_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) {
-  if (g_fast < 0) {
-    const char* e = getenv("MIPIPE_GEMV_FAST");
-    g_fast = e ? (atoi(e) != 0) : 0;
-  }
-  if constexpr (PT == P_Q4_K && NW == 8) {
-    if (g_fast) {
-      switch (epi) {
-        case EPI_STORE: return gemv2_go<PT, EPI_STORE, NW, true>(p, nsplit, st);
-        case EPI_ATOMIC: return gemv2_go<PT, EPI_ATOMIC, NW, true>(p, nsplit, st);
-        case EPI_SWIGLU: return gemv2_go<PT, EPI_SWIGLU, NW, true>(p, nsplit, st);
-      }
-    }
-  }
   switch (epi) {
-    case EPI_STORE: return gemv2_go<PT, EPI_STORE, NW, false>(p, nsplit, st);
-    case EPI_ATOMIC: return gemv2_go<PT, EPI_ATOMIC, NW, false>(p, nsplit, st);
-    case EPI_SWIGLU: return gemv2_go<PT, EPI_SWIGLU, NW, false>(p, nsplit, st);
+    case EPI_STORE: return gemv2_go<PT, EPI_STORE, NW>(p, nsplit, st);
+    case EPI_ATOMIC: return gemv2_go<PT, EPI_ATOMIC, NW>(p, nsplit, st);
+    case EPI_SWIGLU: return gemv2_go<PT, EPI_SWIGLU, NW>(p, nsplit, st);
   }
 }
 

@@ -38,8 +38,18 @@ __global__ void init_packed_kernel(uint8_t* W, size_t nbytes, int pt, float scal
       const float d = scale * 3.4f / (nmax * 63.f);
       const float dmin = d * nmax * 0.5f;           // centres sc*q around m
       v[0] = (uint32_t)f2h(d) | ((uint32_t)f2h(dmin) << 16);
-      // keep scales random; make mins ~ scales so each sub-block is roughly zero-mean
-      v[2] = v[1];
+      // random 6-bit scales with mins = scales, so each sub-block is roughly zero-mean; header
+      // layout of csrc/runtime/pack.cpp: v_g = sc | m << 6 | sc' << 12 | m' << 18, byte b at 4b + g
+      const uint32_t rnd[2] = {v[1], v[2]};
+      uint32_t out[3] = {0u, 0u, 0u};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t s0 = (rnd[g >> 1] >> (16 * (g & 1))) & 63u, s1 = (rnd[g >> 1] >> (16 * (g & 1) + 6)) & 63u;
+        const uint32_t vg = s0 | s0 << 6 | s1 << 12 | s1 << 18;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) out[b] |= ((vg >> (8 * b)) & 0xFFu) << (8 * g);
+      }
+      v[1] = out[0]; v[2] = out[1]; v[3] = out[2];
     }
   } else if (pt == P_Q6_K) {
     if (in_chunk >= 3328) {   // d for 8 rows per 16 B

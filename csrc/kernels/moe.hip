@@ -65,7 +65,7 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
     const int rows = min(16, count - r0);
     const int slot_r = list[r0 + min(r, rows - 1)];
     const int xrow = p.x_per_slot ? slot_r : slot_r / p.k;
-    const f16* xp = p.X + (size_t)xrow * p.ldx + 8 * g;
+    const f16* xp = p.X + (size_t)xrow * p.ldx + t16_xoff(g, 0);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     typename D::Raw ring[NSLOT];
 #pragma unroll
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
         if (cur < sb1) {
           half8_t a[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 32 * i);
+          for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 8 * i);
           half8_t b[4];
           D::template dequant<0>(ring[sl], b, lane);
 #pragma unroll

@@ -56,10 +56,12 @@ __global__ __launch_bounds__(ST) void sample_kernel(const SampleParams p) {
     return;
   }
   const float invT = 1.f / p.temp;
+  // llama.cpp sampler-chain semantics (common_sampler defaults: top-k -> top-p -> min-p -> temp ->
+  // dist): the three cuts are taken on the T = 1 distribution, the draw uses temperature T.
   // top-k threshold on logits: largest thr with count(l >= thr) >= k
   float thr = -INFINITY;
   if (p.top_k > 0 && p.top_k < n) {
-    float lo = gmx - 60.f * p.temp - 1e-3f, hi = gmx;
+    float lo = gmx - 60.f, hi = gmx;
     for (int it = 0; it < 28; ++it) {
       const float mid = 0.5f * (lo + hi);
       float c = 0.f;
@@ -69,27 +71,27 @@ __global__ __launch_bounds__(ST) void sample_kernel(const SampleParams p) {
     }
     thr = lo;
   }
-  // min-p: keep p_i >= min_p * p_max  <=>  l_i >= gmx + T ln(min_p)
-  if (p.min_p > 0.f) thr = fmaxf(thr, gmx + p.temp * __logf(p.min_p));
-  // probabilities (unnormalised) of the survivors
-  auto prob = [&](float l) { return l >= thr ? __expf((l - gmx) * invT) : 0.f; };
-  float tot = 0.f;
-  for (int i = i0; i < i1; ++i) tot += prob(lg[i]);
-  tot = block_reduce(tot, sh, false);
-  // top-p: smallest probability threshold q with sum_{p_i >= q} p_i >= top_p * tot
+  // T = 1 probabilities (relative to the max) of the top-k survivors
+  auto p1 = [&](float l) { return l >= thr ? __expf(l - gmx) : 0.f; };
+  // top-p: largest q with sum_{p1 >= q} p1 >= top_p * sum p1
   float pthr = 0.f;
   if (p.top_p > 0.f && p.top_p < 1.f) {
-    float lo = 0.f, hi = 1.f;   // probs relative to the max (max prob = 1)
+    float tot = 0.f;
+    for (int i = i0; i < i1; ++i) tot += p1(lg[i]);
+    tot = block_reduce(tot, sh, false);
+    float lo = 0.f, hi = 1.f;
     for (int it = 0; it < 24; ++it) {
       const float mid = 0.5f * (lo + hi);
       float s = 0.f;
-      for (int i = i0; i < i1; ++i) { const float q = prob(lg[i]); s += q >= mid ? q : 0.f; }
+      for (int i = i0; i < i1; ++i) { const float q = p1(lg[i]); s += q >= mid ? q : 0.f; }
       s = block_reduce(s, sh, false);
       if (s >= p.top_p * tot) lo = mid; else hi = mid;
     }
     pthr = lo;
   }
-  auto keep = [&](float l) { const float q = prob(l); return q >= pthr ? q : 0.f; };
+  // min-p: p1 >= min_p (the max has p1 = 1)
+  pthr = fmaxf(pthr, p.min_p);
+  auto keep = [&](float l) { return l >= thr && __expf(l - gmx) >= pthr ? __expf((l - gmx) * invT) : 0.f; };
   float mine = 0.f;
   for (int i = i0; i < i1; ++i) mine += keep(lg[i]);
   // inclusive scan of per-thread sums (Hillis-Steele in LDS)
@@ -130,9 +132,44 @@ __global__ __launch_bounds__(ST) void sample_kernel(const SampleParams p) {
   }
 }
 
+__global__ __launch_bounds__(256) void penalize_kernel(const PenaltyParams p) {
+  const int row = blockIdx.x;
+  const int32_t* h = p.hist + (size_t)row * p.last_n;
+  float* lg = p.logits + (size_t)row * p.ld;
+  for (int i = threadIdx.x; i < p.last_n; i += blockDim.x) {
+    const int t = h[i];
+    if (t < 0 || t >= p.n) continue;
+    int c = 0;
+    bool first = true;
+    for (int j = 0; j < p.last_n; ++j)
+      if (h[j] == t) {
+        ++c;
+        first &= j >= i;
+      }
+    if (!first) continue;   // the first occurrence in the window owns the token
+    float l = lg[t];
+    l = l > 0.f ? l / p.repeat : l * p.repeat;
+    lg[t] = l - (float)c * p.freq - p.presence;
+  }
+}
+
+__global__ void hist_push_kernel(int32_t* hist, int32_t* cnt, int last_n, const int32_t* tokens, int M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const int c = cnt[m];
+  hist[(size_t)m * last_n + c % last_n] = tokens[m];
+  cnt[m] = c + 1;
+}
+
 }  // namespace mpk
 
 namespace mp {
+void launch_penalize(const PenaltyParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::penalize_kernel, dim3(p.M), dim3(256), 0, st, p);
+}
+void launch_hist_push(int32_t* hist, int32_t* cnt, int last_n, const int32_t* tokens, int M, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::hist_push_kernel, dim3((M + 63) / 64), dim3(64), 0, st, hist, cnt, last_n, tokens, M);
+}
 void launch_sample(const SampleParams& p, hipStream_t st) {
   hipLaunchKernelGGL(mpk::sample_kernel, dim3(p.M), dim3(mpk::ST), 0, st, p);
 }

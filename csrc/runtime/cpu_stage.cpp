@@ -1,5 +1,7 @@
 #include "cpu_stage.h"
 
+#include <unordered_map>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -361,31 +363,33 @@ void CpuStage::ffn(const Layer& L, int M, const float* xn, float* x) {
   }
 }
 
+// llama.cpp sampler-chain semantics (same as the HIP sampler, csrc/kernels/sample.hip): top-k,
+// top-p and min-p cut the T = 1 distribution, the draw uses temperature T
 int CpuStage::sample_row(const float* lg, uint64_t salt, int row) {
   const int n = cfg_.vocab;
   if (temp_ <= 0.f) return (int)(std::max_element(lg, lg + n) - lg);
   std::vector<std::pair<float, int>> v(n);
-  for (int i = 0; i < n; ++i) v[i] = {lg[i] / temp_, i};
+  for (int i = 0; i < n; ++i) v[i] = {lg[i], i};
   std::sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.first > b.first || (a.first == b.first && a.second < b.second); });
   int keep = (top_k_ > 0 && top_k_ < n) ? top_k_ : n;
   const float mx = v[0].first;
-  std::vector<double> p(keep);
-  double sum = 0;
-  for (int i = 0; i < keep; ++i) { p[i] = std::exp((double)v[i].first - mx); sum += p[i]; }
+  std::vector<double> p1(keep);
+  for (int i = 0; i < keep; ++i) p1[i] = std::exp((double)v[i].first - mx);
+  if (top_p_ > 0.f && top_p_ < 1.f) {
+    double tot = 0, c = 0;
+    for (int i = 0; i < keep; ++i) tot += p1[i];
+    int j = 0;
+    while (j < keep) { c += p1[j++]; if (c >= top_p_ * tot) break; }
+    keep = std::max(1, j);
+  }
   if (min_p_ > 0) {
     int j = 0;
-    while (j < keep && p[j] >= min_p_ * p[0]) ++j;
+    while (j < keep && p1[j] >= min_p_) ++j;
     keep = std::max(1, j);
   }
-  if (top_p_ < 1.f) {
-    double c = 0, tot = 0;
-    for (int i = 0; i < keep; ++i) tot += p[i];
-    int j = 0;
-    while (j < keep) { c += p[j++]; if (c >= top_p_ * tot) break; }
-    keep = std::max(1, j);
-  }
-  sum = 0;
-  for (int i = 0; i < keep; ++i) sum += p[i];
+  std::vector<double> p(keep);
+  double sum = 0;
+  for (int i = 0; i < keep; ++i) { p[i] = std::exp(((double)v[i].first - mx) / temp_); sum += p[i]; }
   const uint64_t r = mix64((seed_ ^ (salt * 0x9E3779B97F4A7C15ULL)) ^ mix64((step_ << 20) ^ (uint64_t)row));
   const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0) * sum;
   double c = 0;
@@ -396,10 +400,44 @@ int CpuStage::sample_row(const float* lg, uint64_t salt, int row) {
   return v[keep - 1].second;
 }
 
-void CpuStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt) {
+void CpuStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) {
+  const int B = opt_.mb_size;
+  if (hist_.empty()) hist_.resize((size_t)opt_.n_mb * B);
+  for (int b = 0; b < B; ++b) {
+    auto& h = hist_[(size_t)mb * B + b];
+    h.clear();
+    if (b < (int)seqs.size()) {
+      const auto& q = seqs[b];
+      const size_t take = std::min<size_t>(q.size(), (size_t)std::max(0, pen_last_n_));
+      h.assign(q.end() - take, q.end());
+    }
+  }
+}
+
+void CpuStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt) {
   rmsnorm(x, out_norm_, xn_.data(), M);
   matmul(out_, xn_.data(), cfg_.d_model, M, logits_.data(), cfg_.vocab, false);
-  for (int m = 0; m < M; ++m) tok_out[m] = sample_row(logits_.data() + (size_t)m * cfg_.vocab, salt, m);
+  const bool pen = penalties_on();
+  if (pen && hist_.empty()) hist_.resize((size_t)opt_.n_mb * opt_.mb_size);
+  for (int m = 0; m < M; ++m) {
+    float* lg = logits_.data() + (size_t)m * cfg_.vocab;
+    std::vector<int32_t>* h = pen ? &hist_[(size_t)mb * opt_.mb_size + m] : nullptr;
+    if (pen) {
+      std::unordered_map<int32_t, int> cnt;
+      for (int32_t t : *h) ++cnt[t];
+      for (const auto& [t, c] : cnt) {
+        if (t < 0 || t >= cfg_.vocab) continue;
+        float l = lg[t];
+        l = l > 0.f ? l / pen_repeat_ : l * pen_repeat_;
+        lg[t] = l - (float)c * pen_freq_ - pen_presence_;
+      }
+    }
+    tok_out[m] = sample_row(lg, salt, m);
+    if (pen) {
+      h->push_back(tok_out[m]);
+      if ((int)h->size() > pen_last_n_) h->erase(h->begin());
+    }
+  }
 }
 
 void CpuStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t) {
@@ -435,7 +473,7 @@ void CpuStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t)
 }
 
 void CpuStage::prefill_finish(int mb, hipStream_t) {
-  if (spec_.last()) head(opt_.mb_size, last_h_[mb].data(), tok_[mb].data(), 1000003ULL + (uint64_t)mb);
+  if (spec_.last()) head(mb, opt_.mb_size, last_h_[mb].data(), tok_[mb].data(), 1000003ULL + (uint64_t)mb);
 }
 
 void CpuStage::decode(int mb, hipStream_t) {
@@ -449,7 +487,7 @@ void CpuStage::decode(int mb, hipStream_t) {
   std::vector<int32_t> slot(B);
   for (int b = 0; b < B; ++b) slot[b] = mb * B + b;
   for (size_t li = 0; li < layers_.size(); ++li) layer_forward((int)li, B, x, pos_[mb].data(), slot.data());
-  if (spec_.last()) head(B, x, tok_[mb].data(), (uint64_t)mb + 1);
+  if (spec_.last()) head(mb, B, x, tok_[mb].data(), (uint64_t)mb + 1);
   for (int b = 0; b < B; ++b) pos_[mb][b] = std::min(pos_[mb][b] + 1, opt_.max_ctx - 1);
   if (mb == 0) ++step_;
 }

@@ -61,7 +61,8 @@ class CpuStage : public Stage {
   void rmsnorm(const float* x, const std::vector<float>& w, float* y, int M);
   void layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* slot);
   void ffn(const Layer& L, int M, const float* xn, float* x);
-  void head(int M, const float* x, int32_t* tok_out, uint64_t salt);
+  void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt);
+  void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) override;
   int sample_row(const float* logits, uint64_t salt, int row);
   CpuMat own_random(int type, int64_t N, int64_t K, uint64_t seed);
 
@@ -86,6 +87,7 @@ class CpuStage : public Stage {
   // scratch
   std::vector<float> xn_, qkv_, att_, h_, gu_;
   uint64_t step_ = 0;
+  std::vector<std::vector<int32_t>> hist_;   // per slot: accepted tokens, most recent last
 };
 
 }  // namespace mp

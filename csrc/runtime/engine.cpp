@@ -160,6 +160,8 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     w->stage->alloc_runtime();
     w->stage->set_sampling((float)j.get_num("temp", 0.0), j.get_int("top_k", 0), (float)j.get_num("top_p", 1.0),
                            (float)j.get_num("min_p", 0.0), seed);
+    w->stage->set_penalties(j.get_int("repeat_last_n", 64), (float)j.get_num("repeat_penalty", 1.0),
+                            (float)j.get_num("frequency_penalty", 0.0), (float)j.get_num("presence_penalty", 0.0));
     if (cpu_) {
       w->ring_pending.assign(M_, false);
       workers_.push_back(std::move(w));
@@ -655,6 +657,13 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
         if (i < prompts.size()) pos[b] = (int)prompts[i].size();
       }
       st.set_positions(mb, pos);
+    }
+    if (st.spec().last()) {   // repetition-penalty windows start with the prompts (llama-cli accepts them)
+      for (int mb = 0; mb < M_; ++mb) {
+        std::vector<std::vector<int32_t>> seqs;
+        for (int b = 0; b < B_ && (size_t)mb * B_ + b < prompts.size(); ++b) seqs.push_back(prompts[(size_t)mb * B_ + b]);
+        st.set_history(mb, seqs);
+      }
     }
     if (st.spec().first()) {
       for (size_t i = 0; i < prompts.size(); ++i) {

@@ -423,6 +423,40 @@ void HipStage::set_sampling(float temp, int top_k, float top_p, float min_p, uin
   if (changed && !graphs_.empty() && spec_.last()) capture_graphs();
 }
 
+void HipStage::set_penalties(int last_n, float repeat, float freq, float presence) {
+  const bool changed = last_n != pen_last_n_ || repeat != pen_repeat_ || freq != pen_freq_ || presence != pen_presence_;
+  Stage::set_penalties(last_n, repeat, freq, presence);
+  if (!spec_.last()) return;
+  ensure_hist();
+  if (changed && !graphs_.empty()) capture_graphs();
+}
+
+void HipStage::ensure_hist() {
+  if (!penalties_on() || (hist_ && hist_n_ == pen_last_n_)) return;
+  const size_t rows = (size_t)opt_.n_mb * opt_.mb_size;
+  hist_ = (int32_t*)dmalloc(rows * pen_last_n_ * 4);
+  HIP_OK(hipMemset(hist_, 0xFF, rows * pen_last_n_ * 4));   // -1: empty
+  if (!hist_cnt_) hist_cnt_ = (int32_t*)dmalloc(rows * 4);
+  HIP_OK(hipMemset(hist_cnt_, 0, rows * 4));
+  hist_n_ = pen_last_n_;
+}
+
+void HipStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) {
+  if (!spec_.last() || !penalties_on()) return;
+  ensure_hist();
+  const int B = opt_.mb_size, n = hist_n_;
+  std::vector<int32_t> h((size_t)B * n, -1), cnt(B, 0);
+  for (int b = 0; b < B && b < (int)seqs.size(); ++b) {
+    const auto& q = seqs[b];
+    const int take = std::min<int>(n, (int)q.size());
+    for (int i = 0; i < take; ++i) h[(size_t)b * n + i] = q[q.size() - take + i];
+    cnt[b] = take;
+  }
+  HIP_OK(hipSetDevice(spec_.device));
+  HIP_OK(hipMemcpy(hist_ + (size_t)mb * B * n, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(hist_cnt_ + (size_t)mb * B, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
+}
+
 void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
                     int n_valid, bool allow_split, hipStream_t st) {
   if (M > 16 && opt_.prefill_gemm) {   // prompt chunks: MFMA GEMM, weights read once per 64 rows
@@ -544,10 +578,18 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
 }
 
-void HipStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st) {
+void HipStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st) {
   const int d = cfg_.d_model;
   launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
   gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
+  const bool pen = penalties_on() && hist_;
+  int32_t* hist = pen ? hist_ + (size_t)mb * opt_.mb_size * hist_n_ : nullptr;
+  if (pen) {
+    PenaltyParams pp{};
+    pp.logits = logits_; pp.ld = logits_ld_; pp.n = cfg_.vocab; pp.M = M;
+    pp.hist = hist; pp.last_n = hist_n_; pp.repeat = pen_repeat_; pp.freq = pen_freq_; pp.presence = pen_presence_;
+    launch_penalize(pp, st);
+  }
   if (temp_ > 0.f) {
     SampleParams sp{};
     sp.logits = logits_; sp.ld = logits_ld_; sp.n = cfg_.vocab; sp.M = M;
@@ -557,6 +599,7 @@ void HipStage::head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipS
   } else {
     launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st);
   }
+  if (pen) launch_hist_push(hist, hist_cnt_ + (size_t)mb * opt_.mb_size, hist_n_, tok_out, M, st);
 }
 
 void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) {
@@ -589,7 +632,7 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
 }
 
 void HipStage::prefill_finish(int mb, hipStream_t st) {
-  if (spec_.last()) head(opt_.mb_size, last_h_[mb], tok_[mb], 1000003ULL + (uint64_t)mb, st);
+  if (spec_.last()) head(mb, opt_.mb_size, last_h_[mb], tok_[mb], 1000003ULL + (uint64_t)mb, st);
 }
 
 void HipStage::decode_eager(int mb, hipStream_t st) {
@@ -599,7 +642,7 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
     launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tok_[mb], B, x, cfg_.d_model, st);
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
-  if (spec_.last()) head(B, x, tok_[mb], (uint64_t)mb + 1, st);
+  if (spec_.last()) head(mb, B, x, tok_[mb], (uint64_t)mb + 1, st);
   launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
 }
 

@@ -100,6 +100,8 @@ class HipStage : public Stage {
   void destroy_graphs();
   // sampling parameters are baked into the decode graphs: re-capture when they change
   void set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) override;
+  void set_penalties(int last_n, float repeat, float freq, float presence) override;
+  void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) override;
 
   size_t weight_bytes() const override { return weight_bytes_; }
   size_t kv_bytes() const override { return kv_bytes_; }
@@ -115,7 +117,8 @@ class HipStage : public Stage {
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
             int n_valid, bool allow_split, hipStream_t st);
-  void head(int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
+  void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
+  void ensure_hist();
   PackedMat upload_packed(int ggml_type, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row);
   // E matrices of N x K packed back to back (MoE experts); row(e, n)
   PackedMat upload_packed_experts(int ggml_type, int E, int64_t N, int64_t K, size_t* stride,
@@ -159,6 +162,11 @@ class HipStage : public Stage {
   std::vector<float*> act_;
   std::vector<int32_t*> tok_, pos_, kvlen_, slot_;
   int32_t* step_ = nullptr;
+  // repetition-penalty windows (last stage): [n_mb][mb_size][hist_n_] token ring, -1 = empty,
+  // and the per-row count of accepted tokens (ring position)
+  int32_t* hist_ = nullptr;
+  int32_t* hist_cnt_ = nullptr;
+  int hist_n_ = 0;
   // prefill metadata
   int32_t* pf_pos_ = nullptr; int32_t* pf_kvlen_ = nullptr; int32_t* pf_slot_ = nullptr;
   int32_t* prompt_dev_ = nullptr;

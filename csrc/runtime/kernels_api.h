@@ -118,6 +118,17 @@ struct SampleParams {
   int32_t* tokens;
 };
 void launch_sample(const SampleParams& p, hipStream_t st);
+// repetition penalties (llama.cpp penalties sampler semantics) over each row's ring of the last
+// `last_n` accepted tokens (-1 = empty): every distinct token t of the window with count c gets
+// l = l > 0 ? l / repeat : l * repeat, then l -= c * freq + presence.  In place, before sampling.
+struct PenaltyParams {
+  float* logits; int ld; int n; int M;
+  const int32_t* hist; int last_n;     // [M][last_n]
+  float repeat, freq, presence;
+};
+void launch_penalize(const PenaltyParams& p, hipStream_t st);
+// append tokens[m] to row m's ring: hist[m][cnt[m] % last_n] = tokens[m]; ++cnt[m]
+void launch_hist_push(int32_t* hist, int32_t* cnt, int last_n, const int32_t* tokens, int M, hipStream_t st);
 
 // pos[i] += 1, kvlen[i] = pos[i] + 1 for i < M (graph-resident decode step advance)
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st);

@@ -55,16 +55,31 @@ static inline int q6k_val(const uint8_t* b, int w) {
   return lo | (hi << 4);
 }
 
-// position of weight w inside the chunk for nibble-style layouts
+// Position of weight w (0..255 of a super-block) of tile row r: MFMA i = 4h + s of lane 16g + r,
+// element j, with w = 64g + 32h + 8s + j (the T16 k-mapping, csrc/kernels/dequant.h): lane group
+// g owns the quarter [64g, 64g + 64) of the super-block.
 struct Pos { int h, s, lane, j; };
 static inline Pos pos_of(int w, int r) {
   Pos p;
-  p.h = w / 128;
-  p.s = (w % 128) / 32;
-  const int g = (w % 32) / 8;
+  const int g = w / 64;
+  p.h = (w % 64) / 32;
+  p.s = (w % 32) / 8;
   p.j = w % 8;
   p.lane = 16 * g + r;
   return p;
+}
+
+// Q4_K / Q5_K header: (d, dmin) as in GGUF, then the 6-bit scales/mins regrouped per lane group g
+// as v_g = sc(2g) | m(2g) << 6 | sc(2g+1) << 12 | m(2g+1) << 18, byte b of v_g at byte 4 + 4b + g
+static void pack_kquarter_header(const uint8_t* src, uint8_t* dst) {
+  std::memcpy(dst, src, 4);
+  for (int g = 0; g < 4; ++g) {
+    int s0, m0, s1, m1;
+    get_scale_min_k4(2 * g, src + 4, s0, m0);
+    get_scale_min_k4(2 * g + 1, src + 4, s1, m1);
+    const uint32_t v = (uint32_t)s0 | (uint32_t)m0 << 6 | (uint32_t)s1 << 12 | (uint32_t)m1 << 18;
+    for (int b = 0; b < 3; ++b) dst[4 + 4 * b + g] = (uint8_t)(v >> (8 * b));
+  }
 }
 static inline void put_nib(uint8_t* chunk, const Pos& p, int v) {
   uint8_t* dw = chunk + p.h * 1024 + p.lane * 16 + p.s * 4;
@@ -78,7 +93,7 @@ static void pack_chunk(int t, int pt, const uint8_t* src, int64_t K, int64_t k0,
   switch (pt) {
     case P_Q4_K: {
       for (int w = 0; w < 256; ++w) put_nib(chunk, pos_of(w, r), q4k_nib(src, w));
-      std::memcpy(chunk + 2048 + 16 * r, src, 16);
+      pack_kquarter_header(src, chunk + 2048 + 16 * r);
       break;
     }
     case P_Q5_K: {
@@ -90,8 +105,7 @@ static void pack_chunk(int t, int pt, const uint8_t* src, int64_t K, int64_t k0,
         const int bit = 8 * p.s + (p.j & 1) * 4 + (p.j >> 1);
         qh[bit / 8] |= (uint8_t)(((v >> 4) & 1) << (bit % 8));
       }
-      std::memcpy(chunk + 2560 + 16 * r, src, 4);
-      std::memcpy(chunk + 2560 + 16 * r + 4, src + 4, 12);
+      pack_kquarter_header(src, chunk + 2560 + 16 * r);
       break;
     }
     case P_Q6_K: {

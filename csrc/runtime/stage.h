@@ -67,11 +67,24 @@ class Stage {
   virtual void set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) {
     temp_ = temp; top_k_ = top_k; top_p_ = top_p; min_p_ = min_p; seed_ = seed;
   }
+  // repetition penalties (llama.cpp penalties sampler, applied before the cuts): every distinct
+  // token among the last `last_n` accepted tokens of a sequence (prompt included) with count c
+  // gets l = l > 0 ? l / repeat : l * repeat, then l -= c * freq + presence
+  virtual void set_penalties(int last_n, float repeat, float freq, float presence) {
+    pen_last_n_ = last_n < 0 ? 0 : last_n; pen_repeat_ = repeat; pen_freq_ = freq; pen_presence_ = presence;
+  }
+  bool penalties_on() const {
+    return pen_last_n_ > 0 && (pen_repeat_ != 1.f || pen_freq_ != 0.f || pen_presence_ != 0.f);
+  }
+  // last stage: seed the penalty window of micro-batch mb (row b <- seqs[b], its last tokens)
+  virtual void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) { (void)mb; (void)seqs; }
 
  protected:
   float temp_ = 0.f, top_p_ = 1.f, min_p_ = 0.f;
   int top_k_ = 0;
   uint64_t seed_ = 0;
+  int pen_last_n_ = 64;
+  float pen_repeat_ = 1.f, pen_freq_ = 0.f, pen_presence_ = 0.f;
 };
 
 }  // namespace mp
