@@ -261,6 +261,26 @@ int mp_op_sample(const void* logits, int ld, int n, int M, float temp, int top_k
   API_CATCH(-1)
 }
 
+int mp_op_penalize(void* logits, int ld, int n, int M, const void* hist, int last_n, float repeat, float freq,
+                   float presence, void* stream) {
+  API_TRY
+  PenaltyParams p{};
+  p.logits = (float*)logits; p.ld = ld; p.n = n; p.M = M; p.hist = (const int32_t*)hist; p.last_n = last_n;
+  p.repeat = repeat; p.freq = freq; p.presence = presence;
+  launch_penalize(p, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_hist_push(void* hist, void* cnt, int last_n, const void* tokens, int M, void* stream) {
+  API_TRY
+  launch_hist_push((int32_t*)hist, (int32_t*)cnt, last_n, (const int32_t*)tokens, M, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 // ------------------------------------------------------------------ tokenizer
 void* mp_tok_open(const char* gguf_path) {
   API_TRY

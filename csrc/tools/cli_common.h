@@ -76,6 +76,8 @@ inline void print_common_usage(FILE* f) {
           "  -n, --n-predict N         tokens to generate (default 200)\n"
           "  -c, --ctx-size N          context per sequence (default 2048)\n"
           "  --temp T --top-k K --top-p P --min-p P --seed S   sampling (default greedy, temp 0)\n"
+          "  --repeat-penalty R --repeat-last-n N --frequency-penalty F --presence-penalty P\n"
+          "                            penalties over the last N tokens (default 1.0 / 64 / 0 / 0)\n"
           "  --sampling greedy         force greedy\n"
           "placement / pipeline:\n"
           "  -ngl, --n-gpu-layers N    0 = CPU backend, otherwise all layers on GPUs (default 99)\n"
@@ -119,6 +121,10 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--top-k") e["top_k"] = std::atoi(val().c_str());
     else if (a == "--top-p") e["top_p"] = std::atof(val().c_str());
     else if (a == "--min-p") e["min_p"] = std::atof(val().c_str());
+    else if (a == "--repeat-penalty") e["repeat_penalty"] = std::atof(val().c_str());
+    else if (a == "--repeat-last-n") e["repeat_last_n"] = std::atoi(val().c_str());
+    else if (a == "--frequency-penalty") e["frequency_penalty"] = std::atof(val().c_str());
+    else if (a == "--presence-penalty") e["presence_penalty"] = std::atof(val().c_str());
     else if (a == "--seed" || a == "-s") e["seed"] = std::atof(val().c_str());
     else if (a == "--sampling") { if (val() == "greedy") e["temp"] = 0.0; }
     else if (a == "--stages" || a == "--pp") stages = std::atoi(val().c_str());

@@ -52,6 +52,8 @@ _SIGS = {
     "mp_op_attention": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "mp_op_argmax": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+    "mp_op_penalize": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float, c_void_p], c_int),
+    "mp_op_hist_push": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_sample": ([c_void_p, c_int, c_int, c_int, c_float, c_int, c_float, c_float, ctypes.c_uint64, c_void_p,
                       c_void_p, c_void_p], c_int),
     "mp_tok_open": ([c_char_p], c_void_p),

@@ -6,7 +6,8 @@
 Config keys mirror the C++ Engine (see engine.h): gguf | synthetic+ftype, mode ("local" or "mp"),
 stages, devices, link ("local" | "rccl" | "tcp"), backend ("hip" | "cpu"), n_mb, mb_size, max_ctx,
 prefill_chunk, split ("even" | "mem" | "cost"), graphs, fused_attn, prefill_gemm, attn_split_len,
-temp/top_k/top_p/min_p/seed (sampling), world/rank/hosts/next_host/base_port/rccl_ids (mp mode),
+temp/top_k/top_p/min_p/seed (sampling; llama.cpp chain order), repeat_penalty/repeat_last_n/
+frequency_penalty/presence_penalty (penalties over the last n tokens, prompt included), world/rank/hosts/next_host/base_port/rccl_ids (mp mode),
 threads (CPU backend), trace, watchdog_s, link_timeout_s, fault (fault injection), verbose, log_file.
 """
 from __future__ import annotations

@@ -131,6 +131,22 @@ def sample(logits: torch.Tensor, temp: float, top_k: int = 0, top_p: float = 1.0
     return out
 
 
+def penalize(logits: torch.Tensor, hist: torch.Tensor, repeat: float = 1.0, freq: float = 0.0,
+             presence: float = 0.0) -> torch.Tensor:
+    """In-place repetition penalties: logits f32 [M][n], hist int32 [M][last_n] (-1 = empty)."""
+    M, n = logits.shape
+    assert hist.dtype == torch.int32 and hist.shape[0] == M and hist.is_contiguous()
+    N.check(N.lib().mp_op_penalize(_ptr(logits), logits.stride(0), n, M, _ptr(hist), hist.shape[1], repeat, freq,
+                                   presence, _stream()), "penalize")
+    return logits
+
+
+def hist_push(hist: torch.Tensor, cnt: torch.Tensor, tokens: torch.Tensor) -> None:
+    """hist[m][cnt[m] % last_n] = tokens[m]; cnt[m] += 1 (int32 device tensors)."""
+    M, last_n = hist.shape
+    N.check(N.lib().mp_op_hist_push(_ptr(hist), _ptr(cnt), last_n, _ptr(tokens), M, _stream()), "hist_push")
+
+
 def rope_cs_table(max_pos: int, hd: int, base: float, freq_factors=None) -> torch.Tensor:
     inv = base ** (-np.arange(0, hd, 2, dtype=np.float64) / hd)
     if freq_factors is not None:

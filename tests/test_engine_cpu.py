@@ -181,3 +181,39 @@ def test_fault_delay_and_trace(native, model_dir, tmp_path):
     assert {e["pid"] for e in spans} == {0, 1}
     dec0 = [e for e in spans if e["pid"] == 0 and e["name"].startswith("decode")]
     assert dec0 and all(e["dur"] >= 0 for e in dec0)
+
+
+def _penalize(lg, window, rep, fq, pr):
+    lg = lg.copy()
+    for t in set(window):
+        c = window.count(t)
+        l = lg[t]
+        lg[t] = (l / rep if l > 0 else l * rep) - c * fq - pr
+    return lg
+
+
+def test_cpu_repetition_penalties_match_reference(native, model_dir):
+    """Greedy decoding with llama.cpp-style penalties over the last n accepted tokens (prompt
+    included) against the torch oracle with the penalties applied in Python."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    ref = RefLlama.from_gguf(path)
+    prompt = [5, 9, 5, 17, 30, 9]
+    rep, fq, pr, last_n = 1.8, 0.3, 0.4, 8
+    with Engine(gguf=path, backend="cpu", max_ctx=64, repeat_penalty=rep, frequency_penalty=fq,
+                presence_penalty=pr, repeat_last_n=last_n) as eng:
+        out, _ = eng.generate([prompt], 10)
+    ref.reset()
+    seq = list(prompt)
+    lg = ref.forward(prompt, 0)[-1].numpy()
+    want = []
+    for step in range(10):
+        tok = int(_penalize(lg, seq[-last_n:], rep, fq, pr).argmax())
+        want.append(tok)
+        lg = ref.forward([tok], len(seq))[-1].numpy()
+        seq.append(tok)
+    assert out[0] == want
+    with Engine(gguf=path, backend="cpu", max_ctx=64) as eng:
+        plain, _ = eng.generate([prompt], 10)
+    assert plain[0] != want   # the penalties changed the greedy path

@@ -202,3 +202,37 @@ def test_prefill_gemm_matches_gemv_path(cuda, native, model_dir):
             res.append((out, eng.logits()))
     assert res[0][0] == res[1][0]
     assert nmse(res[1][1], res[0][1]) < 1e-5
+
+
+def test_repetition_penalties_match_reference(cuda, native, model_dir):
+    """On-GPU penalties (graph-captured penalize + history ring) against the oracle logits with
+    the penalties applied in Python; the returned logits are the penalized ones."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    ref = RefLlama.from_gguf(path)
+    prompt = [5, 9, 5, 17, 30, 9]
+    rep, fq, pr, last_n = 1.8, 0.3, 0.4, 8
+
+    def penalize(lg, window):
+        lg = lg.copy()
+        for t in set(window):
+            c = window.count(t)
+            lg[t] = (lg[t] / rep if lg[t] > 0 else lg[t] * rep) - c * fq - pr
+        return lg
+
+    with Engine(gguf=path, max_ctx=64, graphs=True, repeat_penalty=rep, frequency_penalty=fq,
+                presence_penalty=pr, repeat_last_n=last_n) as eng:
+        eng.start([prompt])
+        ref.reset()
+        seq = list(prompt)
+        rl = penalize(ref.forward(prompt, 0)[-1].numpy(), seq[-last_n:])
+        for step in range(8):
+            lg = eng.logits()[0]
+            assert nmse(lg, rl) < 2e-4, (step, nmse(lg, rl))
+            tok = eng.tokens()[0][-1]
+            if rl.argmax() != tok:   # allowed only on a near-tie
+                assert rl.max() - rl[tok] < 1e-2 * (abs(rl).max() + 1), (step, tok, rl.argmax())
+            seq.append(tok)
+            eng.decode(1)
+            rl = penalize(ref.forward([tok], len(seq) - 1)[-1].numpy(), seq[-last_n:])

@@ -151,6 +151,52 @@ def test_sample_distribution(cuda, native):
     assert int(sample(logits.cuda(), temp=0.0).item()) == 3
 
 
+def test_sample_cut_order(cuda, native):
+    """llama.cpp chain semantics: min-p / top-p cut the T = 1 distribution, the draw uses T."""
+    from mipipe.ops.kernels import sample
+    V = 1000
+    logits = torch.full((1, V), -20.0)
+    logits[0, [3, 10, 500]] = torch.tensor([2.0, 1.0, 0.0])
+    cnt = {}
+    for s in range(600):
+        # T = 1 relative probs (1, .37, .14): min-p 0.3 drops token 500 even though at T = 2 it is .37
+        t = int(sample(logits.cuda(), temp=2.0, min_p=0.3, seed=s).item())
+        cnt[t] = cnt.get(t, 0) + 1
+    assert set(cnt) <= {3, 10}
+    p3 = 1.0 / (1.0 + math.exp(-0.5))            # softmax([2, 1] / 2)[0]
+    assert abs(cnt.get(3, 0) / 600 - p3) < 0.08
+    # top-p 0.6 at T = 1: the max alone holds .665 -> always token 3, whatever T
+    assert {int(sample(logits.cuda(), temp=3.0, top_p=0.6, seed=s).item()) for s in range(40)} == {3}
+
+
+def test_penalize_and_history(cuda, native):
+    from mipipe.ops.kernels import penalize, hist_push
+    M, V, L = 3, 300, 8
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(M, V, generator=g) * 3
+    hist = torch.full((M, L), -1, dtype=torch.int32)
+    hist[0, :5] = torch.tensor([7, 7, 250, 3, 7], dtype=torch.int32)
+    hist[1, :] = torch.tensor([1, 2, 3, 4, 1, 2, 1, 299], dtype=torch.int32)
+    rep, fq, pr = 1.3, 0.25, 0.5
+    ref = logits.clone()
+    for m in range(M):
+        toks = [int(t) for t in hist[m] if t >= 0]
+        for t in set(toks):
+            c = toks.count(t)
+            l = float(ref[m, t])
+            l = l / rep if l > 0 else l * rep
+            ref[m, t] = l - c * fq - pr
+    got = penalize(logits.cuda(), hist.cuda(), rep, fq, pr).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-6)
+    # ring append
+    h = hist.cuda()
+    cnt = torch.tensor([5, 8, 0], dtype=torch.int32, device="cuda")
+    hist_push(h, cnt, torch.tensor([11, 12, 13], dtype=torch.int32, device="cuda"))
+    h = h.cpu()
+    assert int(h[0, 5]) == 11 and int(h[1, 0]) == 12 and int(h[2, 0]) == 13
+    assert cnt.cpu().tolist() == [6, 9, 1]
+
+
 def _ref_attention(q, k, v, kvlen):
     # q [M, Hq, hd], k/v [S, Hkv, hd]; row m attends keys [0, kvlen[m])
     M, Hq, hd = q.shape
