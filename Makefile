@@ -38,7 +38,16 @@ $(BINDIR)/%: csrc/tools/%.cpp $(LIBDIR)/libmipipe.so $(HDRS) $(wildcard csrc/too
 	$(HIPCC) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -Icsrc/tools $< $(wildcard csrc/tools/*_impl.cpp) -o $@ \
 	  -L$(LIBDIR) -lmipipe -Wl,-rpath,'$$ORIGIN/../lib' $(LDFLAGS)
 
+# Host-only ASan/UBSan build of the untrusted-input parsers (GGUF, tokenizer, JSON) for
+# tests/test_sanitize.py; no GPU code involved
+SAN_SRC := csrc/tools/fuzz_host.cpp csrc/runtime/gguf.cpp csrc/runtime/json.cpp csrc/runtime/model.cpp \
+           csrc/runtime/tokenizer.cpp csrc/runtime/log.cpp
+$(BUILD)/fuzz_host_asan: $(SAN_SRC) $(HDRS) | $(BUILD)
+	g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all \
+	  -Icsrc/runtime $(SAN_SRC) -o $@
+sanitize: $(BUILD)/fuzz_host_asan
+
 clean:
 	rm -rf $(BUILD) $(LIBDIR)/libmipipe.so $(TOOLS)
 
-.PHONY: all tools clean
+.PHONY: all tools clean sanitize

@@ -134,7 +134,10 @@ namespace mp {
 
 template <int PT, int EPI, int NW>
 static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
-  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 4>), dim3((p.ntiles + NW - 1) / NW, nsplit), dim3(NW * 64), 0,
+  // super-blocks in flight per wave: 4, fewer for the fat chunks so the kernel stays within
+  // 128 VGPRs (4 waves per SIMD = two 8-wave workgroups per CU)
+  constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS>), dim3((p.ntiles + NW - 1) / NW, nsplit), dim3(NW * 64), 0,
                      st, p);
 }
 
