@@ -3,6 +3,7 @@ model-config extraction, tokenizer construction and the JSON request parser, bui
 AddressSanitizer + UndefinedBehaviorSanitizer (`make sanitize`, csrc/tools/fuzz_host.cpp) and fed
 hypothesis-generated corruptions of valid GGUF files and random request bodies.  A clean
 rejection (exception) is fine; any sanitizer report fails the test."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -20,7 +21,11 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPT
 def fuzz_bin():
     if shutil.which("g++") is None:
         pytest.skip("no host compiler")
-    r = subprocess.run(["make", "-s", "sanitize"], cwd=REPO, capture_output=True, text=True)
+    # xdist workers share the binary: serialise the build so none execs a half-linked file
+    os.makedirs(os.path.join(REPO, "build"), exist_ok=True)
+    with open(os.path.join(REPO, "build", ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "sanitize"], cwd=REPO, capture_output=True, text=True)
     if r.returncode != 0:
         pytest.skip("sanitizer build failed: " + r.stderr[-300:])
     return BIN
