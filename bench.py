@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="llama3-70b", choices=sorted(MODELS))
     ap.add_argument("--ftype", default="Q4_K")
-    ap.add_argument("--mb-size", type=int, default=16, help="sequences per micro-batch (<= 16)")
+    ap.add_argument("--mb-size", type=int, default=16, help="sequences per micro-batch (<= 64; > 16 runs the decode projections on the MFMA GEMM)")
     ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = #GPUs)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")

@@ -257,7 +257,7 @@ void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   if (nsplit < 1) nsplit = 1;
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
-  if (gemv_version() == 2 && epi < 3 && p.M <= 16) return launch_gemv2(ptype, epi, p, nsplit, g_nw, st);
+  if (gemv_version() == 2 && epi < 3 && p.M <= 64) return launch_gemv2(ptype, epi, p, nsplit, g_nw, st);
   switch (ptype) {
     case P_Q4_K: launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
     case P_Q5_K: launch_pt<P_Q5_K>(epi, p, nsplit, st); break;

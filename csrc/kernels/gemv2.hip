@@ -24,12 +24,15 @@ using namespace mp;
 
 constexpr int G2_LDX = 256 + 8;   // padded f16 row in LDS (528 B): 16 rows of a fragment read hit distinct banks
 
-template <int PT, int EPI, int NW, int NSLOT>
+// MT row groups of 16 activation rows (M <= 16 MT) share every dequantized weight fragment: the
+// dequant VALU work, which bounds the kernel near HBM speed at M = 16, is paid once for 16 MT rows.
+template <int PT, int EPI, int NW, int NSLOT, int MT>
 __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int NT = NW * 64;
-  __shared__ __attribute__((aligned(16))) f16 xs[2][16 * G2_LDX];
+  constexpr int XC = 512 * MT;   // 16 B x chunks per super-block
+  __shared__ __attribute__((aligned(16))) f16 xs[2][16 * MT * G2_LDX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int tile = blockIdx.x * NW + wave;
@@ -39,11 +42,11 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   const uint8_t* wt = p.W + (size_t)min(tile, p.ntiles - 1) * p.nsb * CB;
   const int M = p.M;
 
-  // x staging: 16 rows x 256 k per super-block = 512 chunks of 16 B; thread t owns chunks t, t+NT..
+  // x staging: 16 MT rows x 256 k per super-block = 512 MT chunks of 16 B; thread t owns chunks t, t+NT..
   // The x chunks of super-block j are loaded TOGETHER with its weights (register rings of NSLOT),
   // NSLOT steps ahead, and copied to LDS one step before use: every vmcnt wait then leaves the
   // loads of the NSLOT-1 later super-blocks in flight.
-  constexpr int XCH = (512 + NT - 1) / NT;
+  constexpr int XCH = (XC + NT - 1) / NT;
   u32x4 xv[NSLOT][XCH];
   typename D::Raw ring[NSLOT];
   const int last = sbB - 1;
@@ -52,7 +55,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       const int c = tid + NT * j;
-      if (c < 512) {
+      if (c < XC) {
         const int row = c >> 5, col = (c & 31) * 8;
         xv[sl][j] = row < M ? *reinterpret_cast<const u32x4*>(p.X + (size_t)row * p.ldx + (size_t)sb * 256 + col)
                             : u32x4{0u, 0u, 0u, 0u};
@@ -63,14 +66,16 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       const int c = tid + NT * j;
-      if (c < 512) {
+      if (c < XC) {
         const int row = c >> 5, col = (c & 31) * 8;
         *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + col]) = xv[sl][j];
       }
     }
   };
 
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sbA + sl, last));
   store_x(0, 0);
@@ -86,10 +91,16 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     half8_t b[4];
     D::template dequant<0>(ring[sl], b, lane);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 8 * s), b[s], acc);
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 8 * s), b[s], acc[mt]);
     D::template dequant<1>(ring[sl], b, lane);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + 32 + 8 * s), b[s], acc);
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 32 + 8 * s), b[s], acc[mt]);
     store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
     issue(sl, min(cur + NSLOT, last));
     __syncthreads();
@@ -103,25 +114,28 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   for (int sl = 0; sl < NSLOT - 1; ++sl)   // tail (< NSLOT super-blocks; uniform over the workgroup)
     if (sb + sl < sbB) step(sl, sb + sl);
   if (tile >= p.ntiles) return;
-  // lane holds C[m = 4g + i][n = 16*tile + r]
-  if constexpr (EPI == EPI_SWIGLU) {
+  // lane holds C[m = 16 mt + 4g + i][n = 16*tile + r]
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float other = __shfl_xor(acc[i], 8);
-      const int m = 4 * g + i;
-      const int o = tile * 8 + r;
-      if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[i]) * other);
-    }
-  } else {
-    const int n = tile * 16 + r;
-    if (n < p.n_valid) {
+  for (int mt = 0; mt < MT; ++mt) {
+    if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = 4 * g + i;
-        if (m < M) {
-          float* dst = p.Y + (size_t)m * p.ldy + n;
-          if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i]);
-          else *dst = acc[i];
+        const float other = __shfl_xor(acc[mt][i], 8);
+        const int m = 16 * mt + 4 * g + i;
+        const int o = tile * 8 + r;
+        if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[mt][i]) * other);
+      }
+    } else {
+      const int n = tile * 16 + r;
+      if (n < p.n_valid) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 16 * mt + 4 * g + i;
+          if (m < M) {
+            float* dst = p.Y + (size_t)m * p.ldy + n;
+            if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[mt][i]);
+            else *dst = acc[mt][i];
+          }
         }
       }
     }
@@ -135,10 +149,14 @@ namespace mp {
 template <int PT, int EPI, int NW>
 static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
   // super-blocks in flight per wave: 4, fewer for the fat chunks so the kernel stays within
-  // 128 VGPRs (4 waves per SIMD = two 8-wave workgroups per CU)
+  // 128 VGPRs (4 waves per SIMD = two 8-wave workgroups per CU); two row groups (M <= 32) hold
+  // twice the x ring, so one slot less
   constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
-  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS>), dim3((p.ntiles + NW - 1) / NW, nsplit), dim3(NW * 64), 0,
-                     st, p);
+  const dim3 grid((p.ntiles + NW - 1) / NW, nsplit);
+  if (p.M <= 16) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS, 1>), grid, dim3(NW * 64), 0, st, p);
+  else if (p.M <= 32) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, (NS > 2 ? NS - 1 : 2), 2>), grid, dim3(NW * 64), 0, st, p);
+  else if (p.M <= 48) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 3>), grid, dim3(NW * 64), 0, st, p);
+  else hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 4>), grid, dim3(NW * 64), 0, st, p);
 }
 
 template <int PT, int NW>

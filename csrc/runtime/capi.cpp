@@ -156,10 +156,10 @@ int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const voi
   GemvParams p{};
   p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
   p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
-  if (M > 16) {
-    for (int r0 = 0; r0 < M; r0 += 16) {
+  if (M > 64) {
+    for (int r0 = 0; r0 < M; r0 += 64) {
       GemvParams q = p;
-      q.M = std::min(16, M - r0);
+      q.M = std::min(64, M - r0);
       q.X = p.X + (size_t)r0 * ldx;
       if (q.Y) q.Y = p.Y + (size_t)r0 * ldy;
       if (q.H) q.H = p.H + (size_t)r0 * ldh;

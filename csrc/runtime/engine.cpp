@@ -79,7 +79,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   if (j.get_bool("trace", false)) enable_trace(true);
   M_ = std::max(1, j.get_int("n_mb", 1));
   B_ = std::max(1, j.get_int("mb_size", 1));
-  if (B_ > 16) throw std::runtime_error("mb_size > 16 not supported (decode micro-batch is one MFMA row tile)");
+  if (B_ > 64) throw std::runtime_error("mb_size > 64 not supported (the decode GEMV holds at most 4 MFMA row groups)");
   max_ctx_ = (int)round_up(std::max(64, j.get_int("max_ctx", 2048)), 64);
   chunk_ = std::max(16, j.get_int("prefill_chunk", 256));
   const std::string ftype = j.get_str("ftype", "Q4_K_M");

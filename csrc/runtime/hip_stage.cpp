@@ -459,19 +459,21 @@ void HipStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs
 
 void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
                     int n_valid, bool allow_split, hipStream_t st) {
-  if (M > 16 && opt_.prefill_gemm) {   // prompt chunks: MFMA GEMM, weights read once per 64 rows
+  // up to 64 rows (decode micro-batches, short prompt chunks): the dequant GEMV, 1-4 MFMA row
+  // groups per weight fragment; longer prompt chunks: MFMA GEMM, weights read once per 64 rows
+  if (M > 64 && opt_.prefill_gemm) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
     launch_gemm(m.ptype, epi, p, st);
     return;
   }
-  for (int r0 = 0; r0 < M; r0 += 16) {
+  for (int r0 = 0; r0 < M; r0 += 64) {
     GemvParams p{};
     p.W = m.d;
     p.X = X + (size_t)r0 * ldx;
     p.ldx = ldx;
-    p.M = std::min(16, M - r0);
+    p.M = std::min(64, M - r0);
     p.Y = Y ? Y + (size_t)r0 * ldy : nullptr;
     p.ldy = ldy;
     p.H = H ? H + (size_t)r0 * ldh : nullptr;

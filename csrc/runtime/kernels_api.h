@@ -15,7 +15,7 @@ struct GemvParams {
   const uint8_t* W;      // T16-packed weights
   const f16* X;          // activations [M][ldx] (K_pad columns, zero tail)
   int ldx;
-  int M;                 // rows of X (<= 16 for gemv)
+  int M;                 // rows of X (<= 32 for gemv)
   float* Y;              // EPI_STORE / EPI_ATOMIC destination [M][ldy]
   int ldy;
   f16* H;                // EPI_SWIGLU destination [M][ldh]

@@ -17,7 +17,8 @@ import torch  # noqa: F401  (see module docstring: must precede the dlopen)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmipipe.so")
+# MIPIPE_LIB selects another in-tree build of the library (A/B kernel experiments in one GPU call)
+LIB_PATH = os.path.join(PKG_DIR, "lib", os.environ.get("MIPIPE_LIB", "libmipipe.so"))
 BIN_DIR = os.path.join(PKG_DIR, "bin")
 
 _lock = threading.Lock()

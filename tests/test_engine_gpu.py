@@ -84,6 +84,20 @@ def test_microbatch_invariance(cuda, native, model_dir):
     assert o == singles
 
 
+@pytest.mark.parametrize("mb_size", [24, 40, 64])
+def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
+    """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(mb_size)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, size=int(rng.integers(1, 9)))] for _ in range(mb_size)]
+    with Engine(gguf=path, max_ctx=128) as eng:
+        singles = [eng.generate([p], 6)[0][0] for p in prompts[:6]]
+    with Engine(gguf=path, max_ctx=128, n_mb=1, mb_size=mb_size) as eng:
+        o, _ = eng.generate(prompts, 6)
+    assert o[:6] == singles
+
+
 def test_synthetic_engine_runs(cuda, native):
     from mipipe.engine import Engine
     syn = dict(n_layer=2, d_model=1024, n_head=8, n_head_kv=2, d_ff=2816, vocab=4096)

@@ -37,7 +37,7 @@ def test_unpack_matches_dequant(cuda, native, qt):
 
 
 @pytest.mark.parametrize("qt", QTYPES)
-@pytest.mark.parametrize("M", [1, 3, 16])
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 32, 45, 64, 70])
 def test_gemv_store(cuda, native, qt, M):
     from mipipe.ops.kernels import PackedWeight, gemv, EPI_STORE
     n, k = 80, 1024
@@ -53,9 +53,10 @@ def test_gemv_store(cuda, native, qt, M):
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0, Q.F16])
 @pytest.mark.parametrize("nsplit", [1, 3, 8])
-def test_gemv_atomic_split(cuda, native, qt, nsplit):
+@pytest.mark.parametrize("M", [5, 29, 61])
+def test_gemv_atomic_split(cuda, native, qt, nsplit, M):
     from mipipe.ops.kernels import PackedWeight, gemv, EPI_ATOMIC
-    n, k, M = 64, 2048, 5
+    n, k = 64, 2048
     raw, deq = _weights(qt, n, k, 7)
     w = PackedWeight(raw, qt, n, k)
     xh = torch.randn(M, k).half()
@@ -66,9 +67,10 @@ def test_gemv_atomic_split(cuda, native, qt, nsplit):
 
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q5_K, Q.Q8_0])
-def test_gemv_swiglu(cuda, native, qt):
+@pytest.mark.parametrize("M", [4, 32, 48, 64])
+def test_gemv_swiglu(cuda, native, qt, M):
     from mipipe.ops.kernels import PackedWeight, gemv, EPI_SWIGLU
-    F, k, M = 40, 512, 4
+    F, k = 40, 512
     rng = np.random.default_rng(5)
     g = (rng.standard_normal((F, k)) / math.sqrt(k)).astype(np.float32)
     u = (rng.standard_normal((F, k)) / math.sqrt(k)).astype(np.float32)
