@@ -10,7 +10,8 @@ Weights are random-init directly in HBM with the exact Llama-3-70B architecture 
 format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
 cost-balanced split with the LM head on the last stage); activations move stage to stage with
 RCCL send/recv over xGMI; M = N micro-batches of `--mb-size` sequences circulate through the
-piped ring.  Weak scaling: per-GPU work is fixed (every stage streams its own weights once per
+piped ring (default 64 sequences per micro-batch: the decode GEMV shares each dequantized weight
+fragment across 4 MFMA row groups; --mb-size 1 gives the single-stream latency).  Weak scaling: per-GPU work is fixed (every stage streams its own weights once per
 micro-batch per round), global batch = N * mb_size sequences.
 The timed region is exactly K decode rounds (every sequence emits one token per round),
 bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
@@ -47,7 +48,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="llama3-70b", choices=sorted(MODELS))
     ap.add_argument("--ftype", default="Q4_K")
-    ap.add_argument("--mb-size", type=int, default=16, help="sequences per micro-batch (<= 64; > 16 runs the decode projections on the MFMA GEMM)")
+    ap.add_argument("--mb-size", type=int, default=64, help="sequences per micro-batch (<= 64; > 16 runs the decode projections on the MFMA GEMM)")
     ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = #GPUs)")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")

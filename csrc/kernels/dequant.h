@@ -27,6 +27,9 @@ namespace mpk {
 using namespace mp;
 
 __device__ __forceinline__ constexpr int t16_xoff(int g, int i) { return 64 * g + 8 * i; }
+// LDS x tiles (16 B-chunked rows of 256 k, padded to 264 f16): the k-quarters of rows 8..15 (mod 16)
+// are stored swapped in pairs so that an A-fragment ds_read_b128 is bank-conflict free (gemv2.hip)
+__device__ __forceinline__ constexpr int x_qswap(int row) { return ((row >> 3) & 1) << 6; }
 
 __device__ __forceinline__ half2_t h2lo(half2_t v) { return half2_t{v.x, v.x}; }
 __device__ __forceinline__ half2_t h2hi(half2_t v) { return half2_t{v.y, v.y}; }

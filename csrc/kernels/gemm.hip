@@ -18,7 +18,7 @@ namespace mpk {
 using namespace mp;
 
 constexpr int GM_BM = 64;          // rows per workgroup
-constexpr int GM_LDX = 256 + 8;    // padded LDS row (f16): 528 B, rows 4 dwords apart -> no conflicts
+constexpr int GM_LDX = 256 + 8;    // padded LDS row (f16), quarters swapped per x_qswap (dequant.h)
 
 template <int PT, int EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = tid + 256 * j, row = c >> 5, col = (c & 31) * 8;
-      *reinterpret_cast<u32x4*>(&xs[buf][row * GM_LDX + col]) = xv[j];
+      *reinterpret_cast<u32x4*>(&xs[buf][row * GM_LDX + (col ^ x_qswap(row))]) = xv[j];
     }
   };
 
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
       else D::template dequant<1>(raw[cur], b, lane);
 #pragma unroll
       for (int ms = 0; ms < 4; ++ms) {
-        const f16* xr = &xs[cur][(16 * ms + r) * GM_LDX + t16_xoff(g, 4 * h)];
+        const f16* xr = &xs[cur][(16 * ms + r) * GM_LDX + (t16_xoff(g, 4 * h) ^ x_qswap(r))];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const half8_t a = *reinterpret_cast<const half8_t*>(xr + 8 * s);

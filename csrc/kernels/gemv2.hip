@@ -22,7 +22,13 @@
 namespace mpk {
 using namespace mp;
 
-constexpr int G2_LDX = 256 + 8;   // padded f16 row in LDS (528 B): 16 rows of a fragment read hit distinct banks
+// x tile in LDS: padded f16 rows (528 B) and the quarters of rows 8..15 (mod 16) swapped in pairs
+// (k-quarter q of row m stored at quarter q ^ ((m >> 3) & 1)).  The padding alone left every
+// ds_read_b128 of an A fragment 2-way bank-conflicted (its lane groups {0-3,12-15,20-27}.. mix
+// rows r and r + 8 of two quarters: SQ_LDS_BANK_CONFLICT = 44 % of SQ_LDS_IDX_ACTIVE); with the
+// swap the 16 lanes of each group cover the 64 banks exactly once.  The 8-lane groups of the
+// ds_write_b128 staging stay within one row and one quarter: conflict-free as before.
+constexpr int G2_LDX = 256 + 8;
 
 // MT row groups of 16 activation rows (M <= 16 MT) share every dequantized weight fragment: the
 // dequant VALU work, which bounds the kernel near HBM speed at M = 16, is paid once for 16 MT rows.
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
       const int c = tid + NT * j;
       if (c < XC) {
         const int row = c >> 5, col = (c & 31) * 8;
-        *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + col]) = xv[sl][j];
+        *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + (col ^ x_qswap(row))]) = xv[sl][j];
       }
     }
   };
@@ -82,8 +88,8 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   __syncthreads();
 
   // rows >= M are zero in LDS (their outputs are never stored)
-  const f16* xrow0 = &xs[0][r * G2_LDX + t16_xoff(g, 0)];
-  const f16* xrow1 = &xs[1][r * G2_LDX + t16_xoff(g, 0)];
+  const f16* xrow0 = &xs[0][r * G2_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
+  const f16* xrow1 = &xs[1][r * G2_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
   // one super-block; all loads unconditional (clamped to the range): path-independent vmcnt
   auto step = [&](const int sl, const int cur) {
     const int buf = (cur - sbA) & 1;
