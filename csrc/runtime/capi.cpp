@@ -377,6 +377,25 @@ const char* mp_engine_generate(void* h, const int32_t* prompt_tokens, const int3
   return g_str.c_str();
   API_CATCH(nullptr)
 }
+// Speculative (prompt-lookup) greedy generation: same layout as mp_engine_generate; draft_max tokens
+// drafted per sequence per verify round from its last ngram-gram.  Returns JSON stats.
+const char* mp_engine_spec_generate(void* h, const int32_t* prompt_tokens, const int32_t* lens, int n_seq,
+                                    int n_predict, int draft_max, int ngram, int32_t* out_tokens) {
+  API_TRY
+  std::vector<std::vector<int32_t>> prompts;
+  size_t off = 0;
+  for (int i = 0; i < n_seq; ++i) {
+    prompts.emplace_back(prompt_tokens + off, prompt_tokens + off + lens[i]);
+    off += lens[i];
+  }
+  std::vector<std::vector<int32_t>> outs;
+  Json stats = static_cast<Engine*>(h)->spec_generate(prompts, n_predict, draft_max, ngram, &outs);
+  for (int i = 0; i < n_seq; ++i)
+    for (int j = 0; j < n_predict; ++j) out_tokens[(size_t)i * n_predict + j] = j < (int)outs[i].size() ? outs[i][j] : -1;
+  g_str = stats.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
 // Benchmark decode loop: n_warmup + n_steps decode steps of every micro-batch after a prefill of
 // prompt_len synthetic tokens. Returns JSON stats.
 const char* mp_engine_bench(void* h, int prompt_len, int n_warmup, int n_steps) {

@@ -463,13 +463,29 @@ void CpuStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t)
   // rows carry their own slot and position, so the packed chunk runs as one batch (the causal
   // mask per row is its position; other sequences' rows are in other slots)
   for (size_t li = 0; li < layers_.size(); ++li) layer_forward((int)li, T, x, pos.data(), slot.data());
-  if (spec_.last()) {
+  if (spec_.last() && !segs.empty() && segs[0].verify) {
+    // speculative verification: greedy next token after every row of the chunk
+    if (vtok_.size() < (size_t)opt_.n_mb) vtok_.resize(opt_.n_mb);
+    std::vector<float> xn((size_t)T * d), lg((size_t)T * cfg_.vocab);
+    rmsnorm(x, out_norm_, xn.data(), T);
+    matmul(out_, xn.data(), d, T, lg.data(), cfg_.vocab, false);
+    vtok_[mb].assign(T, 0);
+    for (int m = 0; m < T; ++m) {
+      const float* r = lg.data() + (size_t)m * cfg_.vocab;
+      vtok_[mb][m] = (int32_t)(std::max_element(r, r + cfg_.vocab) - r);
+    }
+  } else if (spec_.last()) {
     int row = 0;
     for (const PrefillSeg& s : segs) {
       row += s.T;
       if (s.last) std::memcpy(last_h_[mb].data() + (size_t)s.b * d, x + (size_t)(row - 1) * d, (size_t)d * 4);
     }
   }
+}
+
+void CpuStage::copy_verify_tokens(int mb, int32_t* host, int n) {
+  if ((size_t)mb >= vtok_.size() || (int)vtok_[mb].size() < n) throw std::runtime_error("no verify tokens");
+  std::memcpy(host, vtok_[mb].data(), (size_t)n * 4);
 }
 
 void CpuStage::prefill_finish(int mb, hipStream_t) {

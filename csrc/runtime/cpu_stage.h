@@ -42,6 +42,7 @@ class CpuStage : public Stage {
   void set_positions(int mb, const std::vector<int32_t>& pos) override;
   void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
   void prefill_finish(int mb, hipStream_t st) override;
+  void copy_verify_tokens(int mb, int32_t* host, int n) override;
   void decode(int mb, hipStream_t st) override;
   const float* logits_ptr() const override { return logits_.data(); }
   int logits_ld() const override { return cfg_.vocab; }
@@ -83,6 +84,7 @@ class CpuStage : public Stage {
   std::vector<std::vector<int32_t>> tok_, pos_;
   std::vector<int32_t> prompt_;
   std::vector<std::vector<float>> last_h_;   // last stage: [mb][B][d] final prompt rows
+  std::vector<std::vector<int32_t>> vtok_;   // last stage: [mb][rows] greedy tokens of a verify chunk
   std::vector<float> logits_;
   // scratch
   std::vector<float> xn_, qkv_, att_, h_, gu_;

@@ -784,6 +784,130 @@ Json Engine::generate(const std::vector<std::vector<int32_t>>& prompts, int n_pr
   return j;
 }
 
+// Draft for prompt-lookup decoding: the tokens that followed the most recent earlier occurrence
+// of the context's last g-gram (g = ngram .. 1), at most k of them.
+static std::vector<int32_t> lookup_draft(const std::vector<int32_t>& ctx, int k, int ngram) {
+  const int n = (int)ctx.size();
+  for (int g = std::min(ngram, n - 1); g >= 1; --g)
+    for (int s = n - g - 1; s >= 0; --s)
+      if (std::equal(ctx.begin() + s, ctx.begin() + s + g, ctx.end() - g)) {
+        const int from = s + g;
+        if (from < n) return std::vector<int32_t>(ctx.begin() + from, ctx.begin() + std::min(n, from + k));
+      }
+  return {};
+}
+
+// Speculative decoding by prompt lookup (llama.cpp's `llama-lookup`; the design report's
+// speculative decoding, PDF p.12 / SURVEY.md D10).  Every round, each sequence drafts up to
+// `draft_max` tokens from its own context (lookup_draft), and ONE verify chunk per micro-batch
+// scores [last token, draft...] at positions pos .. pos+k through the whole pipeline on the
+// prefill path (causal attention against the KV cache; every projection one GEMV/GEMM over all
+// rows, i.e. the weights are streamed once for k+1 tokens of every sequence).  The last stage
+// returns the greedy token after each row; the host accepts the longest agreeing draft prefix
+// plus the target's own next token, so the output equals plain greedy decoding.  KV rows written
+// for rejected draft positions are overwritten by the next chunk (attention reads [0, kvlen)).
+Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict, int draft_max,
+                           int ngram, std::vector<std::vector<int32_t>>* out) {
+  if ((int)workers_.size() != S_) throw std::runtime_error("speculative decoding needs every stage in this process");
+  if (jcfg_.get_num("temp", 0.0) > 0.0) throw std::runtime_error("speculative decoding is greedy (temp 0)");
+  if (jcfg_.get_num("repeat_penalty", 1.0) != 1.0 || jcfg_.get_num("frequency_penalty", 0.0) != 0.0 ||
+      jcfg_.get_num("presence_penalty", 0.0) != 0.0)
+    throw std::runtime_error("speculative decoding runs without repetition penalties");
+  // one verify chunk per micro-batch: B sequences x (k + 1) rows <= prefill chunk
+  const int k = std::max(1, std::min(draft_max, chunk_ / B_ - 1));
+  if (k < 1 || chunk_ / B_ < 2) throw std::runtime_error("prefill chunk too small for speculative decoding");
+  ngram = std::max(1, ngram);
+  Worker* wf = nullptr;
+  Worker* wl = nullptr;
+  for (auto& w : workers_) {
+    if (w->stage->spec().first()) wf = w.get();
+    if (w->stage->spec().last()) wl = w.get();
+  }
+  const double t0 = now_ms();
+  start(prompts);
+  const double t1 = now_ms();
+  const size_t n = prompts.size();
+  std::vector<std::vector<int32_t>> ctx(n);
+  for (size_t i = 0; i < n; ++i) {
+    ctx[i] = prompts[i];
+    ctx[i].insert(ctx[i].end(), gen_[i].begin(), gen_[i].end());
+  }
+  long rounds = 0, drafted = 0, accepted = 0;
+  std::vector<int32_t> vt(chunk_);
+  for (;;) {
+    std::vector<Item> items;
+    std::vector<std::vector<int32_t>> chunk(n);
+    for (int mb = 0; mb < M_; ++mb) {
+      Item it{Item::PREFILL};
+      it.mb = mb;
+      for (int b = 0; b < B_; ++b) {
+        const size_t i = (size_t)mb * B_ + b;
+        if (i >= n || (int)gen_[i].size() >= n_predict || (int)ctx[i].size() >= max_ctx_) continue;
+        const int pos = (int)ctx[i].size() - 1;   // the last token is not in the KV cache yet
+        std::vector<int32_t> d = lookup_draft(ctx[i], k, ngram);
+        const int room = std::min(max_ctx_ - pos - 1, n_predict - (int)gen_[i].size() - 1);
+        if ((int)d.size() > room) d.resize(std::max(0, room));
+        chunk[i].push_back(ctx[i].back());
+        chunk[i].insert(chunk[i].end(), d.begin(), d.end());
+        drafted += (long)d.size();
+        if (cpu_) std::memcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4);
+        else {
+          HIP_OK(hipSetDevice(wf->device));
+          HIP_OK(hipMemcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4,
+                           hipMemcpyHostToDevice));
+        }
+        PrefillSeg sg;
+        sg.b = b; sg.p0 = pos; sg.T = (int)chunk[i].size(); sg.last = true; sg.verify = true;
+        it.segs.push_back(sg);
+        it.T += sg.T;
+      }
+      if (it.T > 0) items.push_back(it);
+    }
+    if (items.empty()) break;
+    run_all(items);
+    ++rounds;
+    for (const Item& it : items) {
+      if (!cpu_) HIP_OK(hipSetDevice(wl->device));
+      wl->stage->copy_verify_tokens(it.mb, vt.data(), it.T);
+      int row = 0;
+      for (const PrefillSeg& sg : it.segs) {
+        const size_t i = (size_t)it.mb * B_ + sg.b;
+        const std::vector<int32_t>& c = chunk[i];
+        int a = 0;   // accepted draft tokens: c[1 + a] agrees with the target's token after row a
+        while (1 + a < (int)c.size() && c[1 + a] == vt[row + a]) ++a;
+        accepted += a;
+        for (int j = 0; j <= a; ++j) {
+          const int32_t t = vt[row + j];   // = c[1 + j] for j < a, the target's own token at j = a
+          gen_[i].push_back(t);
+          ctx[i].push_back(t);
+          if (on_token) on_token((int)i, t);
+        }
+        if ((int)gen_[i].size() > n_predict) gen_[i].resize(n_predict);
+        row += sg.T;
+      }
+    }
+  }
+  started_ = false;   // positions on the devices no longer follow the decode schedule
+  const double t2 = now_ms();
+  if (out) *out = gen_;
+  size_t n_prompt = 0, n_gen = 0;
+  for (auto& p : prompts) n_prompt += p.size();
+  for (auto& g : gen_) n_gen += g.size() > 0 ? g.size() - 1 : 0;
+  Json j = Json::object();
+  j["prefill_ms"] = t1 - t0;
+  j["decode_ms"] = t2 - t1;
+  j["n_prompt_tokens"] = (int64_t)n_prompt;
+  j["n_decode_tokens"] = (int64_t)n_gen;
+  j["decode_tok_s"] = n_gen / std::max(1e-9, (t2 - t1) / 1e3);
+  j["verify_rounds"] = (int64_t)rounds;
+  j["draft_max"] = k;
+  j["drafted"] = (int64_t)drafted;
+  j["accepted"] = (int64_t)accepted;
+  j["acceptance"] = drafted ? (double)accepted / drafted : 0.0;
+  j["tokens_per_round"] = rounds ? (double)n_gen / rounds / std::max<size_t>(1, n) : 0.0;
+  return j;
+}
+
 Json Engine::bench(int prompt_len, int warmup, int steps) {
   std::vector<std::vector<int32_t>> prompts(M_ * B_);
   uint32_t h = 12345;

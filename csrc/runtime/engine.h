@@ -69,6 +69,9 @@ class Engine {
 
   Json generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict,
                 std::vector<std::vector<int32_t>>* out);
+  // Speculative decoding by prompt lookup (greedy; every stage in this process): see engine.cpp
+  Json spec_generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict, int draft_max, int ngram,
+                     std::vector<std::vector<int32_t>>* out);
   Json bench(int prompt_len, int warmup, int steps);
   int copy_logits(int mb, float* out, int rows);
   // Chrome-trace timeline of compute / send / recv spans per stage

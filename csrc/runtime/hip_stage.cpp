@@ -622,7 +622,16 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, T, x, pf_pos_, pf_kvlen_, pf_slot_, false, st);
   segs_ = nullptr;
-  if (spec_.last()) {
+  if (spec_.last() && !segs.empty() && segs[0].verify) {
+    // speculative verification: LM head over every row of the chunk, greedy next token per row
+    if (!vlogits_) {
+      vlogits_ = (float*)dmalloc((size_t)opt_.prefill_chunk * logits_ld_ * 4);
+      vtok_ = (int32_t*)dmalloc((size_t)opt_.n_mb * opt_.prefill_chunk * 4);
+    }
+    launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, T, nullptr, 0, st);
+    gemv(out_, EPI_STORE, xn_, Kd_, T, vlogits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
+    launch_argmax(vlogits_, logits_ld_, cfg_.vocab, T, vtok_ + (size_t)mb * opt_.prefill_chunk, st);
+  } else if (spec_.last()) {
     int row = 0;
     for (const PrefillSeg& s : segs) {
       row += s.T;
@@ -631,6 +640,12 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
                               hipMemcpyDeviceToDevice, st));
     }
   }
+}
+
+void HipStage::copy_verify_tokens(int mb, int32_t* host, int n) {
+  if (!vtok_ || n > opt_.prefill_chunk) throw std::runtime_error("no verify tokens");
+  HIP_OK(hipSetDevice(spec_.device));
+  HIP_OK(hipMemcpy(host, vtok_ + (size_t)mb * opt_.prefill_chunk, (size_t)n * 4, hipMemcpyDeviceToHost));
 }
 
 void HipStage::prefill_finish(int mb, hipStream_t st) {

@@ -93,6 +93,7 @@ class HipStage : public Stage {
   // packed prefill chunk (see Stage::prefill) and the head over the kept last rows
   void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
   void prefill_finish(int mb, hipStream_t st) override;
+  void copy_verify_tokens(int mb, int32_t* host, int n) override;
 
   // One decode step for micro-batch mb (graph replay if captured).
   void decode(int mb, hipStream_t st) override;
@@ -171,6 +172,8 @@ class HipStage : public Stage {
   int32_t* pf_pos_ = nullptr; int32_t* pf_kvlen_ = nullptr; int32_t* pf_slot_ = nullptr;
   int32_t* prompt_dev_ = nullptr;
   std::vector<float*> last_h_;                       // last stage: [mb][B][d] final prompt rows
+  float* vlogits_ = nullptr;                          // last stage, speculative verify: [chunk][logits_ld_]
+  int32_t* vtok_ = nullptr;                           // [n_mb][chunk] greedy token after each verify row
   const std::vector<PrefillSeg>* segs_ = nullptr;    // segments of the prefill in progress
   // graphs
   std::vector<hipGraphExec_t> graphs_;

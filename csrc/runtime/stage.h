@@ -32,6 +32,8 @@ struct PrefillSeg {
   int p0 = 0;         // first position of this segment
   int T = 0;          // tokens
   bool last = false;  // ends the prompt
+  bool verify = false;  // speculative verification chunk: the last stage scores EVERY row (greedy
+                        // argmax after each row -> verify_tokens), nothing is kept for prefill_finish
 };
 
 class Stage {
@@ -59,6 +61,9 @@ class Stage {
   // last stage: LM head + sampling over the kept rows -> tokens(mb)[b] for every sequence of mb
   virtual void prefill_finish(int mb, hipStream_t st) = 0;
   virtual void decode(int mb, hipStream_t st) = 0;
+  // last stage, after a prefill() of verify segments of micro-batch mb: the greedy next token after
+  // each of the chunk's n rows (row order = segment order) -> host
+  virtual void copy_verify_tokens(int mb, int32_t* host, int n) = 0;
   virtual const float* logits_ptr() const = 0;   // last computed logits (device/host)
   virtual int logits_ld() const = 0;
   virtual size_t weight_bytes() const = 0;

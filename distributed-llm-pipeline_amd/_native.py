@@ -69,6 +69,7 @@ _SIGS = {
     "mp_engine_health": ([c_void_p], c_char_p),
     "mp_engine_trace": ([c_void_p, c_int, c_char_p], c_int),
     "mp_engine_generate": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p], c_char_p),
+    "mp_engine_spec_generate": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p], c_char_p),
     "mp_engine_bench": ([c_void_p, c_int, c_int, c_int], c_char_p),
     "mp_engine_start": ([c_void_p, c_void_p, c_void_p, c_int], c_int),
     "mp_engine_decode": ([c_void_p, c_int], c_char_p),

@@ -61,6 +61,15 @@ class Engine:
                         n_predict, out.ctypes.data, what="generate")
         return out.tolist(), stats
 
+    def spec_generate(self, prompts, n_predict: int, draft_max: int = 4, ngram: int = 3):
+        """Greedy speculative decoding by prompt lookup (drafts from each sequence's own context,
+        one verify chunk per micro-batch per round); output equals generate() at temp 0."""
+        flat, lens = self._flat(prompts)
+        out = np.full((len(prompts), n_predict), -1, np.int32)
+        stats = N.jcall(N.lib().mp_engine_spec_generate, self._h, flat.ctypes.data, lens.ctypes.data, len(prompts),
+                        n_predict, draft_max, ngram, out.ctypes.data, what="spec_generate")
+        return out.tolist(), stats
+
     def start(self, prompts):
         flat, lens = self._flat(prompts)
         self._n_seq = len(prompts)

@@ -217,3 +217,50 @@ def test_cpu_repetition_penalties_match_reference(native, model_dir):
     with Engine(gguf=path, backend="cpu", max_ctx=64) as eng:
         plain, _ = eng.generate([prompt], 10)
     assert plain[0] != want   # the penalties changed the greedy path
+
+
+@pytest.mark.parametrize("stages,n_mb,mb_size", [(1, 1, 1), (1, 2, 2), (2, 2, 2)])
+def test_cpu_speculative_lookup_matches_greedy(native, model_dir, stages, n_mb, mb_size):
+    """Prompt-lookup speculative decoding reproduces plain greedy decoding exactly,
+    across micro-batches and pipeline stages, and accepts drafts on repetitive context."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(3)
+    motif = [int(t) for t in rng.integers(3, cfg.vocab, 6)]
+    prompts = [motif * 4, [int(t) for t in rng.integers(3, cfg.vocab, 11)], motif * 2 + [7, 8], [42, 43, 44]]
+    prompts = prompts[: n_mb * mb_size]
+    kw = dict(gguf=path, backend="cpu", max_ctx=128, n_mb=n_mb, mb_size=mb_size, prefill_chunk=32,
+              stages=stages, split="even")
+    with Engine(**kw) as eng:
+        ref, _ = eng.generate(prompts, 24)
+    with Engine(**kw) as eng:
+        out, st = eng.spec_generate(prompts, 24, draft_max=5, ngram=3)
+        # the engine stays usable for plain generation afterwards
+        again, _ = eng.generate(prompts[:1], 6)
+    assert out == ref
+    assert again[0] == ref[0][:6]
+    assert st["verify_rounds"] <= 23
+    assert st["drafted"] >= st["accepted"] >= 0
+
+
+def test_cpu_speculative_lookup_accepts_repeats(native, model_dir):
+    """Greedy decoding of stories15m (random init) falls into a repeated-token run that prompt
+    lookup drafts and the verifier accepts: fewer verify rounds than tokens, same output."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "stories15m", "F32")
+    rng = np.random.default_rng(3)
+    prompt = [int(t) for t in rng.integers(3, cfg.vocab, 6)] * 4
+    with Engine(gguf=path, backend="cpu", max_ctx=256) as eng:
+        ref, _ = eng.generate([prompt], 60)
+        out, st = eng.spec_generate([prompt], 60, draft_max=5, ngram=3)
+    assert out == ref
+    assert st["accepted"] > 0 and st["verify_rounds"] < 59, st
+    assert st["n_decode_tokens"] == 59
+
+
+def test_cpu_speculative_rejects_sampling(native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=64, temp=0.8) as eng:
+        with pytest.raises(RuntimeError, match="greedy"):
+            eng.spec_generate([[5, 6, 7]], 4)

@@ -250,3 +250,25 @@ def test_repetition_penalties_match_reference(cuda, native, model_dir):
             seq.append(tok)
             eng.decode(1)
             rl = penalize(ref.forward([tok], len(seq) - 1)[-1].numpy(), seq[-last_n:])
+
+
+@pytest.mark.parametrize("stages,n_mb,mb_size", [(1, 1, 1), (1, 2, 2), (2, 2, 2)])
+def test_speculative_lookup_matches_greedy(cuda, native, model_dir, stages, n_mb, mb_size):
+    """Prompt-lookup speculative decoding on the HIP path (verify chunks through the prefill GEMV/
+    GEMM + per-row LM head and argmax) equals plain greedy decoding; PP=2 emulated on one GPU."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(3)
+    motif = [int(t) for t in rng.integers(3, cfg.vocab, 6)]
+    prompts = [motif * 4, [int(t) for t in rng.integers(3, cfg.vocab, 11)], motif * 2 + [7, 8], [42, 43, 44]]
+    prompts = prompts[: n_mb * mb_size]
+    kw = dict(gguf=path, max_ctx=128, n_mb=n_mb, mb_size=mb_size, prefill_chunk=32, stages=stages,
+              devices=[0] * stages, link="local", split="even")
+    with Engine(**kw) as eng:
+        ref, _ = eng.generate(prompts, 24)
+    with Engine(**kw) as eng:
+        out, st = eng.spec_generate(prompts, 24, draft_max=5, ngram=3)
+        again, _ = eng.generate(prompts[:1], 6)
+    assert out == ref
+    assert again[0] == ref[0][:6]
+    assert st["drafted"] >= st["accepted"] >= 0
