@@ -827,6 +827,8 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
   start(prompts);
   const double t1 = now_ms();
   const size_t n = prompts.size();
+  if (on_token)
+    for (size_t i = 0; i < n; ++i) on_token((int)i, gen_[i][0]);
   std::vector<std::vector<int32_t>> ctx(n);
   for (size_t i = 0; i < n; ++i) {
     ctx[i] = prompts[i];
@@ -843,6 +845,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
       for (int b = 0; b < B_; ++b) {
         const size_t i = (size_t)mb * B_ + b;
         if (i >= n || (int)gen_[i].size() >= n_predict || (int)ctx[i].size() >= max_ctx_) continue;
+        if (keep_going && !keep_going((int)i)) continue;
         const int pos = (int)ctx[i].size() - 1;   // the last token is not in the KV cache yet
         std::vector<int32_t> d = lookup_draft(ctx[i], k, ngram);
         const int room = std::min(max_ctx_ - pos - 1, n_predict - (int)gen_[i].size() - 1);

@@ -83,6 +83,9 @@ class Engine {
   // streaming hook: called on the host (from the worker of the last stage) after each round
   // with (sequence index, token) pairs
   std::function<void(int seq, int32_t tok)> on_token;
+  // spec_generate: a sequence for which this returns false is finished (e.g. end of generation)
+  std::function<bool(int seq)> keep_going;
+  const Json& config() const { return jcfg_; }
 
  private:
   struct Worker {

@@ -95,6 +95,39 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
     if (emit && !p.empty() && reqs[i].on_piece && !reqs[i].on_piece(p)) { active[i] = false; r.stop = "cancelled"; }
   };
   const double t0 = now_ms();
+  const int draft_max = eng_.config().get_int("draft_max", 0);
+  if (draft_max > 0 && early_stop) {
+    // speculative decoding by prompt lookup (greedy): tokens arrive in accepted runs per round
+    std::vector<int> steps(reqs.size(), 0);
+    double t_first = 0;
+    eng_.on_token = [&](int i, int32_t t) { consume((size_t)i, t, steps[i]++); };
+    eng_.keep_going = [&](int i) { return (bool)active[i]; };
+    auto cleanup = [&] { eng_.on_token = nullptr; eng_.keep_going = nullptr; };
+    try {
+      std::vector<std::vector<int32_t>> gen;
+      const Json st = eng_.spec_generate(prompts, std::max(1, n_max), draft_max,
+                                         eng_.config().get_int("lookup_ngram", 3), &gen);
+      t_first = t0 + st.get_num("prefill_ms", 0.0);
+      MP_LOGI("speculative lookup: %ld verify rounds, %ld/%ld drafted tokens accepted",
+              (long)st.get_num("verify_rounds", 0), (long)st.get_num("accepted", 0), (long)st.get_num("drafted", 0));
+    } catch (...) {
+      cleanup();
+      throw;
+    }
+    cleanup();
+    const double t2 = now_ms();
+    for (size_t i = 0; i < reqs.size(); ++i) {
+      if (active[i]) res[i].stop = n_max < reqs[i].n_predict ? "context" : "length";
+      const std::string tail = acc[i].buf;
+      if (!tail.empty()) {
+        res[i].text += tail;
+        if (emit && active[i] && reqs[i].on_piece) reqs[i].on_piece(tail);
+      }
+      res[i].prefill_ms = t_first - t0;
+      res[i].decode_ms = t2 - t_first;
+    }
+    return res;
+  }
   eng_.start(prompts);
   const double t1 = now_ms();
   if (n_max > 0)

@@ -79,6 +79,8 @@ inline void print_common_usage(FILE* f) {
           "  --repeat-penalty R --repeat-last-n N --frequency-penalty F --presence-penalty P\n"
           "                            penalties over the last N tokens (default 1.0 / 64 / 0 / 0)\n"
           "  --sampling greedy         force greedy\n"
+          "  --draft-max K             speculative decoding by prompt lookup: up to K drafted tokens per\n"
+          "                            verify round (greedy; --lookup-ngram N, default 3)\n"
           "placement / pipeline:\n"
           "  -ngl, --n-gpu-layers N    0 = CPU backend, otherwise all layers on GPUs (default 99)\n"
           "  --stages N, --pp N        pipeline stages (one GPU each)\n"
@@ -135,6 +137,8 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--link") e["link"] = val();
     else if (a == "--prefill-chunk" || a == "-ub" || a == "--ubatch-size") e["prefill_chunk"] = std::atoi(val().c_str());
     else if (a == "--no-graphs") e["graphs"] = false;
+    else if (a == "--draft-max" || a == "--draft") e["draft_max"] = std::atoi(val().c_str());   // prompt-lookup speculation
+    else if (a == "--lookup-ngram") e["lookup_ngram"] = std::atoi(val().c_str());
     else if (a == "--threads" || a == "-t") e["threads"] = std::atoi(val().c_str());
     else if (a == "--world") world = std::atoi(val().c_str());
     else if (a == "--rank") rank = std::atoi(val().c_str());

@@ -213,3 +213,14 @@ def test_cli_daemon_and_bench(native_bins, tiny_gguf):
     tr = json.load(open(os.path.join(os.path.dirname(tiny_gguf), "tr.json")))
     names = {e["name"].split(" ")[0] for e in tr["traceEvents"] if e["ph"] == "X"}
     assert {"decode", "send", "recv", "prefill"} <= names
+
+
+def test_cli_speculative_lookup_same_text(native_bins, tiny_gguf):
+    """mi-cli --draft-max (prompt-lookup speculative decoding) prints the same greedy text."""
+    prompt = "the cat sat on the mat and the cat sat on the"
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-p", prompt, "-n", "24", "-c", "256", "-ngl", "0"]
+    a = subprocess.run(base, capture_output=True, timeout=120)
+    b = subprocess.run(base + ["--draft-max", "4"], capture_output=True, timeout=120)
+    assert a.returncode == 0 and b.returncode == 0, b.stderr.decode(errors="replace")
+    assert a.stdout == b.stdout and len(a.stdout) > len(prompt)
+    assert b"speculative lookup" in b.stderr
