@@ -14,10 +14,43 @@ const Json& Json::operator[](const std::string& k) const {
   return it == o_.end() ? kNull : it->second;
 }
 
+// length of the valid UTF-8 sequence starting at s[i] (0 if invalid: stray continuation byte,
+// overlong form, surrogate, > U+10FFFF or truncated)
+static size_t utf8_len(const std::string& s, size_t i) {
+  const unsigned char c = (unsigned char)s[i];
+  size_t n;
+  uint32_t cp;
+  if (c < 0x80) return 1;
+  if ((c & 0xE0) == 0xC0) { n = 2; cp = c & 0x1F; }
+  else if ((c & 0xF0) == 0xE0) { n = 3; cp = c & 0x0F; }
+  else if ((c & 0xF8) == 0xF0) { n = 4; cp = c & 0x07; }
+  else return 0;
+  if (i + n > s.size()) return 0;
+  for (size_t k = 1; k < n; ++k) {
+    const unsigned char d = (unsigned char)s[i + k];
+    if ((d & 0xC0) != 0x80) return 0;
+    cp = (cp << 6) | (d & 0x3F);
+  }
+  if ((n == 2 && cp < 0x80) || (n == 3 && cp < 0x800) || (n == 4 && cp < 0x10000) || cp > 0x10FFFF ||
+      (cp >= 0xD800 && cp <= 0xDFFF))
+    return 0;
+  return n;
+}
+
+// JSON string body; bytes that are not valid UTF-8 (a token piece cut inside a character, a
+// binary prompt) become U+FFFD, like the reference's lossy decoding (main.rs:68,88)
 std::string json_escape(const std::string& s) {
   std::string o;
   o.reserve(s.size() + 8);
-  for (unsigned char c : s) {
+  for (size_t i = 0; i < s.size();) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c >= 0x80) {
+      const size_t n = utf8_len(s, i);
+      if (n == 0) { o += "\xEF\xBF\xBD"; ++i; }
+      else { o.append(s, i, n); i += n; }
+      continue;
+    }
+    ++i;
     switch (c) {
       case '"': o += "\\\""; break;
       case '\\': o += "\\\\"; break;

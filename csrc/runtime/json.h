@@ -43,6 +43,7 @@ class Json {
   const Json& operator[](const std::string& k) const;
   Json& operator[](const std::string& k) { t_ = OBJ; return o_[k]; }
   void push(Json v) { t_ = ARR; a_.push_back(std::move(v)); }
+  void erase(const std::string& k) { o_.erase(k); }
 
   double get_num(const std::string& k, double d) const { return has(k) && o_.at(k).is_num() ? o_.at(k).n_ : d; }
   int get_int(const std::string& k, int d) const { return (int)get_num(k, d); }

@@ -12,13 +12,19 @@
 //   GET  /metrics     Prometheus text (requests, tokens, tok/s, p50/p90/p99 per token, stage
 //                     heartbeats, link bytes)
 //   GET  /health      engine health JSON
+//   GET  /models      registered models ({"data": [{"id", "loaded", "source"}]}); requests pick one
+//                     with "model": NAME (--model-alias NAME=PATH|synthetic:NAME, PDF p.7 item 3:
+//                     multi-model management), at most --max-models engines resident (LRU)
 //   GET  /*           static files (default ./static, index.html at /) (main.rs:104)
 //   CORS: Access-Control-Allow-Origin * on every response, OPTIONS preflight (main.rs:105)
 //   errors as axum's Json extractor: 415 (not application/json), 400 (bad JSON), 422 (no
 //   "prompt" string), 405 (wrong method), 404; optional --api-key (401) and --rate-limit (429)
 //
 // Concurrency: connection thread per client; one generation thread batches up to
-// n_mb * mb_size queued requests into one engine run (request-level batching).
+// n_mb * mb_size queued requests for the same model into one engine run (request-level batching,
+// SURVEY.md D5).  A failed run whose engine reports a fault (stage exception, link abort, watchdog)
+// is answered with an error and the engine is rebuilt from its config (the design report's worker
+// auto-restart, PDF p.6-7 / SURVEY.md D6).
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -62,6 +68,7 @@ struct Event {
 
 struct Job {
   std::string prompt;
+  std::string model;   // "" = the default model
   int n_predict = 200;
   std::mutex mu;
   std::condition_variable cv;
@@ -103,9 +110,21 @@ double pctl(std::vector<double> v, double p) {
 }
 
 // ------------------------------------------------------------------ server state
-struct Server {
+struct ModelSlot {
+  std::string name, source;
+  Json cfg;
   std::unique_ptr<Engine> eng;
   std::unique_ptr<Session> sess;
+  double last_used = 0;
+  int restarts = 0;
+};
+
+struct Server {
+  Engine* eng = nullptr;     // the default model's engine (models[0])
+  std::vector<std::unique_ptr<ModelSlot>> models;
+  int max_models = 2;        // resident engines (the default one included)
+  std::mutex eng_mu;         // engine swaps (restart / load) vs /health and /metrics readers
+  bool ready = false;        // start-up finished (later logs are not replayed to new requests)
   bool mock = false;
   int mock_delay_ms = 2;
   int capacity = 1;
@@ -154,15 +173,94 @@ GenResult mock_run(Job& j, int delay_ms) {
   return r;
 }
 
+ModelSlot* find_model(Server& S, const std::string& name) {
+  if (name.empty()) return S.models.empty() ? nullptr : S.models[0].get();
+  for (auto& m : S.models)
+    if (m->name == name) return m.get();
+  return nullptr;
+}
+
+void load_slot(Server& S, ModelSlot& m) {
+  const bool dflt = &m == S.models[0].get();
+  {
+    std::lock_guard<std::mutex> l(S.eng_mu);
+    if (dflt) S.eng = nullptr;
+    m.sess.reset();
+    m.eng.reset();
+  }
+  std::unique_ptr<Engine> e(new Engine(m.cfg));
+  std::unique_ptr<Session> ss(new Session(*e, m.cfg.get_str("gguf", "")));
+  std::lock_guard<std::mutex> l(S.eng_mu);
+  m.eng = std::move(e);
+  m.sess = std::move(ss);
+  if (dflt) S.eng = m.eng.get();
+}
+
+// generation thread only: the slot of `name`, loaded (evicting the least recently used other
+// model when more than max_models engines would be resident)
+ModelSlot* acquire_model(Server& S, const std::string& name) {
+  ModelSlot* m = find_model(S, name);
+  if (!m) throw std::runtime_error("unknown model " + name);
+  if (!m->eng) {
+    int resident = 0;
+    for (auto& x : S.models) resident += x->eng ? 1 : 0;
+    while (resident >= S.max_models) {
+      ModelSlot* lru = nullptr;
+      for (size_t i = 1; i < S.models.size(); ++i)
+        if (S.models[i]->eng && (!lru || S.models[i]->last_used < lru->last_used)) lru = S.models[i].get();
+      if (!lru) break;
+      MP_LOGI("orchestrator: unloading model %s", lru->name.c_str());
+      std::lock_guard<std::mutex> l(S.eng_mu);
+      lru->sess.reset();
+      lru->eng.reset();
+      --resident;
+    }
+    MP_LOGI("orchestrator: loading model %s (%s)", m->name.c_str(), m->source.c_str());
+    load_slot(S, *m);
+  }
+  m->last_used = now_ms();
+  return m;
+}
+
 void generation_loop(Server& S) {
   while (!S.stop) {
     std::vector<std::shared_ptr<Job>> batch;
+    ModelSlot* slot = nullptr;
+    std::string model;
     {
       std::unique_lock<std::mutex> l(S.jobs_mu);
       S.jobs_cv.wait_for(l, std::chrono::milliseconds(200), [&] { return !S.pending.empty() || S.stop; });
-      while (!S.pending.empty() && (int)batch.size() < S.capacity) {
-        batch.push_back(S.pending.front());
-        S.pending.pop_front();
+      if (S.pending.empty()) continue;
+      model = S.pending.front()->model;
+    }
+    int cap = S.capacity;
+    if (!S.mock) {
+      try {
+        slot = acquire_model(S, model);
+        cap = slot->sess->capacity();
+      } catch (const std::exception& e) {
+        MP_LOGE("orchestrator: model %s unavailable: %s", model.c_str(), e.what());
+        std::shared_ptr<Job> j;
+        {
+          std::lock_guard<std::mutex> l(S.jobs_mu);
+          j = S.pending.front();
+          S.pending.pop_front();
+        }
+        j->push({"log", std::string("error: ") + e.what() + "\n"});
+        j->finish();
+        continue;
+      }
+    }
+    {
+      // the oldest request's model; later requests for other models keep their place in the queue
+      std::lock_guard<std::mutex> l(S.jobs_mu);
+      for (auto it = S.pending.begin(); it != S.pending.end() && (int)batch.size() < cap;) {
+        if ((*it)->model == model) {
+          batch.push_back(*it);
+          it = S.pending.erase(it);
+        } else {
+          ++it;
+        }
       }
     }
     if (batch.empty()) continue;
@@ -190,12 +288,12 @@ void generation_loop(Server& S) {
             return true;
           };
         }
-        res = S.sess->run(reqs);
+        res = slot->sess->run(reqs);
       }
       for (size_t i = 0; i < batch.size(); ++i) {
         auto& j = batch[i];
         j->result = res[i];
-        const std::string perf = Session::perf_summary(res[i], S.eng ? S.eng->load_ms() : 0.0);
+        const std::string perf = Session::perf_summary(res[i], slot ? slot->eng->load_ms() : 0.0);
         j->push({"log", perf});
         fputs(perf.c_str(), stderr);
         std::lock_guard<std::mutex> l(S.metrics.mu);
@@ -211,9 +309,24 @@ void generation_loop(Server& S) {
       }
     } catch (const std::exception& e) {
       MP_LOGE("generation failed: %s", e.what());
-      std::lock_guard<std::mutex> l(S.metrics.mu);
-      S.metrics.errors += batch.size();
+      {
+        std::lock_guard<std::mutex> l(S.metrics.mu);
+        S.metrics.errors += batch.size();
+      }
       for (auto& j : batch) j->push({"log", std::string("error: ") + e.what() + "\n"});
+      if (slot && slot->eng && !slot->eng->health().get_bool("ok", true)) {
+        // the engine is poisoned (aborted links, failed stage): rebuild it; injected faults are
+        // a one-shot test hook and are not re-armed
+        slot->cfg["fault"] = Json::object();
+        try {
+          load_slot(S, *slot);
+          slot->restarts++;
+          MP_LOGW("orchestrator: engine of model %s restarted after a fault (%d restarts)", slot->name.c_str(),
+                  slot->restarts);
+        } catch (const std::exception& e2) {
+          MP_LOGE("orchestrator: engine restart failed: %s", e2.what());
+        }
+      }
     }
     {
       std::lock_guard<std::mutex> l(S.active_mu);
@@ -358,7 +471,8 @@ void serve_static(Server& S, int fd, const Request& r) {
 }
 
 // axum Json<ChatRequest> extractor semantics (main.rs:18-21)
-bool parse_prompt_body(int fd, const Request& r, std::string* prompt, int* n_predict, int def_n) {
+bool parse_prompt_body(int fd, const Request& r, std::string* prompt, int* n_predict, int def_n,
+                       std::string* model = nullptr) {
   if (lower(r.header("content-type")).find("application/json") == std::string::npos) {
     respond_text(fd, 415, "Expected request with `Content-Type: application/json`");
     return false;
@@ -377,6 +491,7 @@ bool parse_prompt_body(int fd, const Request& r, std::string* prompt, int* n_pre
   *prompt = j["prompt"].str();
   *n_predict = j.get_int("n_predict", def_n);
   if (*n_predict < 0) *n_predict = def_n;
+  if (model) *model = j.get_str("model", "");
   return true;
 }
 
@@ -402,10 +517,21 @@ bool authorized(Server& S, int fd, const Request& r) {
   return true;
 }
 
-std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n) {
+bool known_model(Server& S, int fd, std::string* model) {
+  if (S.mock || model->empty()) return true;
+  if (ModelSlot* m = find_model(S, *model)) {
+    if (m == S.models[0].get()) model->clear();   // the default model under its own name
+    return true;
+  }
+  respond(fd, 404, "application/json", "{\"error\":\"unknown model\"}");
+  return false;
+}
+
+std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n, const std::string& model = "") {
   auto job = std::make_shared<Job>();
   job->prompt = prompt;
   job->n_predict = n;
+  job->model = model;
   {
     std::lock_guard<std::mutex> l(S.metrics.mu);
     S.metrics.requests++;
@@ -436,8 +562,9 @@ std::string chunk(const std::string& s) {
 void handle_chat(Server& S, int fd, const Request& r) {
   std::string prompt;
   int n = S.default_n;
-  if (!parse_prompt_body(fd, r, &prompt, &n, S.default_n)) return;
-  auto job = submit(S, prompt, n);
+  std::string model;
+  if (!parse_prompt_body(fd, r, &prompt, &n, S.default_n, &model) || !known_model(S, fd, &model)) return;
+  auto job = submit(S, prompt, n, model);
   std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/event-stream\r\nCache-Control: no-cache\r\n";
   h += kCors;
   h += "Transfer-Encoding: chunked\r\nConnection: close\r\n\r\n";
@@ -473,8 +600,9 @@ void handle_chat(Server& S, int fd, const Request& r) {
 void handle_completion(Server& S, int fd, const Request& r) {
   std::string prompt;
   int n = 128;   // PDF p.10: n_predict 128
-  if (!parse_prompt_body(fd, r, &prompt, &n, 128)) return;
-  auto job = submit(S, prompt, n);
+  std::string model;
+  if (!parse_prompt_body(fd, r, &prompt, &n, 128, &model) || !known_model(S, fd, &model)) return;
+  auto job = submit(S, prompt, n, model);
   {
     std::unique_lock<std::mutex> l(job->mu);
     job->cv.wait(l, [&] { return job->done; });
@@ -527,8 +655,10 @@ void handle_metrics(Server& S, int fd) {
   }
   snprintf(b, sizeof(b), "# TYPE mipipe_open_connections gauge\nmipipe_open_connections %d\n", S.connections.load());
   m += b;
+  std::unique_lock<std::mutex> el(S.eng_mu);
   if (S.eng) {
     Json h = S.eng->health();
+    el.unlock();
     m += "# TYPE mipipe_stage_items_done counter\n";
     for (auto& st : h["stages"].arr()) {
       snprintf(b, sizeof(b), "mipipe_stage_items_done{stage=\"%d\"} %lld\n", (int)st["stage"].num(),
@@ -565,10 +695,34 @@ void handle_conn(Server& S, int fd, std::string peer) {
       } else if (r.path == "/metrics" && r.method == "GET") {
         handle_metrics(S, fd);
       } else if (r.path == "/health" && r.method == "GET") {
-        Json h = S.eng ? S.eng->health() : Json::object();
-        if (!S.eng) h["ok"] = true;
+        Json h;
+        {
+          std::lock_guard<std::mutex> l(S.eng_mu);
+          h = S.eng ? S.eng->health() : Json::object();
+          if (!S.eng) h["ok"] = S.mock;
+          int restarts = 0;
+          for (auto& mm : S.models) restarts += mm->restarts;
+          h["engine_restarts"] = restarts;
+        }
         h["mock"] = S.mock;
         respond(fd, 200, "application/json", h.dump());
+      } else if (r.path == "/models" && r.method == "GET") {
+        Json arr = Json::array();
+        {
+          std::lock_guard<std::mutex> l(S.eng_mu);
+          for (auto& mm : S.models) {
+            Json e = Json::object();
+            e["id"] = mm->name;
+            e["source"] = mm->source;
+            e["loaded"] = (bool)mm->eng;
+            e["restarts"] = mm->restarts;
+            arr.push(e);
+          }
+        }
+        Json o = Json::object();
+        o["object"] = "list";
+        o["data"] = arr;
+        respond(fd, 200, "application/json", o.dump());
       } else if (r.method == "GET" || r.method == "HEAD") {
         serve_static(S, fd, r);
       } else {
@@ -585,7 +739,8 @@ void handle_conn(Server& S, int fd, std::string peer) {
 
 void usage() {
   fprintf(stderr, "usage: orchestrator (-m MODEL.gguf | --synthetic NAME | --mock) [--port 3005] [--host 0.0.0.0]\n"
-                  "                    [--static DIR] [--api-key KEY] [--rate-limit N/min] [engine flags]\n");
+                  "                    [--static DIR] [--api-key KEY] [--rate-limit N/min] [engine flags]\n"
+                  "                    [--alias NAME] [--model-alias NAME=PATH.gguf|synthetic:NAME ...] [--max-models N]\n");
   print_common_usage(stderr);
 }
 
@@ -598,6 +753,10 @@ int main(int argc, char** argv) {
   int port = 3005;   // main.rs:107
   std::string host = "0.0.0.0";
   bool mock = false;
+  std::string alias, synthetic_name = "model";
+  std::vector<std::string> aliases;
+  for (int i = 1; i + 1 < argc; ++i)
+    if (!strcmp(argv[i], "--synthetic")) synthetic_name = argv[i + 1];
   CliOptions o;
   std::vector<char*> args(argv, argv + argc);
   for (int i = 1; i < argc; ++i)
@@ -611,6 +770,9 @@ int main(int argc, char** argv) {
       else if (a == "--rate-limit") S.rate_limit = std::atoi(val().c_str());
       else if (a == "--mock") {}
       else if (a == "--mock-delay-ms") S.mock_delay_ms = std::atoi(val().c_str());
+      else if (a == "--alias") alias = val();
+      else if (a == "--model-alias") aliases.push_back(val());
+      else if (a == "--max-models") S.max_models = std::max(1, std::atoi(val().c_str()));
       else if (a == "-h" || a == "--help") { usage(); exit(0); }
       else return false;
       return true;
@@ -646,15 +808,36 @@ int main(int argc, char** argv) {
   }
   // capture start-up logs (placement / offload lines) to replay to every request's log pane
   log_set_callback([&S](const std::string& line) {
-    if (!S.eng && !S.mock) S.startup_logs.push_back(line);
+    if (!S.ready && !S.mock) S.startup_logs.push_back(line);
     else broadcast_log(line);
   });
   try {
     if (!mock) {
       if (!o.eng.has("mb_size")) o.eng["mb_size"] = 4;
-      S.eng.reset(new Engine(o.eng));
-      S.sess.reset(new Session(*S.eng, o.eng.get_str("gguf", "")));
-      S.capacity = S.sess->capacity();
+      std::unique_ptr<ModelSlot> d(new ModelSlot);
+      d->cfg = o.eng;
+      d->source = o.eng.has("gguf") ? o.eng.get_str("gguf", "") : "synthetic:" + synthetic_name;
+      d->name = !alias.empty() ? alias : d->source.substr(d->source.rfind('/') + 1);
+      S.models.push_back(std::move(d));
+      for (const std::string& a : aliases) {
+        const size_t eq = a.find('=');
+        if (eq == std::string::npos || eq == 0) throw std::runtime_error("--model-alias expects NAME=PATH");
+        std::unique_ptr<ModelSlot> m(new ModelSlot);
+        m->name = a.substr(0, eq);
+        m->source = a.substr(eq + 1);
+        m->cfg = o.eng;
+        if (m->source.rfind("synthetic:", 0) == 0) {
+          m->cfg.erase("gguf");
+          m->cfg["synthetic"] = synthetic_arch(m->source.substr(10));
+        } else {
+          m->cfg.erase("synthetic");
+          m->cfg["gguf"] = m->source;
+        }
+        S.models.push_back(std::move(m));
+      }
+      load_slot(S, *S.models[0]);
+      S.models[0]->last_used = now_ms();
+      S.capacity = S.models[0]->sess->capacity();
     } else {
       S.startup_logs.push_back("mock engine: stage 0: layers 0-5 offloaded to GPU 0 (mock)\n");
       S.capacity = 4;
@@ -663,6 +846,7 @@ int main(int argc, char** argv) {
     MP_LOGE("orchestrator: engine init failed: %s", e.what());
     return 1;
   }
+  S.ready = true;
   int ls = socket(AF_INET, SOCK_STREAM, 0);
   int one = 1;
   setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));

@@ -224,3 +224,68 @@ def test_cli_speculative_lookup_same_text(native_bins, tiny_gguf):
     assert a.returncode == 0 and b.returncode == 0, b.stderr.decode(errors="replace")
     assert a.stdout == b.stdout and len(a.stdout) > len(prompt)
     assert b"speculative lookup" in b.stderr
+
+
+def test_multi_model_registry(native_bins, model_dir, tiny_gguf):
+    """--model-alias: requests pick a model by name (PDF p.7 multi-model management); at most
+    --max-models engines stay resident; unknown names are 404."""
+    other, _ = make_model(model_dir, "tiny-gqa", "Q8_0", seed=5)
+    prompt = "abc"
+    def cli(path):
+        p = subprocess.run([os.path.join(BIN, "mi-cli"), "-m", path, "-p", prompt, "-n", "8", "-c", "128",
+                            "-ngl", "0"], capture_output=True, timeout=120)
+        assert p.returncode == 0
+        return p.stdout.decode(errors="replace")[len(prompt):].rstrip("\n")
+    want_a, want_b = cli(tiny_gguf), cli(other)
+    s = Orchestrator("-m", tiny_gguf, "--alias", "a", "--model-alias", "b=" + other,
+                     "--model-alias", "c=synthetic:stories15m", "--max-models", "2", "-ngl", "0", "-n", "8", "-c", "128")
+    try:
+        m = httpx.get(s.url + "/models", timeout=30).json()
+        assert [e["id"] for e in m["data"]] == ["a", "b", "c"]
+        assert [e["loaded"] for e in m["data"]] == [True, False, False]
+        post = lambda body: httpx.post(s.url + "/completion", json=body, timeout=120)
+        ra = post({"prompt": prompt, "n_predict": 8}).json()
+        rb = post({"prompt": prompt, "n_predict": 8, "model": "b"}).json()
+        ra2 = post({"prompt": prompt, "n_predict": 8, "model": "a"}).json()
+        clean = lambda t: t.replace("\ufffd", "")   # invalid UTF-8 bytes are U+FFFD on both sides
+        assert clean(ra["content"]) == clean(want_a)
+        assert clean(rb["content"]) == clean(want_b)
+        assert ra2["content"] == ra["content"]
+        rc = post({"prompt": prompt, "n_predict": 4, "model": "c"}).json()
+        assert rc["tokens_predicted"] >= 1
+        m = httpx.get(s.url + "/models", timeout=30).json()
+        loaded = {e["id"]: e["loaded"] for e in m["data"]}
+        assert loaded["a"] and loaded["c"] and not loaded["b"]   # b was the least recently used
+        assert post({"prompt": prompt, "model": "nope"}).status_code == 404
+    finally:
+        s.close()
+
+
+def test_engine_restart_after_fault(native_bins, tiny_gguf):
+    """A stage fault fails the request in flight; the orchestrator rebuilds the engine and the next
+    request succeeds (design report worker auto-restart)."""
+    env_fault = json.dumps({"stage": 0, "fail_at": 2})
+    port = free_port()
+    proc = subprocess.Popen([os.path.join(BIN, "orchestrator"), "--host", "127.0.0.1", "--port", str(port),
+                             "-m", tiny_gguf, "-ngl", "0", "-n", "8", "-c", "128"],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                            env={**os.environ, "MIPIPE_FAULT": env_fault})
+    url = f"http://127.0.0.1:{port}"
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                httpx.get(url + "/health", timeout=1)
+                break
+            except Exception:
+                time.sleep(0.2)
+        with httpx.stream("POST", url + "/chat", json={"prompt": "abc"}, timeout=120) as r:
+            ev, _ = sse_events(r)
+        assert any("injected fault" in e["content"] for e in ev if e["msg_type"] == "log")
+        h = httpx.get(url + "/health", timeout=30).json()
+        assert h["ok"] and h["engine_restarts"] == 1
+        ok = httpx.post(url + "/completion", json={"prompt": "abc", "n_predict": 6}, timeout=120).json()
+        assert ok["tokens_predicted"] >= 1 and ok["stop_reason"] in ("length", "eog")
+    finally:
+        proc.terminate()
+        proc.wait(timeout=30)
