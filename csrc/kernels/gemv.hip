@@ -209,23 +209,31 @@ static void launch_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st)
 // Tiles per wave: with M > 4 the x fragments (16 rows x 32 k per MFMA) cost more L1/L2 traffic
 // than the weights themselves (3.5x at M = 16); sharing them across tiles pays.  Measured on
 // MI355X (tools/gemv_bench.py, 70B shapes): M = 16 gate/up 115 -> 67 us with 4 tiles per wave.
-void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, hipStream_t st);
+void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, int tw, hipStream_t st);
 
 // kernel version (MIPIPE_GEMV_V: 1 = per-wave x loads, 2 = workgroup-shared x in LDS, default 2)
-// and waves per workgroup of v2 (MIPIPE_GEMV_NW: 4 or 8)
-static int g_ver = -1, g_nw = 8;
+// and waves per workgroup of v2 (MIPIPE_GEMV_NW: 4 or 8), tiles per wave of v2 at M > 32
+// (MIPIPE_GEMV2_TW: 1 or 2; 0 = auto: 2 for the gate/up SwiGLU GEMV only).  Measured on MI355X
+// (profiles/r1g_gemv_tiles_per_wave_ab.txt, 70B Q4_K, M = 64): gate/up 115.9 -> 104.3 us with two
+// tiles per wave; the split-K projections (qkv, o, down) gain nothing at their best split.
+static int g_ver = -1, g_nw = 8, g_tw2 = 0;
+static int gemv2_tw(int M, int epi) {
+  if (M <= 32) return 1;
+  if (g_tw2) return g_tw2;
+  return epi == EPI_SWIGLU ? 2 : 1;
+}
 static int gemv_version() {
   if (g_ver < 0) {
     const char* e = getenv("MIPIPE_GEMV_V");
     g_ver = e ? atoi(e) : 2;
     if (const char* w = getenv("MIPIPE_GEMV_NW")) g_nw = atoi(w) == 4 ? 4 : 8;
+    if (const char* w = getenv("MIPIPE_GEMV2_TW")) g_tw2 = atoi(w) == 2 ? 2 : atoi(w) == 1 ? 1 : 0;
   }
   return g_ver;
 }
 
 int gemv_tiles_per_wave(int M, int epi) {
-  (void)epi;
-  if (gemv_version() == 2) return 1;   // v2: one tile per wave, x shared through LDS
+  if (gemv_version() == 2) return gemv2_tw(M, epi);   // v2: x shared through LDS
   if (g_tpw) return g_tpw;
   return M <= 4 ? 1 : 4;
 }
@@ -257,7 +265,7 @@ void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   if (nsplit < 1) nsplit = 1;
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
-  if (gemv_version() == 2 && epi < 3 && p.M <= 64) return launch_gemv2(ptype, epi, p, nsplit, g_nw, st);
+  if (gemv_version() == 2 && epi < 3 && p.M <= 64) return launch_gemv2(ptype, epi, p, nsplit, g_nw, gemv2_tw(p.M, epi), st);
   switch (ptype) {
     case P_Q4_K: launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
     case P_Q5_K: launch_pt<P_Q5_K>(epi, p, nsplit, st); break;
