@@ -350,6 +350,19 @@ const char* mp_engine_health(void* h) {
   return g_str.c_str();
   API_CATCH(nullptr)
 }
+// checkpoint / resume (Engine::save_state / load_state); returns a JSON summary
+const char* mp_engine_save_state(void* h, const char* dir) {
+  API_TRY
+  g_str = static_cast<Engine*>(h)->save_state(dir).dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+const char* mp_engine_load_state(void* h, const char* dir) {
+  API_TRY
+  g_str = static_cast<Engine*>(h)->load_state(dir).dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
 int mp_engine_trace(void* h, int on, const char* path) {
   API_TRY
   Engine* e = static_cast<Engine*>(h);

@@ -400,6 +400,32 @@ int CpuStage::sample_row(const float* lg, uint64_t salt, int row) {
   return v[keep - 1].second;
 }
 
+// KV of one slot: per layer, K rows then V rows [n_tok][kv_dim] f32 (contiguous in kc_/vc_)
+size_t CpuStage::kv_state_bytes(int n_tok) const {
+  return kc_.size() * 2 * (size_t)n_tok * cfg_.kv_dim() * 4;
+}
+
+void CpuStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
+  const size_t row = (size_t)cfg_.kv_dim(), n = (size_t)n_tok * row * 4;
+  const size_t off = (size_t)slot * opt_.max_ctx * row;
+  for (size_t li = 0; li < kc_.size(); ++li)
+    for (const auto* c : {&kc_[li], &vc_[li]}) {
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(c->data() + off);
+      out.insert(out.end(), p, p + n);
+    }
+}
+
+void CpuStage::kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) {
+  if (bytes != kv_state_bytes(n_tok)) throw std::runtime_error("kv_import: size mismatch");
+  const size_t row = (size_t)cfg_.kv_dim(), n = (size_t)n_tok * row * 4;
+  const size_t off = (size_t)slot * opt_.max_ctx * row;
+  for (size_t li = 0; li < kc_.size(); ++li)
+    for (auto* c : {&kc_[li], &vc_[li]}) {
+      std::memcpy(c->data() + off, data, n);
+      data += n;
+    }
+}
+
 void CpuStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) {
   const int B = opt_.mb_size;
   if (hist_.empty()) hist_.resize((size_t)opt_.n_mb * B);

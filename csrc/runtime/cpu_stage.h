@@ -64,6 +64,12 @@ class CpuStage : public Stage {
   void ffn(const Layer& L, int M, const float* xn, float* x);
   void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt);
   void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) override;
+  void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) override;
+  void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) override;
+  size_t kv_state_bytes(int n_tok) const override;
+  uint64_t sample_step() override { return step_; }
+  void set_sample_step(uint64_t s) override { step_ = s; }
+  const char* backend_name() const override { return "cpu"; }
   int sample_row(const float* logits, uint64_t salt, int row);
   CpuMat own_random(int type, int64_t N, int64_t K, uint64_t seed);
 

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <fstream>
+#include <sys/stat.h>
 #include <numeric>
 #include <stdexcept>
 
@@ -646,6 +648,7 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   prompts_ = prompts;
   gen_.assign(prompts.size(), {});
   rounds_done_ = 0;
+  resumable_ = true;
   std::vector<Item> items;
   for (auto& w : workers_) {
     Stage& st = *w->stage;
@@ -707,6 +710,176 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   started_ = true;
   if (owns_last())
     for (size_t i = 0; i < prompts.size(); ++i) gen_[i].push_back(out_host_[i]);
+}
+
+// ---------------------------------------------------------------- checkpoint / resume
+static Json state_fingerprint(const ModelConfig& c, int S, int M, int B, int max_ctx) {
+  Json f = Json::object();
+  f["n_layer"] = c.n_layer; f["d_model"] = c.d_model; f["n_head"] = c.n_head; f["n_head_kv"] = c.n_head_kv;
+  f["d_ff"] = c.d_ff; f["vocab"] = c.vocab; f["n_stages"] = S; f["n_mb"] = M; f["mb_size"] = B;
+  f["max_ctx"] = max_ctx;
+  return f;
+}
+
+Json Engine::save_state(const std::string& dir) {
+  if (!started_) throw std::runtime_error("save_state before start");
+  if (failed_) throw std::runtime_error("save_state after a pipeline fault");
+  if (!resumable_) throw std::runtime_error("save_state: not supported after speculative decoding");
+  ::mkdir(dir.c_str(), 0755);
+  sync_all();
+  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_);
+  // tokens already in each slot's KV: prompt + generated - 1 (the newest token is the next input)
+  std::vector<int> n_tok((size_t)M_ * B_, 0);
+  for (size_t i = 0; i < prompts_.size(); ++i) n_tok[i] = (int)prompts_[i].size() + rounds_done_;
+  size_t total = 0;
+  for (auto& wp : workers_) {
+    Stage& st = *wp->stage;
+    if (!cpu_) HIP_OK(hipSetDevice(wp->device));
+    Json h = Json::object();
+    h["magic"] = "mipipe-stage-state"; h["version"] = 1; h["fingerprint"] = fp;
+    h["stage"] = st.spec().stage; h["layer_begin"] = st.spec().layer_begin; h["layer_end"] = st.spec().layer_end;
+    h["backend"] = st.backend_name(); h["sample_step"] = (double)st.sample_step();
+    Json lens = Json::array();
+    for (int v : n_tok) lens.push(v);
+    h["n_tok"] = lens;
+    if (st.spec().first()) {   // current decode input of every row (received over the ring for S > 1)
+      Json toks = Json::array();
+      std::vector<int32_t> t(B_);
+      for (int mb = 0; mb < M_; ++mb) {
+        if (cpu_) std::memcpy(t.data(), st.tokens(mb), (size_t)B_ * 4);
+        else HIP_OK(hipMemcpy(t.data(), st.tokens(mb), (size_t)B_ * 4, hipMemcpyDeviceToHost));
+        for (int b = 0; b < B_; ++b) toks.push(t[b]);
+      }
+      h["tokens"] = toks;
+    }
+    std::vector<uint8_t> kv;
+    for (size_t i = 0; i < n_tok.size(); ++i)
+      if (n_tok[i] > 0) st.kv_export((int)i, n_tok[i], kv);
+    h["kv_bytes"] = (double)kv.size();
+    const std::string path = dir + "/stage" + std::to_string(st.spec().stage) + ".bin";
+    std::ofstream f(path, std::ios::binary | std::ios::trunc);
+    const std::string hs = h.dump() + "\n";
+    f.write(hs.data(), (std::streamsize)hs.size());
+    f.write(reinterpret_cast<const char*>(kv.data()), (std::streamsize)kv.size());
+    if (!f) throw std::runtime_error("save_state: cannot write " + path);
+    total += hs.size() + kv.size();
+  }
+  if (owns_last()) {
+    Json sj = Json::object();
+    sj["magic"] = "mipipe-session"; sj["version"] = 1; sj["fingerprint"] = fp; sj["rounds_done"] = rounds_done_;
+    Json ps = Json::array(), gs = Json::array();
+    for (size_t i = 0; i < prompts_.size(); ++i) {
+      Json p = Json::array(), g = Json::array();
+      for (int32_t t : prompts_[i]) p.push(t);
+      for (int32_t t : gen_[i]) g.push(t);
+      ps.push(p);
+      gs.push(g);
+    }
+    sj["prompts"] = ps;
+    sj["generated"] = gs;
+    std::ofstream f(dir + "/session.json", std::ios::trunc);
+    f << sj.dump() << "\n";
+    if (!f) throw std::runtime_error("save_state: cannot write session.json");
+  }
+  MP_LOGI("state saved to %s: %zu sequences, %d rounds, %.1f MiB", dir.c_str(), prompts_.size(), rounds_done_,
+          total / 1048576.0);
+  Json r = Json::object();
+  r["bytes"] = (double)total; r["rounds_done"] = rounds_done_; r["sequences"] = (int)prompts_.size();
+  return r;
+}
+
+Json Engine::load_state(const std::string& dir) {
+  auto slurp = [](const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("load_state: cannot read " + path);
+    return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  };
+  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_);
+  const Json sj = Json::parse(slurp(dir + "/session.json"));
+  if (sj.get_str("magic", "") != "mipipe-session" || sj["fingerprint"].dump() != fp.dump())
+    throw std::runtime_error("load_state: session was saved by a different model / pipeline shape");
+  prompts_.clear();
+  gen_.clear();
+  for (const Json& p : sj["prompts"].arr()) {
+    std::vector<int32_t> v;
+    for (const Json& t : p.arr()) v.push_back((int32_t)t.num());
+    prompts_.push_back(v);
+  }
+  for (const Json& g : sj["generated"].arr()) {
+    std::vector<int32_t> v;
+    for (const Json& t : g.arr()) v.push_back((int32_t)t.num());
+    gen_.push_back(v);
+  }
+  rounds_done_ = sj.get_int("rounds_done", 0);
+  if ((int)prompts_.size() > M_ * B_ || gen_.size() != prompts_.size()) throw std::runtime_error("load_state: bad session");
+  for (auto& wp : workers_) {
+    Stage& st = *wp->stage;
+    if (!cpu_) HIP_OK(hipSetDevice(wp->device));
+    const std::string path = dir + "/stage" + std::to_string(st.spec().stage) + ".bin";
+    const std::string raw = slurp(path);
+    const size_t nl = raw.find('\n');
+    if (nl == std::string::npos) throw std::runtime_error("load_state: bad stage file " + path);
+    const Json h = Json::parse(raw.substr(0, nl));
+    if (h.get_str("magic", "") != "mipipe-stage-state" || h["fingerprint"].dump() != fp.dump() ||
+        h.get_int("layer_begin", -1) != st.spec().layer_begin || h.get_int("layer_end", -1) != st.spec().layer_end ||
+        h.get_str("backend", "") != st.backend_name())
+      throw std::runtime_error("load_state: " + path + " does not match this stage (layers / backend / shape)");
+    const uint8_t* kv = reinterpret_cast<const uint8_t*>(raw.data()) + nl + 1;
+    const uint8_t* end = reinterpret_cast<const uint8_t*>(raw.data()) + raw.size();
+    const auto& lens = h["n_tok"].arr();
+    for (size_t i = 0; i < lens.size(); ++i) {
+      const int n = (int)lens[i].num();
+      if (n <= 0) continue;
+      if (n >= max_ctx_) throw std::runtime_error("load_state: sequence longer than max_ctx");
+      const size_t nb = st.kv_state_bytes(n);
+      if (kv + nb > end) throw std::runtime_error("load_state: truncated " + path);
+      st.kv_import((int)i, n, kv, nb);
+      kv += nb;
+    }
+    st.set_sample_step((uint64_t)h.get_num("sample_step", 0));
+    for (int mb = 0; mb < M_; ++mb) {   // next decode position: prompt + rounds (idle rows advance too)
+      std::vector<int32_t> pos(B_, rounds_done_);
+      for (int b = 0; b < B_; ++b) {
+        const size_t i = (size_t)mb * B_ + b;
+        if (i < prompts_.size()) pos[b] += (int)prompts_[i].size();
+      }
+      st.set_positions(mb, pos);
+    }
+    if (st.spec().first()) {
+      const auto& toks = h["tokens"].arr();
+      if ((int)toks.size() != M_ * B_) throw std::runtime_error("load_state: missing first-stage tokens");
+      std::vector<int32_t> t(B_);
+      for (int mb = 0; mb < M_; ++mb) {
+        for (int b = 0; b < B_; ++b) t[b] = (int32_t)toks[(size_t)mb * B_ + b].num();
+        if (cpu_) std::memcpy(st.tokens(mb), t.data(), (size_t)B_ * 4);
+        else HIP_OK(hipMemcpy(st.tokens(mb), t.data(), (size_t)B_ * 4, hipMemcpyHostToDevice));
+      }
+      for (size_t i = 0; i < prompts_.size(); ++i) {
+        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
+        else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4,
+                              hipMemcpyHostToDevice));
+      }
+      if (cpu_) std::fill(wp->ring_pending.begin(), wp->ring_pending.end(), false);
+    }
+    if (st.spec().last()) {   // penalty windows: prompt + accepted tokens
+      for (int mb = 0; mb < M_; ++mb) {
+        std::vector<std::vector<int32_t>> seqs;
+        for (int b = 0; b < B_ && (size_t)mb * B_ + b < prompts_.size(); ++b) {
+          const size_t i = (size_t)mb * B_ + b;
+          std::vector<int32_t> q = prompts_[i];
+          q.insert(q.end(), gen_[i].begin(), gen_[i].end());
+          seqs.push_back(q);
+        }
+        st.set_history(mb, seqs);
+      }
+    }
+  }
+  started_ = true;
+  resumable_ = true;
+  MP_LOGI("state loaded from %s: %zu sequences, %d rounds", dir.c_str(), prompts_.size(), rounds_done_);
+  Json r = Json::object();
+  r["rounds_done"] = rounds_done_; r["sequences"] = (int)prompts_.size();
+  return r;
 }
 
 StepStats Engine::decode_steps(int k) {
@@ -825,6 +998,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
   }
   const double t0 = now_ms();
   start(prompts);
+  resumable_ = false;   // sequences advance by different amounts: positions are not prompt + rounds
   const double t1 = now_ms();
   const size_t n = prompts.size();
   if (on_token)

@@ -79,6 +79,14 @@ class Engine {
   void write_trace(const std::string& path) const;
   // heartbeat counters + link byte counters per owned stage; "ok" false after a fault
   Json health() const;
+  // Checkpoint / resume of a running generation: between decode_steps calls,
+  // write every owned stage's KV shard (only the used positions of each sequence), its current
+  // input tokens and sampler step to <dir>/stage<k>.bin, and the sequences (prompts, generated
+  // tokens, rounds done) to <dir>/session.json (by the owner of the last stage).  load_state on an
+  // engine built with the same model / partition / micro-batch shape continues the generation
+  // exactly where it stopped (greedy and seeded sampling alike).
+  Json save_state(const std::string& dir);
+  Json load_state(const std::string& dir);
 
   // streaming hook: called on the host (from the worker of the last stage) after each round
   // with (sequence index, token) pairs
@@ -140,6 +148,7 @@ class Engine {
   Json fault_;
   int rounds_cap_ = 0, rounds_done_ = 0;
   bool started_ = false;
+  bool resumable_ = true;   // false after spec_generate (per-sequence positions)
   double load_ms_ = 0;
 };
 

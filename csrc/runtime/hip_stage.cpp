@@ -417,6 +417,56 @@ void HipStage::set_positions(int mb, const std::vector<int32_t>& pos) {
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
+// KV of one slot: its pages are contiguous (identity block table: slot s owns pages
+// [s * max_pages, (s + 1) * max_pages)), page = [Hkv][64][Dp] f16; per layer the first
+// ceil(n_tok / 64) pages of K, then of V
+size_t HipStage::kv_state_bytes(int n_tok) const {
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  return kc_.size() * 2 * (size_t)((n_tok + 63) / 64) * page;
+}
+
+void HipStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
+  HIP_OK(hipSetDevice(spec_.device));
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2, n = (size_t)((n_tok + 63) / 64) * page;
+  const size_t off = (size_t)slot * max_pages_ * page;
+  const size_t base = out.size();
+  out.resize(base + kv_state_bytes(n_tok));
+  uint8_t* dst = out.data() + base;
+  HIP_OK(hipStreamSynchronize(stream_));
+  for (size_t li = 0; li < kc_.size(); ++li)
+    for (f16* c : {kc_[li], vc_[li]}) {
+      HIP_OK(hipMemcpy(dst, reinterpret_cast<const uint8_t*>(c) + off, n, hipMemcpyDeviceToHost));
+      dst += n;
+    }
+}
+
+void HipStage::kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) {
+  if (bytes != kv_state_bytes(n_tok)) throw std::runtime_error("kv_import: size mismatch");
+  HIP_OK(hipSetDevice(spec_.device));
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2, n = (size_t)((n_tok + 63) / 64) * page;
+  const size_t off = (size_t)slot * max_pages_ * page;
+  HIP_OK(hipStreamSynchronize(stream_));
+  for (size_t li = 0; li < kc_.size(); ++li)
+    for (f16* c : {kc_[li], vc_[li]}) {
+      HIP_OK(hipMemcpy(reinterpret_cast<uint8_t*>(c) + off, data, n, hipMemcpyHostToDevice));
+      data += n;
+    }
+}
+
+uint64_t HipStage::sample_step() {
+  HIP_OK(hipSetDevice(spec_.device));
+  HIP_OK(hipStreamSynchronize(stream_));
+  int32_t v = 0;
+  HIP_OK(hipMemcpy(&v, step_, 4, hipMemcpyDeviceToHost));
+  return (uint64_t)(uint32_t)v;
+}
+
+void HipStage::set_sample_step(uint64_t s) {
+  HIP_OK(hipSetDevice(spec_.device));
+  const int32_t v = (int32_t)s;
+  HIP_OK(hipMemcpy(step_, &v, 4, hipMemcpyHostToDevice));
+}
+
 void HipStage::set_sampling(float temp, int top_k, float top_p, float min_p, uint64_t seed) {
   const bool changed = temp != temp_ || top_k != top_k_ || top_p != top_p_ || min_p != min_p_ || seed != seed_;
   Stage::set_sampling(temp, top_k, top_p, min_p, seed);

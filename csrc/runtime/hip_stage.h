@@ -106,6 +106,12 @@ class HipStage : public Stage {
 
   size_t weight_bytes() const override { return weight_bytes_; }
   size_t kv_bytes() const override { return kv_bytes_; }
+  void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) override;
+  void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) override;
+  size_t kv_state_bytes(int n_tok) const override;
+  uint64_t sample_step() override;
+  void set_sample_step(uint64_t s) override;
+  const char* backend_name() const override { return "hip"; }
   const float* logits_ptr() const override { return logits_; }
   int logits_ld() const override { return logits_ld_; }
 

@@ -9,30 +9,27 @@
 
 namespace mp {
 
-namespace {
-double now_ms() {
+double session_now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-// complete-UTF-8 emitter per sequence
-struct Utf8Acc {
-  std::string buf;
-  std::string push(const std::string& b) {
-    buf += b;
-    size_t cut = buf.size();
-    for (size_t k = 1; k <= 4 && k <= buf.size(); ++k) {
-      const unsigned char c = (unsigned char)buf[buf.size() - k];
-      if ((c & 0xC0) == 0x80) continue;
-      const int need = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 1;
-      if (need > (int)k) cut = buf.size() - k;
-      break;
-    }
-    std::string o = buf.substr(0, cut);
-    buf.erase(0, cut);
-    return o;
-  }
-};
+namespace {
+double now_ms() { return session_now_ms(); }
 }  // namespace
+
+std::string Utf8Acc::push(const std::string& b) {
+  buf += b;
+  size_t cut = buf.size();
+  for (size_t k = 1; k <= 4 && k <= buf.size(); ++k) {
+    const unsigned char c = (unsigned char)buf[buf.size() - k];
+    if ((c & 0xC0) == 0x80) continue;
+    const int need = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : c >= 0xC0 ? 2 : 1;
+    if (need > (int)k) cut = buf.size() - k;
+    break;
+  }
+  std::string o = buf.substr(0, cut);
+  buf.erase(0, cut);
+  return o;
+}
 
 Session::Session(Engine& eng, const std::string& gguf_path) : eng_(eng) {
   if (!gguf_path.empty()) {

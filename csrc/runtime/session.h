@@ -13,6 +13,13 @@
 
 namespace mp {
 
+// complete-UTF-8 emitter: push() returns the bytes up to the last whole character, keeps the rest
+struct Utf8Acc {
+  std::string buf;
+  std::string push(const std::string& b);
+};
+double session_now_ms();
+
 struct GenRequest {
   std::string prompt;
   int n_predict = 200;

@@ -84,6 +84,19 @@ class Stage {
   // last stage: seed the penalty window of micro-batch mb (row b <- seqs[b], its last tokens)
   virtual void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) { (void)mb; (void)seqs; }
 
+  // Checkpoint / resume (the reference has none beyond re-reading the GGUF):
+  // the KV of sequence slot `slot` (= mb * mb_size + row) for positions [0, n_tok) of every layer
+  // of this stage as opaque bytes in the backend's own layout (HIP: bf16-class f16 pages, CPU:
+  // f32 rows), appended to `out`; kv_import writes the same bytes back.  Called with the stage
+  // idle (between decode_steps calls).
+  virtual void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) = 0;
+  virtual void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) = 0;
+  virtual size_t kv_state_bytes(int n_tok) const = 0;   // bytes kv_export appends for n_tok
+  // sampling step counter (seeds the per-row RNG streams of the sampler)
+  virtual uint64_t sample_step() = 0;
+  virtual void set_sample_step(uint64_t s) = 0;
+  virtual const char* backend_name() const = 0;
+
  protected:
   float temp_ = 0.f, top_p_ = 1.f, min_p_ = 0.f;
   int top_k_ = 0;

@@ -25,7 +25,9 @@ static void usage() {
           "mi-cli:\n"
           "  --bench [--bench-prompt L --bench-warmup W --bench-steps K]   decode throughput of full batches\n"
           "  --daemon                  read {\"prompt\":..,\"n_predict\":..} lines on stdin, answer with JSON lines\n"
-          "  --no-display-prompt       do not echo the prompt\n");
+          "  --no-display-prompt       do not echo the prompt\n"
+          "  --state-save DIR          after generating, checkpoint the KV shards + sequences to DIR\n"
+          "  --state-load DIR          resume a checkpoint: continue its sequence for -n more tokens\n");
 }
 
 static int run_daemon(Session& s) {
@@ -69,10 +71,13 @@ static int run_daemon(Session& s) {
 
 int main(int argc, char** argv) {
   bool daemon = false;
+  std::string state_save, state_load;
   CliOptions o;
   try {
-    o = parse_cli(argc, argv, [&](const std::string& a, const std::function<std::string()>&) {
+    o = parse_cli(argc, argv, [&](const std::string& a, const std::function<std::string()>& val) {
       if (a == "--daemon") { daemon = true; return true; }
+      if (a == "--state-save") { state_save = val(); return true; }
+      if (a == "--state-load") { state_load = val(); return true; }
       if (a == "-h" || a == "--help") { usage(); exit(0); }
       return false;
     });
@@ -98,6 +103,29 @@ int main(int argc, char** argv) {
     }
     Session s(eng, o.eng.get_str("gguf", ""));
     if (daemon) return run_daemon(s);
+    if (!state_load.empty()) {
+      // resume: continue sequence 0 of the checkpoint token by token
+      eng.load_state(state_load);
+      const bool solo = eng.owns_first() && eng.owns_last();
+      Utf8Acc acc;
+      int n = 0;
+      const double t0 = session_now_ms();
+      for (; n < o.n_predict; ++n) {
+        eng.decode_steps(1);
+        if (!eng.owns_last()) continue;
+        const int32_t t = eng.tokens()[0].back();
+        if (s.is_eog(t) && solo) break;
+        const std::string p = acc.push(s.piece(t));
+        fwrite(p.data(), 1, p.size(), stdout);
+        fflush(stdout);
+      }
+      if (eng.owns_last()) {
+        fputs((acc.buf + "\n").c_str(), stdout);
+        MP_LOGI("resumed %s: %d tokens in %.1f ms", state_load.c_str(), n, session_now_ms() - t0);
+      }
+      if (!state_save.empty()) eng.save_state(state_save);
+      return 0;
+    }
     if (o.echo_prompt && eng.owns_last()) {
       fputs(o.prompt.c_str(), stdout);
       fflush(stdout);
@@ -116,6 +144,7 @@ int main(int argc, char** argv) {
       fflush(stdout);
       MP_LOGI("\n%s", Session::perf_summary(r, eng.load_ms()).c_str());
     }
+    if (!state_save.empty()) eng.save_state(state_save);
     if (!o.trace.empty()) eng.write_trace(o.trace);
   } catch (const std::exception& e) {
     MP_LOGE("mi-cli: error: %s", e.what());

@@ -90,6 +90,18 @@ class Engine:
         """Per-stage heartbeat (items done), link byte counters, ok=False after a pipeline fault."""
         return N.jcall(N.lib().mp_engine_health, self._h, what="engine health")
 
+    def save_state(self, path: str) -> dict:
+        """Checkpoint a running generation: every owned stage's KV shard (used positions only),
+        decode inputs and sampler step under `path`/, plus the sequences in session.json."""
+        return N.jcall(N.lib().mp_engine_save_state, self._h, N.cstr(path), what="save_state")
+
+    def load_state(self, path: str) -> dict:
+        """Resume a generation saved by save_state (same model, partition and micro-batch shape);
+        decode() then continues exactly where the saved engine stopped."""
+        r = N.jcall(N.lib().mp_engine_load_state, self._h, N.cstr(path), what="load_state")
+        self._n_seq = r["sequences"]
+        return r
+
     def trace(self, on: bool = True):
         N.check(N.lib().mp_engine_trace(self._h, int(on), None), "trace")
 

@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out; mkdir -p $O; cd $R
 step() { echo "== $1"; }
 step tests
-timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 grep -E "passed|failed|FAILED|Error" $O/tests.log | tail -12
 [ $rc -gt 1 ] && exit $rc
 step bench70b

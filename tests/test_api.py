@@ -289,3 +289,17 @@ def test_engine_restart_after_fault(native_bins, tiny_gguf):
     finally:
         proc.terminate()
         proc.wait(timeout=30)
+
+
+def test_cli_state_save_and_resume(native_bins, tiny_gguf, tmp_path):
+    """mi-cli --state-save after 10 tokens, then --state-load -n 6 prints exactly the last 6 tokens
+    of an uninterrupted 16-token run (checkpoint/resume)."""
+    prompt = "The pipeline sends activations"
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-p", prompt, "-c", "256", "-ngl", "0", "--stages", "2"]
+    full = subprocess.run(base + ["-n", "16"], capture_output=True, timeout=120)
+    a = subprocess.run(base + ["-n", "10", "--state-save", str(tmp_path / "st")], capture_output=True, timeout=120)
+    b = subprocess.run(base + ["-n", "6", "--state-load", str(tmp_path / "st")], capture_output=True, timeout=120)
+    for r in (full, a, b):
+        assert r.returncode == 0, r.stderr.decode(errors="replace")
+    assert b"state saved" in a.stderr and b"resumed" in b.stderr
+    assert full.stdout == a.stdout.rstrip(b"\n") + b.stdout

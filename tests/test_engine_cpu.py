@@ -264,3 +264,44 @@ def test_cpu_speculative_rejects_sampling(native, model_dir):
     with Engine(gguf=path, backend="cpu", max_ctx=64, temp=0.8) as eng:
         with pytest.raises(RuntimeError, match="greedy"):
             eng.spec_generate([[5, 6, 7]], 4)
+
+
+@pytest.mark.parametrize("stages,n_mb,sampling", [(1, 1, False), (2, 2, False), (3, 3, True)])
+def test_cpu_checkpoint_resume(native, model_dir, tmp_path, stages, n_mb, sampling):
+    """save_state between decode rounds, load into a fresh engine: the resumed generation equals
+    the uninterrupted one token for token (greedy, and seeded sampling with penalties)."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(3)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 70, 3, 17, 5, 2)[: 2 * n_mb]]
+    kw = dict(gguf=path, backend="cpu", max_ctx=128, n_mb=n_mb, mb_size=2, prefill_chunk=16, stages=stages,
+              split="even")
+    if sampling:
+        kw.update(temp=1.2, top_k=30, top_p=0.95, seed=11, repeat_penalty=1.3, repeat_last_n=16)
+    with Engine(**kw) as eng:
+        eng.start(prompts)
+        eng.decode(3)
+        r = eng.save_state(str(tmp_path / "st"))
+        assert r["rounds_done"] == 3 and r["sequences"] == len(prompts)
+        eng.decode(6)
+        full = eng.tokens()
+    assert (tmp_path / "st" / "session.json").exists()
+    assert all((tmp_path / "st" / f"stage{k}.bin").exists() for k in range(stages))
+    with Engine(**kw) as eng:
+        eng.load_state(str(tmp_path / "st"))
+        assert eng.tokens() == [t[:4] for t in full]
+        eng.decode(6)
+        resumed = eng.tokens()
+    assert resumed == full
+
+
+def test_cpu_checkpoint_rejects_other_shape(native, model_dir, tmp_path):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=64, mb_size=2) as eng:
+        eng.start([[5, 6, 7], [8, 9]])
+        eng.decode(2)
+        eng.save_state(str(tmp_path / "st"))
+    with Engine(gguf=path, backend="cpu", max_ctx=64, mb_size=1, n_mb=2) as eng:
+        with pytest.raises(RuntimeError):
+            eng.load_state(str(tmp_path / "st"))

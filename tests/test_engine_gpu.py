@@ -272,3 +272,28 @@ def test_speculative_lookup_matches_greedy(cuda, native, model_dir, stages, n_mb
     assert out == ref
     assert again[0] == ref[0][:6]
     assert st["drafted"] >= st["accepted"] >= 0
+
+
+@pytest.mark.parametrize("stages,sampling", [(1, False), (2, True)])
+def test_checkpoint_resume(cuda, native, model_dir, tmp_path, stages, sampling):
+    """HIP stages: KV pages, ring tokens and sampler step survive save_state / load_state; the
+    resumed engine (graphs re-captured) continues the generation token for token."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    rng = np.random.default_rng(4)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 70, 3, 17)]
+    kw = dict(gguf=path, max_ctx=256, n_mb=2, mb_size=2, prefill_chunk=16, stages=stages,
+              devices=[0] * stages, link="local", split="even")
+    if sampling:
+        kw.update(temp=1.1, top_k=40, seed=5, repeat_penalty=1.2, repeat_last_n=16)
+    with Engine(**kw) as eng:
+        eng.start(prompts)
+        eng.decode(5)
+        eng.save_state(str(tmp_path / "st"))
+        eng.decode(7)
+        full = eng.tokens()
+    with Engine(**kw) as eng:
+        eng.load_state(str(tmp_path / "st"))
+        eng.decode(7)
+        resumed = eng.tokens()
+    assert resumed == full
