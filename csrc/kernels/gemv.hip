@@ -217,10 +217,12 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
 // (profiles/r1g_gemv_tiles_per_wave_ab.txt, 70B Q4_K, M = 64): gate/up 115.9 -> 104.3 us with two
 // tiles per wave; the split-K projections (qkv, o, down) gain nothing at their best split.
 static int g_ver = -1, g_nw = 8, g_tw2 = 0;
-static int gemv2_tw(int M, int epi) {
+static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
   if (M <= 32) return 1;
   if (g_tw2) return g_tw2;
-  return epi == EPI_SWIGLU ? 2 : 1;
+  // two tiles per wave halve the workgroups: only where >= 192 remain (70B gate/up: 224;
+  // 8B gate/up would drop to 112 of 256 CUs)
+  return epi == EPI_SWIGLU && ntiles / (2 * g_nw) >= 192 ? 2 : 1;
 }
 static int gemv_version() {
   if (g_ver < 0) {
@@ -265,7 +267,7 @@ void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   if (nsplit < 1) nsplit = 1;
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
-  if (gemv_version() == 2 && epi < 3 && p.M <= 64) return launch_gemv2(ptype, epi, p, nsplit, g_nw, gemv2_tw(p.M, epi), st);
+  if (gemv_version() == 2 && epi < 3 && p.M <= 64) return launch_gemv2(ptype, epi, p, nsplit, g_nw, gemv2_tw(p.M, epi, p.ntiles), st);
   switch (ptype) {
     case P_Q4_K: launch_pt<P_Q4_K>(epi, p, nsplit, st); break;
     case P_Q5_K: launch_pt<P_Q5_K>(epi, p, nsplit, st); break;
