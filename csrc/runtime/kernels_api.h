@@ -34,7 +34,9 @@ int gemv_tiles_per_wave(int M, int epi);
 inline int gemv_auto_split(int ntiles, int nsb, int M, int epi) {
   if (epi != EPI_ATOMIC) return 1;
   const int tpw = gemv_tiles_per_wave(M, epi);
-  const int target_waves = 4096 / tpw;
+  // wide row groups (M > 32) pay more per split (x re-staged per split, M atomics per output):
+  // 70B M=64 best at ~2048 tile-waves (qkv 31 -> 29 us, o 25.4 -> 22.1 us; r1g_gemv_tiles_per_wave_ab.txt)
+  const int target_waves = (M > 32 ? 2048 : 4096) / tpw;
   const int waves = (ntiles + tpw - 1) / tpw;
   int s = (target_waves + waves - 1) / waves;
   const int smax = nsb / 4 > 1 ? nsb / 4 : 1;
