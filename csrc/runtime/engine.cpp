@@ -145,6 +145,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
   packed_prefill_ = j.get_bool("packed_prefill", true);
+  prefix_cache_ = j.get_bool("prefix_cache", true);
 
   // ---- stages this process owns
   for (int s = 0; s < S_; ++s) {
@@ -600,6 +601,7 @@ void Engine::write_trace(const std::string& path) const {
 Json Engine::health() const {
   Json j = Json::object();
   j["ok"] = !failed_;
+  j["prefix_reused_tokens"] = (int64_t)reused_tokens_;
   Json st = Json::array();
   for (auto& w : workers_) {
     Json o = Json::object();
@@ -691,7 +693,16 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
       const size_t i = (size_t)mb * B_ + b;
       if (i >= prompts.size()) continue;
       const int n = (int)prompts[i].size();
-      for (int p0 = 0; p0 < n;) {
+      // prefix cache: the slot's KV already holds the tokens of slot_toks_[i]; only the part after
+      // the common prefix is prefilled (at least the last prompt token, whose row feeds the head)
+      int reuse = 0;
+      if (prefix_cache_ && i < slot_toks_.size()) {
+        const auto& c = slot_toks_[i];
+        const size_t lim = std::min(c.size(), (size_t)n - 1);
+        while ((size_t)reuse < lim && c[reuse] == prompts[i][reuse]) ++reuse;
+      }
+      reused_tokens_ += reuse;
+      for (int p0 = reuse; p0 < n;) {
         const int take = std::min(chunk_ - it.T, n - p0);
         PrefillSeg sg;
         sg.b = b; sg.p0 = p0; sg.T = take; sg.last = p0 + take >= n;
@@ -706,10 +717,24 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
     e.mb = mb;
     items.push_back(e);
   }
+  slot_toks_.clear();   // KV content unknown until this prefill has completed
   run_all(items);
   started_ = true;
   if (owns_last())
     for (size_t i = 0; i < prompts.size(); ++i) gen_[i].push_back(out_host_[i]);
+  slot_toks_ = prompts;
+}
+
+// tokens whose KV a slot holds after the last decode round: prompt + every generated token that went
+// through a decode step (all but the newest).  The generated part is only known where the last
+// stage lives, so a multi-process pipeline caches prompts only (every rank must agree on reuse).
+void Engine::refresh_slot_cache() {
+  slot_toks_ = prompts_;
+  if (!resumable_ || !owns_first() || !owns_last()) return;
+  for (size_t i = 0; i < slot_toks_.size() && i < gen_.size(); ++i) {
+    const size_t n = std::min(gen_[i].size(), (size_t)rounds_done_);
+    slot_toks_[i].insert(slot_toks_[i].end(), gen_[i].begin(), gen_[i].begin() + n);
+  }
 }
 
 // ---------------------------------------------------------------- checkpoint / resume
@@ -876,6 +901,7 @@ Json Engine::load_state(const std::string& dir) {
   }
   started_ = true;
   resumable_ = true;
+  refresh_slot_cache();
   MP_LOGI("state loaded from %s: %zu sequences, %d rounds", dir.c_str(), prompts_.size(), rounds_done_);
   Json r = Json::object();
   r["rounds_done"] = rounds_done_; r["sequences"] = (int)prompts_.size();
@@ -928,6 +954,7 @@ StepStats Engine::decode_steps(int k) {
         if (on_token) on_token((int)i, t);
       }
   rounds_done_ += k;
+  refresh_slot_cache();
   return ss;
 }
 
@@ -999,6 +1026,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
   const double t0 = now_ms();
   start(prompts);
   resumable_ = false;   // sequences advance by different amounts: positions are not prompt + rounds
+  slot_toks_.clear();   // the verify chunks write draft rows past the accepted tokens
   const double t1 = now_ms();
   const size_t n = prompts.size();
   if (on_token)

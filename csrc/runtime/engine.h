@@ -149,6 +149,12 @@ class Engine {
   int rounds_cap_ = 0, rounds_done_ = 0;
   bool started_ = false;
   bool resumable_ = true;   // false after spec_generate (per-sequence positions)
+  // prefix cache (config "prefix_cache", default on): per slot, the tokens its KV holds; start()
+  // prefills only what follows the common prefix (multi-turn chat re-sends the whole history)
+  bool prefix_cache_ = true;
+  std::vector<std::vector<int32_t>> slot_toks_;
+  long reused_tokens_ = 0;
+  void refresh_slot_cache();
   double load_ms_ = 0;
 };
 

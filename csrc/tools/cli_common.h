@@ -88,6 +88,7 @@ inline void print_common_usage(FILE* f) {
           "  --micro-batches M         micro-batches in flight;  --mb-size B sequences per micro-batch\n"
           "  --split even|mem|cost     layer partitioner (default cost)\n"
           "  --link local|rccl|tcp     stage transport;  --prefill-chunk N;  --no-graphs;  --threads N\n"
+          "  --no-prefix-cache         prefill every request in full (no KV reuse of a common prefix)\n"
           "  --world N --rank R        one process per stage (multi-process / multi-host)\n"
           "  --next HOST --master HOST --base-port P   TCP ring neighbours (prima.cpp style)\n"
           "  --rpc host:port,...       accepted for llama-cli parity: hosts of the stage processes\n"
@@ -149,6 +150,7 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--device") e["device"] = std::atoi(val().c_str());
     else if (a == "--verbose" || a == "-v") { o.verbose = true; e["verbose"] = true; }
     else if (a == "--log-file") e["log_file"] = val();
+    else if (a == "--no-prefix-cache") e["prefix_cache"] = false;
     else if (a == "--trace") o.trace = val();
     else if (a == "--no-display-prompt") o.echo_prompt = false;
     else if (a == "--bench") o.bench = true;

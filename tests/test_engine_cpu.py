@@ -305,3 +305,25 @@ def test_cpu_checkpoint_rejects_other_shape(native, model_dir, tmp_path):
     with Engine(gguf=path, backend="cpu", max_ctx=64, mb_size=1, n_mb=2) as eng:
         with pytest.raises(RuntimeError):
             eng.load_state(str(tmp_path / "st"))
+
+
+@pytest.mark.parametrize("stages", [1, 2])
+def test_cpu_prefix_cache_multiturn(native, model_dir, stages):
+    """Multi-turn: the second request re-sends prompt + reply + new text; with the prefix cache the
+    slot's KV is reused (only the new tail is prefilled) and the output equals a cold engine's."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(5)
+    p1 = [int(t) for t in rng.integers(3, cfg.vocab, 37)]
+    kw = dict(gguf=path, backend="cpu", max_ctx=256, prefill_chunk=16, stages=stages, split="even")
+    with Engine(**kw) as eng:
+        o1, _ = eng.generate([p1], 9)
+        p2 = p1 + o1[0] + [int(t) for t in rng.integers(3, cfg.vocab, 11)]
+        o2, _ = eng.generate([p2], 9)
+        reused = eng.health()["prefix_reused_tokens"]
+    # KV of p1 + the 8 generated tokens that went through decode
+    assert reused == len(p1) + 8
+    with Engine(prefix_cache=False, **kw) as eng:
+        c2, _ = eng.generate([p2], 9)
+        assert eng.health()["prefix_reused_tokens"] == 0
+    assert o2 == c2

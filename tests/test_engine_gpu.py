@@ -297,3 +297,22 @@ def test_checkpoint_resume(cuda, native, model_dir, tmp_path, stages, sampling):
         eng.decode(7)
         resumed = eng.tokens()
     assert resumed == full
+
+
+def test_prefix_cache_multiturn(cuda, native, model_dir):
+    """HIP stages: a follow-up request that extends the previous prompt + reply prefills only its
+    new tail and produces the same greedy tokens as an engine without the prefix cache."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    rng = np.random.default_rng(6)
+    p1 = [int(t) for t in rng.integers(3, cfg.vocab, 50)]
+    kw = dict(gguf=path, max_ctx=256, prefill_chunk=16, n_mb=2, mb_size=2, stages=2, devices=[0, 0],
+              link="local", split="even")
+    with Engine(**kw) as eng:
+        o1, _ = eng.generate([p1, p1[:20]], 8)
+        p2 = [p1 + o1[0] + [5, 6, 7], p1[:20] + [9]]
+        o2, _ = eng.generate(p2, 8)
+        assert eng.health()["prefix_reused_tokens"] == (len(p1) + 7) + 20
+    with Engine(prefix_cache=False, **kw) as eng:
+        c2, _ = eng.generate(p2, 8)
+    assert o2 == c2
