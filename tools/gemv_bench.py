@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--splits", default="auto")
     ap.add_argument("--iters", type=int, default=24)
     ap.add_argument("--target", type=int, default=2048)
+    ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 store, 1 atomic): timing probes")
     ap.add_argument("--probe", type=int, default=0, help="3: loads only, 4: weight+x loads, 5: dequant+MFMA without x loads")
     a = ap.parse_args()
     L = N.lib()
@@ -39,6 +40,8 @@ def main():
         n, k, epi = SHAPES[sname]
         if a.probe:
             epi = a.probe
+        if a.epi >= 0:
+            epi = a.epi
         for tname in a.types.split(","):
             qt = TYPES[tname]
             if sname.endswith("head") and tname == "Q4_K":
@@ -59,7 +62,7 @@ def main():
                 for tpw in [int(t) for t in a.tpw.split(",")]:
                     L.mp_set_gemv_tpw(tpw)
                     waves = (ntiles + tpw - 1) // tpw
-                    if epi != EPI_ATOMIC:
+                    if epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
                         splits = [1]
                     elif a.splits == "auto":
                         splits = [max(1, min((a.target + waves - 1) // waves, max(1, nsb // 4)))]
