@@ -64,11 +64,7 @@ def main():
         if world == 1 and args.gpus > 1:
             print("bench.py: --gpus > 1 must be launched with torchrun (one rank per GPU)", file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    from mipipe.engine import Engine, rccl_unique_id_hex
+    from mipipe.parallel import init_from_torchrun
 
     n_mb = args.n_mb or world
     max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
@@ -77,20 +73,9 @@ def main():
     for kv in args.set:
         k, v = kv.split("=", 1)
         cfg[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
-    if world > 1:
-        cfg.update(mode="mp", world=world, rank=rank, device=local_rank, link=args.link)
-        if args.link == "rccl":
-            # link r = stage r -> stage (r+1) % N; its sender (rank r) creates the RCCL unique id,
-            # so every bootstrap root lives in a process that is a member of that communicator
-            ids = [None] * world
-            dist.all_gather_object(ids, rccl_unique_id_hex())
-            cfg["rccl_ids"] = ids
-        else:
-            cfg["base_port"] = int(os.environ.get("MASTER_PORT", "29500")) + 11
-    else:
-        cfg.update(mode="local", stages=1, devices=[local_rank])
-
-    eng = Engine(**cfg)
+    # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
+    # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
+    eng = init_from_torchrun(link=args.link, **cfg)
     g = torch.Generator().manual_seed(0)
     prompts = torch.randint(3, MODELS[args.model]["vocab"], (n_mb * args.mb_size, args.prompt_len),
                             generator=g).tolist()

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "engine.h"
+#include "model.h"
 #include "gguf.h"
 #include "hip_stage.h"
 #include "json.h"
@@ -459,6 +460,27 @@ int mp_engine_logits(void* h, int mb, float* out, int rows) {
   API_TRY
   return static_cast<Engine*>(h)->copy_logits(mb, out, rows);
   API_CATCH(-1)
+}
+// stage partitioner (model.cpp) on its own: {"layer_cost": [...], "first_extra", "last_extra",
+// "device_speed": [...] (one per stage), "split": "even"|"mem"|"cost"} -> [[begin, end], ...]
+const char* mp_plan_partition(const char* cfg) {
+  API_TRY
+  const Json j = Json::parse(cfg);
+  std::vector<double> cost, speed;
+  for (const Json& v : j["layer_cost"].arr()) cost.push_back(v.num());
+  for (const Json& v : j["device_speed"].arr()) speed.push_back(v.num());
+  const auto specs = partition_layers(cost, j.get_num("first_extra", 0.0), j.get_num("last_extra", 0.0), speed,
+                                      parse_split_mode(j.get_str("split", "cost")));
+  Json out = Json::array();
+  for (const auto& s : specs) {
+    Json r = Json::array();
+    r.push(s.layer_begin);
+    r.push(s.layer_end);
+    out.push(r);
+  }
+  g_str = out.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
 }
 // multi-process rendezvous helpers: unique id bytes for RCCL
 int mp_rccl_unique_id(uint8_t* out128) {

@@ -68,6 +68,7 @@ _SIGS = {
     "mp_engine_info": ([c_void_p], c_char_p),
     "mp_engine_health": ([c_void_p], c_char_p),
     "mp_engine_save_state": ([c_void_p, c_char_p], c_char_p),
+    "mp_plan_partition": ([c_char_p], c_char_p),
     "mp_engine_load_state": ([c_void_p, c_char_p], c_char_p),
     "mp_engine_trace": ([c_void_p, c_int, c_char_p], c_int),
     "mp_engine_generate": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p], c_char_p),

@@ -1,0 +1,87 @@
+"""mipipe.parallel: the native partitioner through the C API, the piped-ring schedule model, and the
+torchrun launch helper (2 processes, CPU stages over TCP, gloo rendezvous)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO, make_model
+
+
+def test_plan_partition_modes(native):
+    from mipipe.parallel import plan_partition
+    cost = [1.0] * 10
+    assert plan_partition(cost, 3, split="even") == [(0, 4), (4, 7), (7, 10)]
+    # a heavy LM head pushes layers off the last stage under "cost", not under "mem"
+    cst = plan_partition(cost, 2, split="cost", last_extra=4.0)
+    mem = plan_partition(cost, 2, split="mem", last_extra=4.0)
+    assert mem == [(0, 5), (5, 10)]
+    assert cst == [(0, 7), (7, 10)]
+    # a twice-as-fast device takes twice the layers
+    assert plan_partition([1.0] * 9, device_speed=[2.0, 1.0]) == [(0, 6), (6, 9)]
+    with pytest.raises(RuntimeError):
+        plan_partition(cost, 11)
+
+
+@pytest.mark.parametrize("stages,n_mb", [(1, 1), (2, 1), (2, 2), (4, 4), (4, 8), (8, 8)])
+def test_piped_ring_model_matches_bound(stages, n_mb):
+    from mipipe.parallel import simulate_piped_ring
+    st = [1.0 + 0.1 * s for s in range(stages)]
+    r = simulate_piped_ring(st, n_mb, rounds=24, link_ms=0.05, ring_ms=0.02)
+    assert r["round_ms"] == pytest.approx(r["bound_ms"])
+    if r["bound_ms"] == pytest.approx(n_mb * max(st)):   # throughput-bound: the slowest stage never idles
+        assert r["stage_busy"][-1] == pytest.approx(1.0) and r["bubble"] == pytest.approx(0.0, abs=1e-9)
+    assert 0.0 <= r["bubble"] < 1.0
+
+
+def test_piped_ring_needs_micro_batches():
+    """One micro-batch on 8 stages leaves each stage busy 1/8 of the time; 8 fill the ring."""
+    from mipipe.parallel import simulate_piped_ring
+    one = simulate_piped_ring([1.0] * 8, 1)
+    eight = simulate_piped_ring([1.0] * 8, 8)
+    assert one["round_ms"] == pytest.approx(8.0) and one["stage_busy"][0] == pytest.approx(1 / 8)
+    assert eight["round_ms"] == pytest.approx(8.0) and eight["stage_busy"][0] == pytest.approx(1.0)
+
+
+_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+from mipipe.parallel import init_from_torchrun
+import torch.distributed as dist
+eng = init_from_torchrun(gguf={path!r}, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16,
+                         split="even", base_port={port})
+out, _ = eng.generate({prompts!r}, 6)
+stages = eng.info["stages"]
+eng.close()
+dist.barrier()
+print("OUT " + json.dumps(dict(rank=dist.get_rank(), out=out, stages=stages)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_init_from_torchrun_two_processes(native, model_dir, tmp_path):
+    from mipipe.engine import Engine
+    from test_engine_cpu import free_port
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts = [[5, 6, 7, 8], [9, 10]]
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16) as eng:
+        ref, _ = eng.generate(prompts, 6)
+    script = tmp_path / "run.py"
+    script.write_text(_SCRIPT.format(repo=REPO, path=path, prompts=prompts, port=free_port()))
+    mport = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(mport))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    res = {}
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+        d = json.loads([l for l in o.splitlines() if l.startswith("OUT ")][-1][4:])
+        res[d["rank"]] = d
+    assert [(s["layer_begin"], s["layer_end"]) for s in res[1]["stages"]] == [(0, 2), (2, 4)]
+    assert res[1]["out"] == ref   # the last stage's process holds the generated tokens
