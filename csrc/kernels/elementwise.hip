@@ -26,7 +26,7 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
 // in flight.
 __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
                                                        float eps, f16* out, int ldo, float* zero,
-                                                       int64_t zero_n, int M) {
+                                                       int64_t zero_n, int M, const float* bias, int bias_n) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
@@ -41,7 +41,10 @@ __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, 
       ww[k] = i < d ? *reinterpret_cast<const float4*>(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  if (zero) {
+  if (zero && bias) {
+    const int64_t z0 = (int64_t)blockIdx.x * 16384, z1 = min(zero_n, z0 + 16384);
+    for (int64_t i = z0 + tid; i < z1; i += 1024) zero[i] = bias[i % bias_n];
+  } else if (zero) {
     const int64_t z0 = (int64_t)blockIdx.x * 16384, z1 = min(zero_n, z0 + 16384);
     for (int64_t i = z0 + tid * 4; i < z1; i += 4096) {
       if (i + 4 <= z1) *reinterpret_cast<float4*>(zero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -231,10 +234,10 @@ void launch_prefill_meta(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, in
 }
 
 void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
-                    float* zero, int64_t zero_n, hipStream_t st) {
+                    float* zero, int64_t zero_n, hipStream_t st, const float* bias, int bias_n) {
   const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
   hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
-                     zero_n, M);
+                     zero_n, M, bias, bias_n);
 }
 
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,

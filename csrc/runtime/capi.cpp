@@ -134,6 +134,7 @@ const char* mp_model_config_json(const char* gguf_path) {
   j["head_dim"] = c.head_dim; j["d_ff"] = c.d_ff; j["vocab"] = c.vocab; j["rope_base"] = (double)c.rope_base;
   j["eps"] = (double)c.eps; j["n_expert"] = c.n_expert; j["n_expert_used"] = c.n_expert_used;
   j["rope_freqs"] = c.rope_freqs; j["tied_output"] = c.tied_output;
+  j["arch"] = c.arch; j["rope_neox"] = c.rope_neox; j["qkv_bias"] = c.qkv_bias;
   g_str = j.dump();
   return g_str.c_str();
   API_CATCH(nullptr)
@@ -322,10 +323,10 @@ int mp_tok_info(void* h, int32_t* out) {  // vocab, bos, eos, eot
   API_CATCH(-1)
 }
 // pre-tokenizer split (tests): returns pieces joined by '\x1f'
-const char* mp_tok_pretokenize(const char* text) {
+const char* mp_tok_pretokenize(const char* text, int max_digits) {
   API_TRY
   g_str.clear();
-  for (auto& p : Tokenizer::llama3_pretokenize(text)) { g_str += p; g_str += '\x1f'; }
+  for (auto& p : Tokenizer::llama3_pretokenize(text, max_digits > 0 ? max_digits : 3)) { g_str += p; g_str += '\x1f'; }
   return g_str.c_str();
   API_CATCH(nullptr)
 }

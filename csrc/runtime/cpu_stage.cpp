@@ -114,6 +114,11 @@ void CpuStage::load_gguf(const GgufFile& f) {
     Layer& L = layers_[li - spec_.layer_begin];
     const std::string p = "blk." + std::to_string(li) + ".";
     L.attn_norm = tensor_f32(need(p + "attn_norm.weight"));
+    if (cfg_.qkv_bias) {
+      L.bq = tensor_f32(need(p + "attn_q.bias"));
+      L.bk = tensor_f32(need(p + "attn_k.bias"));
+      L.bv = tensor_f32(need(p + "attn_v.bias"));
+    }
     L.ffn_norm = tensor_f32(need(p + "ffn_norm.weight"));
     L.q = mat(p + "attn_q.weight");
     L.k = mat(p + "attn_k.weight");
@@ -275,17 +280,26 @@ void CpuStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   matmul(L.q, xn_.data(), d, M, qkv_.data(), ldq, false);
   matmul(L.k, xn_.data(), d, M, qkv_.data() + qd, ldq, false);
   matmul(L.v, xn_.data(), d, M, qkv_.data() + qd + kvd, ldq, false);
-  // RoPE (adjacent pairs, GGUF Llama layout) + KV append
+  if (!L.bq.empty())
+    for (int m = 0; m < M; ++m) {
+      float* row = qkv_.data() + (size_t)m * ldq;
+      for (int i = 0; i < qd; ++i) row[i] += L.bq[i];
+      for (int i = 0; i < kvd; ++i) row[qd + i] += L.bk[i], row[qd + kvd + i] += L.bv[i];
+    }
+  // RoPE (GGUF Llama layout: adjacent pairs (2i, 2i+1); Qwen2 NEOX: (i, i + hd/2)) + KV append
+  const int half = hd / 2, pstride = cfg_.rope_neox ? 1 : 2, poff = cfg_.rope_neox ? half : 1;
   for (int m = 0; m < M; ++m) {
     float* row = qkv_.data() + (size_t)m * ldq;
     const int p = pos[m];
     for (int h = 0; h < Hq + Hkv; ++h) {
       float* v = row + (size_t)h * hd;   // q heads then k heads (contiguous)
-      for (int i = 0; i < hd / 2; ++i) {
+      for (int i = 0; i < half; ++i) {
         const float a = p * inv_freq_[i], c = std::cos(a), s = std::sin(a);
-        const float x0 = v[2 * i], x1 = v[2 * i + 1];
-        v[2 * i] = x0 * c - x1 * s;
-        v[2 * i + 1] = x0 * s + x1 * c;
+        float* e0 = v + pstride * i;
+        float* e1 = e0 + poff;
+        const float x0 = *e0, x1 = *e1;
+        *e0 = x0 * c - x1 * s;
+        *e1 = x0 * s + x1 * c;
       }
     }
     const size_t kv_off = ((size_t)slot[m] * ctx + p) * kvd;

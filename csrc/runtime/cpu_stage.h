@@ -53,6 +53,7 @@ class CpuStage : public Stage {
   struct Layer {
     std::vector<float> attn_norm, ffn_norm;
     CpuMat q, k, v, o, gate, up, down;
+    std::vector<float> bq, bk, bv;   // Qwen2 q/k/v biases (empty: none)
     bool moe = false;
     CpuMat router;
     std::vector<CpuMat> eg, eu, ed;   // experts

@@ -155,11 +155,15 @@ void HipStage::load_gguf(const GgufFile& f) {
       int64_t N = 0;
       std::vector<std::pair<const GgufTensor*, int64_t>> parts;
       for (int k = i; k < j; ++k) { parts.push_back({qkv[k], N}); N += qkv[k]->ne[1]; }
-      auto rowfn = [&parts](int64_t n) -> const uint8_t* {
+      const bool neox = cfg_.rope_neox;
+      const int hd = cfg_.head_dim;
+      auto rowfn = [&parts, &tq, &tk, neox, hd](int64_t n) -> const uint8_t* {
         for (auto it = parts.rbegin(); it != parts.rend(); ++it)
           if (n >= it->second) {
             const GgufTensor* t = it->first;
-            return t->data + (n - it->second) * row_bytes(t->type, t->ne[0]);
+            int64_t r = n - it->second;
+            if (neox && (t == &tq || t == &tk)) r = neox_src_row(r, hd);
+            return t->data + r * row_bytes(t->type, t->ne[0]);
           }
         return nullptr;
       };
@@ -169,6 +173,17 @@ void HipStage::load_gguf(const GgufFile& f) {
       off += (int)N;
       L.qkv.push_back(s);
       i = j;
+    }
+    if (cfg_.qkv_bias) {
+      std::vector<float> b(qkv_n_, 0.f);
+      const char* nm[3] = {"attn_q.bias", "attn_k.bias", "attn_v.bias"};
+      const int o[3] = {0, cfg_.q_dim(), cfg_.q_dim() + cfg_.kv_dim()};
+      for (int i = 0; i < 3; ++i) {
+        const std::vector<float> v = tensor_f32(need(p + nm[i]));
+        for (size_t r = 0; r < v.size(); ++r)
+          b[o[i] + r] = v[i < 2 && cfg_.rope_neox ? neox_src_row((long)r, cfg_.head_dim) : r];
+      }
+      L.qkv_bias = upload_f32(b.data(), b.size());
     }
     L.wo = pack_mat(need(p + "attn_output.weight"));
     if (cfg_.n_expert) {
@@ -565,7 +580,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
                              const int32_t* slot, bool decode, hipStream_t st) {
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
-  launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st);
+  launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st, L.qkv_bias, qkv_n_);
   for (const MatSeg& s : L.qkv)
     gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
   if (decode && opt_.fused_attn) {

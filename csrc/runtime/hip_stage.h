@@ -57,6 +57,7 @@ struct LayerW {
   float* attn_norm = nullptr;
   float* ffn_norm = nullptr;
   std::vector<MatSeg> qkv;
+  float* qkv_bias = nullptr;  // [q | k | v] f32 (Qwen2), q/k rows NEOX-permuted like the weights
   PackedMat wo;
   bool fused_gateup = true;
   PackedMat gateup;           // interleaved (fused SwiGLU)

@@ -48,8 +48,10 @@ void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, i
 void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
 
 // x f32 [M][ldx] -> out f16 [M][ldo] = rmsnorm(x) * w ; also zero `zero_n` floats at `zero`
+// `zero` is filled with 0, or with `bias` repeated every `bias_n` floats when bias != nullptr (the
+// split-K accumulator of the next GEMV starts at the projection bias: Qwen2 q/k/v biases)
 void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo,
-                    int M, float* zero, int64_t zero_n, hipStream_t st);
+                    int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias = nullptr, int bias_n = 0);
 // same but f32 output (final norm before LM head may use f16 as well)
 
 // embedding gather + dequant of raw GGUF rows -> x f32 [M][ldx]

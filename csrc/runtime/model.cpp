@@ -15,7 +15,9 @@ ModelConfig ModelConfig::from_gguf(const GgufFile& f) {
   c.arch = f.get_str("general.architecture", "llama");
   c.name = f.get_str("general.name", "");
   const std::string a = c.arch + ".";
-  if (c.arch != "llama") throw std::runtime_error("unsupported architecture: " + c.arch);
+  if (c.arch != "llama" && c.arch != "qwen2") throw std::runtime_error("unsupported architecture: " + c.arch);
+  c.rope_neox = c.arch == "qwen2";
+  c.qkv_bias = f.tensor("blk.0.attn_q.bias") != nullptr;
   c.n_layer = (int)f.get_int(a + "block_count", 0);
   c.d_model = (int)f.get_int(a + "embedding_length", 0);
   c.n_head = (int)f.get_int(a + "attention.head_count", 0);
@@ -46,6 +48,8 @@ std::string ModelConfig::describe() const {
     << " n_head_kv=" << n_head_kv << " head_dim=" << head_dim << " d_ff=" << d_ff << " vocab=" << vocab
     << " rope_base=" << rope_base;
   if (n_expert) o << " n_expert=" << n_expert << " n_expert_used=" << n_expert_used;
+  if (rope_neox) o << " rope=neox";
+  if (qkv_bias) o << " qkv_bias";
   return o.str();
 }
 

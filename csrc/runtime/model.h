@@ -22,6 +22,13 @@ struct ModelConfig {
   int n_expert = 0, n_expert_used = 0;
   bool rope_freqs = false;
   bool tied_output = false;
+  // Qwen2 family (arch "qwen2"): q/k/v projections carry biases, and RoPE rotates the pairs
+  // (i, i + hd/2) ("NEOX" mode) instead of (2i, 2i+1).  The stages permute the rows of Wq / Wk
+  // (and the q/k biases) per head at load time, new row 2i <- i, 2i+1 <- i + hd/2 (neox_src_row),
+  // which turns NEOX rotation into the adjacent-pair rotation the kernels implement; q.k is
+  // invariant under the shared permutation and V is untouched, so no kernel changes.
+  bool rope_neox = false;
+  bool qkv_bias = false;
 
   int q_dim() const { return n_head * head_dim; }
   int kv_dim() const { return n_head_kv * head_dim; }
@@ -29,6 +36,12 @@ struct ModelConfig {
   static ModelConfig from_gguf(const GgufFile& f);
   std::string describe() const;
 };
+
+// source row of permuted q/k row r (rope_neox): within a head of hd rows, 2i <- i, 2i+1 <- i + hd/2
+inline long neox_src_row(long r, int hd) {
+  const long h = r / hd, j = r % hd;
+  return h * hd + ((j & 1) ? j / 2 + hd / 2 : j / 2);
+}
 
 struct StageSpec {
   int stage = 0, n_stages = 1;

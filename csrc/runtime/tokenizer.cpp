@@ -76,7 +76,7 @@ bool uc_is_space(uint32_t cp) { return cp >= 0x09 && in_ranges(kSpaces, cp); }
 
 // ------------------------------------------------------------------ Llama-3 pre-tokenizer
 // (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+
-std::vector<std::string> Tokenizer::llama3_pretokenize(const std::string& text) {
+std::vector<std::string> Tokenizer::llama3_pretokenize(const std::string& text, int max_digits) {
   const std::vector<uint32_t> cp = utf8_decode(text);
   const size_t n = cp.size();
   auto L = [&](size_t i) { return i < n && uc_is_letter(cp[i]); };
@@ -107,7 +107,7 @@ std::vector<std::string> Tokenizer::llama3_pretokenize(const std::string& text) 
     // 3. \p{N}{1,3}
     if (!e && N(i)) {
       size_t j = i;
-      while (j < i + 3 && N(j)) ++j;
+      while (j < i + (size_t)max_digits && N(j)) ++j;
       e = j;
     }
     // 4.  ?[^\s\p{L}\p{N}]+[\r\n]*
@@ -190,7 +190,9 @@ Tokenizer Tokenizer::from_gguf(const GgufFile& f) {
   t.eot_ = (int32_t)f.get_int("tokenizer.ggml.eot_token_id", -1);
   t.unk_ = (int32_t)f.get_int("tokenizer.ggml.unknown_token_id", 0);
   t.add_space_prefix_ = f.get_bool("tokenizer.ggml.add_space_prefix", t.kind_ == SPM);
-  t.add_bos_default_ = f.get_bool("tokenizer.ggml.add_bos_token", true);
+  const std::string pre = f.get_str("tokenizer.ggml.pre", "llama-bpe");
+  t.max_digits_ = pre == "qwen2" ? 1 : 3;   // qwen2 splits numbers into single digits
+  t.add_bos_default_ = f.get_bool("tokenizer.ggml.add_bos_token", pre != "qwen2");
   for (size_t i = 0; i < V; ++i)
     if ((t.types_[i] == 3 || t.types_[i] == 4) && !t.tokens_[i].empty()) t.specials_.push_back({t.tokens_[i], (int32_t)i});
   std::sort(t.specials_.begin(), t.specials_.end(),
@@ -207,7 +209,7 @@ Tokenizer Tokenizer::from_gguf(const GgufFile& f) {
 // ------------------------------------------------------------------ encode
 void Tokenizer::encode_bpe_segment(const std::string& s, std::vector<int32_t>& out) const {
   const ByteMap& bm = bytemap();
-  for (const std::string& word : llama3_pretokenize(s)) {
+  for (const std::string& word : llama3_pretokenize(s, max_digits_)) {
     std::vector<std::string> sym;
     for (unsigned char c : word) sym.push_back(utf8_encode(bm.b2u[c]));
     while (sym.size() > 1) {

@@ -33,9 +33,11 @@ class Tokenizer {
   Kind kind() const { return kind_; }
 
   // exposed for tests
-  static std::vector<std::string> llama3_pretokenize(const std::string& text);
+  // max_digits: \p{N}{1,3} for llama-bpe, single digits (\p{N}) for the qwen2 pre-tokenizer
+  static std::vector<std::string> llama3_pretokenize(const std::string& text, int max_digits = 3);
 
  private:
+  int max_digits_ = 3;
   void encode_bpe_segment(const std::string& s, std::vector<int32_t>& out) const;
   void encode_spm_segment(const std::string& s, std::vector<int32_t>& out) const;
 

@@ -82,7 +82,7 @@ _SIGS = {
     "mp_set_gemv_wpb": ([c_int], None),
     "mp_set_gemv_tpw": ([c_int], None),
     "mp_init_packed": ([c_void_p, ctypes.c_size_t, c_int, c_float, ctypes.c_uint64, c_void_p], c_int),
-    "mp_tok_pretokenize": ([c_char_p], c_char_p),
+    "mp_tok_pretokenize": ([c_char_p, c_int], c_char_p),
 }
 
 

@@ -29,6 +29,9 @@ class LlamaConfig:
     head_dim: int = 0           # 0 -> d_model // n_head
     tokenizer: str = "llama"    # "gpt2" (byte-level BPE) or "llama" (SPM)
     rope_freq_factors: bool = False   # Llama-3.1 rope_freqs.weight
+    arch: str = "llama"         # GGUF general.architecture: "llama" or "qwen2"
+    qkv_bias: bool = False      # Qwen2: attn_{q,k,v}.bias
+    tied_output: bool = False   # no output.weight (LM head = token_embd)
 
     @property
     def hd(self) -> int:
@@ -50,10 +53,14 @@ CONFIGS = {
                               tokenizer="gpt2", rope_freq_factors=True),
     "mixtral-8x7b": LlamaConfig("mixtral-8x7b", 32, 4096, 32, 8, 14336, 32000, 1e6, 1e-5, 32768,
                                 n_expert=8, n_expert_used=2),
+    "qwen2-7b": LlamaConfig("qwen2-7b", 28, 3584, 28, 4, 18944, 152064, 1e6, 1e-6, 32768,
+                            tokenizer="gpt2", arch="qwen2", qkv_bias=True),
     # small test shapes (same code paths, fast to generate)
     "tiny-gqa": LlamaConfig("tiny-gqa", 4, 512, 8, 2, 1024, 2048, 10000.0, 1e-5, 1024),
     "tiny-moe": LlamaConfig("tiny-moe", 3, 512, 8, 2, 768, 2048, 10000.0, 1e-5, 1024,
                             n_expert=4, n_expert_used=2),
+    "tiny-qwen2": LlamaConfig("tiny-qwen2", 4, 512, 8, 2, 1024, 4096, 1e6, 1e-6, 1024,
+                              tokenizer="gpt2", arch="qwen2", qkv_bias=True, tied_output=True),
     "tiny-l3": LlamaConfig("tiny-l3", 4, 1024, 8, 2, 2048, 4096, 500000.0, 1e-5, 1024,
                            tokenizer="gpt2", rope_freq_factors=True),
 }

@@ -46,6 +46,7 @@ class RefLlama:
                   eps=float(g("attention.layer_norm_rms_epsilon", 1e-5)),
                   n_expert=int(g("expert_count", 0)), n_expert_used=int(g("expert_used_count", 0)))
         hp["head_dim"] = int(g("rope.dimension_count", hp["d_model"] // hp["n_head"]))
+        hp["rope_neox"] = a == "qwen2"   # llama.cpp LLM_ARCH_QWEN2 uses LLAMA_ROPE_TYPE_NEOX
         tensors = {name: r.tensor_f32(name) for name in r.tensors}
         return cls(tensors, hp, dtype, device)
 
@@ -55,12 +56,18 @@ class RefLlama:
         return x * w
 
     def rope(self, x, pos):
-        # x: [T, H, hd]; adjacent pairs (2i, 2i+1)
+        # x: [T, H, hd]; Llama: adjacent pairs (2i, 2i+1); NEOX (Qwen2): pairs (i, i + hd/2)
         ang = torch.as_tensor(np.outer(np.asarray(pos, np.float64), self.inv_freq),
                               dtype=torch.float64, device=x.device)
         c, s = torch.cos(ang).to(x.dtype)[:, None, :], torch.sin(ang).to(x.dtype)[:, None, :]
-        x0, x1 = x[..., 0::2], x[..., 1::2]
         out = torch.empty_like(x)
+        if self.hp.get("rope_neox"):
+            h = x.shape[-1] // 2
+            x0, x1 = x[..., :h], x[..., h:]
+            out[..., :h] = x0 * c - x1 * s
+            out[..., h:] = x0 * s + x1 * c
+            return out
+        x0, x1 = x[..., 0::2], x[..., 1::2]
         out[..., 0::2] = x0 * c - x1 * s
         out[..., 1::2] = x0 * s + x1 * c
         return out
@@ -87,9 +94,10 @@ class RefLlama:
         for i in range(a, b):
             p = f"blk.{i}."
             h = self.rmsnorm(x, t[p + "attn_norm.weight"])
-            q = (h @ t[p + "attn_q.weight"].T).view(T, H, hd)
-            k = (h @ t[p + "attn_k.weight"].T).view(T, Hk, hd)
-            v = (h @ t[p + "attn_v.weight"].T).view(T, Hk, hd)
+            q, k, v = (h @ t[p + "attn_q.weight"].T), (h @ t[p + "attn_k.weight"].T), (h @ t[p + "attn_v.weight"].T)
+            if p + "attn_q.bias" in t:
+                q, k, v = q + t[p + "attn_q.bias"], k + t[p + "attn_k.bias"], v + t[p + "attn_v.bias"]
+            q, k, v = q.view(T, H, hd), k.view(T, Hk, hd), v.view(T, Hk, hd)
             q, k = self.rope(q, pos), self.rope(k, pos)
             if self.cache_k[i] is None or start_pos == 0:
                 self.cache_k[i], self.cache_v[i] = k, v

@@ -21,7 +21,8 @@ def llama_tensor_specs(cfg: LlamaConfig, ftype: str):
     L = cfg.n_layer
     yield ("token_embd.weight", (d, cfg.vocab), tensor_type(ftype, "token_embd", 0, L, d), "embd")
     yield ("output_norm.weight", (d,), Q.F32, "norm")
-    yield ("output.weight", (d, cfg.vocab), tensor_type(ftype, "output", 0, L, d), "w")
+    if not cfg.tied_output:
+        yield ("output.weight", (d, cfg.vocab), tensor_type(ftype, "output", 0, L, d), "w")
     if cfg.rope_freq_factors:
         yield ("rope_freqs.weight", (hd // 2,), Q.F32, "rope")
     for i in range(L):
@@ -30,6 +31,10 @@ def llama_tensor_specs(cfg: LlamaConfig, ftype: str):
         yield (p + "attn_q.weight", (d, cfg.n_head * hd), tensor_type(ftype, "attn_q", i, L, d), "w")
         yield (p + "attn_k.weight", (d, cfg.n_head_kv * hd), tensor_type(ftype, "attn_k", i, L, d), "w")
         yield (p + "attn_v.weight", (d, cfg.n_head_kv * hd), tensor_type(ftype, "attn_v", i, L, d), "w")
+        if cfg.qkv_bias:
+            yield (p + "attn_q.bias", (cfg.n_head * hd,), Q.F32, "bias")
+            yield (p + "attn_k.bias", (cfg.n_head_kv * hd,), Q.F32, "bias")
+            yield (p + "attn_v.bias", (cfg.n_head_kv * hd,), Q.F32, "bias")
         yield (p + "attn_output.weight", (cfg.n_head * hd, d),
                tensor_type(ftype, "attn_output", i, L, cfg.n_head * hd), "wo")
         yield (p + "ffn_norm.weight", (d,), Q.F32, "norm")
@@ -55,6 +60,8 @@ def _float_init(rng, name, shape, kind, cfg: LlamaConfig, wscale: float):
         # Llama-3.1 style frequency factors: 1 for high freqs, up to 8 for low freqs
         i = np.arange(n)
         return (1.0 + 7.0 * (i / max(n - 1, 1)) ** 2).astype(np.float32)
+    if kind == "bias":
+        return (rng.standard_normal(n) * 0.5).astype(np.float32)
     if kind == "router":
         return (rng.standard_normal(n) * 0.5).astype(np.float32)
     if kind == "embd":
@@ -72,7 +79,7 @@ def write_synthetic_gguf(path: str, cfg: LlamaConfig, ftype: str = "Q4_K_M", see
     if fast_random_blocks is None:
         fast_random_blocks = cfg.d_model >= 2048
     w = GGUFWriter(path)
-    arch = "llama"
+    arch = cfg.arch
     w.add("general.architecture", arch)
     w.add("general.name", f"synthetic-{cfg.name}-{ftype}")
     w.add("general.file_type", 15 if ftype.upper() == "Q4_K_M" else 0, U32)

@@ -136,7 +136,7 @@ def add_tokenizer_kv(w, cfg):
     if cfg.tokenizer == "gpt2":
         tokens, types, merges, bos, eos, eot = bpe_vocab(cfg.vocab)
         w.add("tokenizer.ggml.model", "gpt2")
-        w.add("tokenizer.ggml.pre", "llama-bpe")
+        w.add("tokenizer.ggml.pre", "qwen2" if cfg.arch == "qwen2" else "llama-bpe")
         w.add("tokenizer.ggml.tokens", tokens, elem_type=STRING)
         w.add("tokenizer.ggml.token_type", types, elem_type=I32)
         w.add("tokenizer.ggml.merges", merges, elem_type=STRING)

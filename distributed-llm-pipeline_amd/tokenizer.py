@@ -59,7 +59,8 @@ class Tokenizer:
         return buf.raw[:n]
 
     @staticmethod
-    def pretokenize(text: str) -> list[str]:
-        """The native Llama-3 pre-tokenizer split (regex-free implementation)."""
-        r = N.lib().mp_tok_pretokenize(text.encode("utf-8"))
+    def pretokenize(text: str, pre: str = "llama-bpe") -> list[str]:
+        """The native pre-tokenizer split (regex-free implementation): "llama-bpe" (Llama-3, numbers
+        in groups of up to 3 digits) or "qwen2" (single digits)."""
+        r = N.lib().mp_tok_pretokenize(text.encode("utf-8"), 1 if pre == "qwen2" else 3)
         return r.decode("utf-8").split("\x1f")[:-1]

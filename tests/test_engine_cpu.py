@@ -28,7 +28,8 @@ def free_port():
 
 
 @pytest.mark.parametrize("name,ftype", [("stories15m", "F32"), ("tiny-gqa", "Q8_0"), ("tiny-gqa", "Q4_K_M"),
-                                        ("tiny-l3", "Q6_K"), ("tiny-moe", "Q5_K_M"), ("tiny-gqa", "BF16")])
+                                        ("tiny-l3", "Q6_K"), ("tiny-moe", "Q5_K_M"), ("tiny-gqa", "BF16"),
+                                        ("tiny-qwen2", "Q4_K_M")])
 def test_cpu_engine_matches_reference(native, model_dir, name, ftype):
     from mipipe.engine import Engine
     from mipipe.models.reference import RefLlama

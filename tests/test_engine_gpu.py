@@ -16,7 +16,8 @@ def nmse(a, b):
 
 @pytest.mark.parametrize("name,ftype", [("stories15m", "F32"), ("tiny-gqa", "Q8_0"), ("tiny-gqa", "Q4_K_M"),
                                         ("tiny-l3", "Q6_K"), ("tiny-gqa", "Q5_K_M"), ("tiny-gqa", "BF16"),
-                                        ("tiny-moe", "Q8_0"), ("tiny-moe", "Q4_K_M")])
+                                        ("tiny-moe", "Q8_0"), ("tiny-moe", "Q4_K_M"), ("tiny-qwen2", "Q4_K_M"),
+                                        ("tiny-qwen2", "Q8_0")])
 def test_engine_matches_reference(cuda, native, model_dir, name, ftype):
     from mipipe.engine import Engine
     from mipipe.models.reference import RefLlama

@@ -44,6 +44,11 @@ def test_pretokenizer_matches_regex(native):
     pat = regex.compile(LLAMA3_PAT)
     for t in TEXTS + ["x's y'T Z'Ll", "  \n\n  a", "123456789012", "😀😀 a😀b"]:
         assert Tokenizer.pretokenize(t) == pat.findall(t), t
+    # Qwen2's pre-tokenizer differs only in splitting numbers into single digits
+    qpat = regex.compile(LLAMA3_PAT.replace(r"\p{N}{1,3}", r"\p{N}"))
+    assert qpat.pattern != pat.pattern
+    for t in TEXTS + ["123456789012 and 3.14159", "x1y22z333"]:
+        assert Tokenizer.pretokenize(t, "qwen2") == qpat.findall(t), t
 
 
 def test_bpe_matches_hf_tokenizers(bpe):
