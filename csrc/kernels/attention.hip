@@ -201,12 +201,15 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
+
 template <int DP>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
   constexpr int KK = DP / 32;
   constexpr int DT = DP / 16;
   __shared__ float sm_m[4][16], sm_l[4][16];
   __shared__ float sm_o[4][16][DP];
+  __shared__ float sm_mz[16][ATTN_MAX_SPLITS], sm_lz[16][ATTN_MAX_SPLITS];   // split merge
   __shared__ int sm_last;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -384,20 +387,41 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
   }
   __syncthreads();
   if (!sm_last) return;
+  // merge: the (m, l) pairs of every (head row, split) are read once, in parallel, into LDS; each
+  // head's max, weights and sum are formed there by one wave; then every output element sums its
+  // n_act partials with independent loads.  (Reading the pairs per element in a serial loop made
+  // the merge the long-context bottleneck: 8B single stream at 32K context spent ~60 us/layer.)
+  for (int i = threadIdx.x; i < G * n_act; i += 256) {
+    const int r = i / n_act, zz = i - r * n_act;
+    const size_t rid = (size_t)t * p.Hq + kvh * G + r;
+    sm_mz[r][zz] = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
+    sm_lz[r][zz] = ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1);
+  }
+  __syncthreads();
+  for (int r = wave; r < G; r += 4) {
+    float M = -INFINITY;
+    for (int zz = lane; zz < n_act; zz += 64) M = fmaxf(M, sm_mz[r][zz]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+    float L = 0.f;
+    for (int zz = lane; zz < n_act; zz += 64) {
+      const float mz = sm_mz[r][zz];
+      const float f = mz == -INFINITY ? 0.f : __expf(mz - M);
+      sm_mz[r][zz] = f;   // becomes the split's weight
+      L += sm_lz[r][zz] * f;
+    }
+    L = wave_sum(L);
+    if (lane == 0) sm_m[0][r] = L;
+  }
+  __syncthreads();
   for (int e = threadIdx.x; e < G * DP; e += 256) {
     const int r = e / DP, d = e % DP;
     const int hh = kvh * G + r;
     const size_t rid = (size_t)t * p.Hq + hh;
-    float M = -INFINITY;
-    for (int zz = 0; zz < n_act; ++zz) M = fmaxf(M, ld_sc1(p.ml_part + (zz * stride + rid) * 2));
-    float L = 0.f, O = 0.f;
-    for (int zz = 0; zz < n_act; ++zz) {
-      const float mz = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
-      if (mz == -INFINITY) continue;
-      const float f = __expf(mz - M);
-      L += ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1) * f;
-      O += ld_sc1(p.o_part + (zz * stride + rid) * DP + d) * f;
-    }
+    float O = 0.f;
+#pragma unroll 8
+    for (int zz = 0; zz < n_act; ++zz) O += sm_mz[r][zz] * ld_sc1(p.o_part + (zz * stride + rid) * DP + d);
+    const float L = sm_m[0][r];
     if (d < p.hd) p.out[(size_t)t * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
   }
   if (threadIdx.x == 0)

@@ -1,6 +1,7 @@
 #include "hip_stage.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -358,11 +359,14 @@ void HipStage::alloc_runtime() {
   if (split <= 0) {
     // auto: enough (sequence, kv head, split) workgroups to cover the CUs, but >= 256 keys per
     // split (a split merge costs a publish/acquire round trip; short contexts use one split)
+    static const int target = [] { const char* e = getenv("MIPIPE_ATTN_WG_TARGET"); return e ? std::max(1, atoi(e)) : 256; }();
     const int pairs = std::max(1, B * Hkv);
-    const int want = std::max(1, std::min((256 + pairs - 1) / pairs, (opt_.max_ctx + 255) / 256));
+    const int want = std::max(1, std::min((target + pairs - 1) / pairs, (opt_.max_ctx + 255) / 256));
     split = (opt_.max_ctx + want - 1) / want;
   }
   split = std::max(128, (int)round_up(split, 128));
+  // the fused decode attention merges at most 128 splits per (token, kv head) in LDS
+  split = std::max(split, (int)round_up((opt_.max_ctx + 127) / 128, 128));
   opt_.attn_split_len = split;
   n_split_ = (int)((opt_.max_ctx + split - 1) / split);
   if (n_split_ > 1) {

@@ -317,3 +317,28 @@ def test_prefix_cache_multiturn(cuda, native, model_dir):
     with Engine(prefix_cache=False, **kw) as eng:
         c2, _ = eng.generate(p2, 8)
     assert o2 == c2
+
+
+def test_long_context_matches_reference(cuda, native, model_dir):
+    """~3000-token prompt: chunked prefill attention over a long cache and flash-decoding with many
+    KV splits (auto split: 16 splits of 256 keys) against the fp32 torch oracle."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    ref = RefLlama.from_gguf(path)
+    rng = np.random.default_rng(9)
+    prompt = [int(t) for t in rng.integers(3, cfg.vocab, 3000)]
+    with Engine(gguf=path, max_ctx=4096, prefill_chunk=256) as eng:
+        eng.start([prompt])
+        lg = eng.logits()[0]
+        ref.reset()
+        rl = ref.forward(prompt, 0)[-1].numpy()
+        assert nmse(lg, rl) < 1e-4, nmse(lg, rl)
+        pos = len(prompt)
+        for step in range(3):
+            tok = eng.tokens()[0][-1]
+            eng.decode(1)
+            lg = eng.logits()[0]
+            rl = ref.forward([tok], pos)[-1].numpy()
+            pos += 1
+            assert nmse(lg, rl) < 1e-4, (step, nmse(lg, rl))
