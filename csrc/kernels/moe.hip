@@ -3,6 +3,7 @@
 // router writes per-expert token lists, the expert kernels read the counts and exit early for
 // idle experts, so a decode step streams only the weights of the experts actually selected.
 #include "kcommon.h"
+#include <cstdlib>
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
@@ -108,6 +109,123 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
   }
 }
 
+// Grouped GEMV v2 (decode, M <= 64 tokens): the gemv2 design per expert.  Workgroup = NW waves =
+// NW weight tiles of expert blockIdx.z; the x rows routed to that expert (gathered through its
+// slot list) are staged ONCE per workgroup in LDS per super-block (double-buffered, quarter-swapped
+// rows as in gemv2.hip), and every dequantized weight fragment feeds MT MFMA row groups (all of
+// the expert's rows in one pass: count <= M <= 16 MT).  v1 above re-streamed the expert's weights
+// for every 16 routed rows and loaded x fragments per wave.
+constexpr int MOE_LDX = 256 + 8;
+
+template <int PT, int EPI, int NW, int NSLOT, int MT>
+__global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams p) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB;
+  constexpr int NT = NW * 64;
+  constexpr int XC = 512 * MT;
+  constexpr int XCH = (XC + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) f16 xs[2][16 * MT * MOE_LDX];
+  __shared__ int s_xrow[16 * MT];
+  const int e = blockIdx.z;
+  const int count = p.counts[e];
+  if (count == 0) return;   // uniform over the workgroup
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int tile = blockIdx.x * NW + wave;
+  const int sbA = blockIdx.y * p.sb_per_split;
+  const int sbB = min(sbA + p.sb_per_split, p.nsb);
+  if (sbA >= sbB) return;
+  const int32_t* list = p.lists + (size_t)e * p.list_cap;
+  const int rows = min(count, 16 * MT);
+  for (int i = tid; i < 16 * MT; i += NT) s_xrow[i] = i < rows ? (p.x_per_slot ? list[i] : list[i] / p.k) : -1;
+  __syncthreads();
+  const uint8_t* wt = p.W + (size_t)e * p.estride + (size_t)min(tile, p.ntiles - 1) * p.nsb * CB;
+
+  u32x4 xv[NSLOT][XCH];
+  typename D::Raw ring[NSLOT];
+  const int last = sbB - 1;
+  auto issue = [&](const int sl, const int sb) {
+    D::load(ring[sl], wt + (size_t)sb * CB, lane);
+#pragma unroll
+    for (int j = 0; j < XCH; ++j) {
+      const int c = tid + NT * j;
+      if (c < XC) {
+        const int row = c >> 5, col = (c & 31) * 8;
+        const int xr = s_xrow[row];
+        xv[sl][j] = xr >= 0 ? *reinterpret_cast<const u32x4*>(p.X + (size_t)xr * p.ldx + (size_t)sb * 256 + col)
+                            : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  auto store_x = [&](const int sl, const int buf) {
+#pragma unroll
+    for (int j = 0; j < XCH; ++j) {
+      const int c = tid + NT * j;
+      if (c < XC) {
+        const int row = c >> 5, col = (c & 31) * 8;
+        *reinterpret_cast<u32x4*>(&xs[buf][row * MOE_LDX + (col ^ x_qswap(row))]) = xv[sl][j];
+      }
+    }
+  };
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sbA + sl, last));
+  store_x(0, 0);
+  __syncthreads();
+  const f16* xrow0 = &xs[0][r * MOE_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
+  const f16* xrow1 = &xs[1][r * MOE_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
+  auto step = [&](const int sl, const int cur) {
+    const int buf = (cur - sbA) & 1;
+    const f16* xr = buf ? xrow1 : xrow0;
+    half8_t b[4];
+    D::template dequant<0>(ring[sl], b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 8 * s), b[s], acc[mt]);
+    D::template dequant<1>(ring[sl], b, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 32 + 8 * s), b[s], acc[mt]);
+    store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
+    issue(sl, min(cur + NSLOT, last));
+    __syncthreads();
+  };
+  int sb = sbA;
+  for (; sb + NSLOT <= sbB; sb += NSLOT) {
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) step(sl, sb + sl);
+  }
+#pragma unroll
+  for (int sl = 0; sl < NSLOT - 1; ++sl)
+    if (sb + sl < sbB) step(sl, sb + sl);
+  if (tile >= p.ntiles) return;
+  // lane holds C[m = 16 mt + 4g + i][n = 16*tile + r]; row m = the expert's m-th routed slot
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 16 * mt + 4 * g + i;
+      if constexpr (EPI == EPI_SWIGLU) {
+        const float other = __shfl_xor(acc[mt][i], 8);
+        const int o = tile * 8 + r;
+        if (r < 8 && m < rows && o < p.n_valid) p.H[(size_t)list[m] * p.ldh + o] = (f16)(silu(acc[mt][i]) * other);
+      } else {
+        const int n = tile * 16 + r;
+        if (m < rows && n < p.n_valid) {
+          const int slot = list[m];
+          unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[mt][i]);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace mpk
 
 namespace mp {
@@ -116,8 +234,32 @@ void launch_moe_route(const MoeRouteParams& p, hipStream_t st) {
   hipLaunchKernelGGL(mpk::moe_route_kernel, dim3(1), dim3(256), 0, st, p);
 }
 
+template <int PT, int EPI, int MT>
+static void moe2_go(const MoeGemvParams& p, int nsplit, hipStream_t st) {
+  constexpr int NW = 8;
+  // super-blocks in flight: as gemv2 (<= 128 VGPRs), one less per extra row group
+  constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+  constexpr int NSL = MT == 1 ? NS : MT == 2 ? (NS > 2 ? NS - 1 : 2) : 2;
+  const dim3 grid((p.ntiles + NW - 1) / NW, nsplit, p.E);
+  hipLaunchKernelGGL((mpk::moe_gemv2_kernel<PT, EPI, NW, NSL, MT>), grid, dim3(NW * 64), 0, st, p);
+}
+
+template <int PT, int EPI>
+static void moe2_mt(const MoeGemvParams& p, int nsplit, hipStream_t st) {
+  if (p.M <= 16) moe2_go<PT, EPI, 1>(p, nsplit, st);
+  else if (p.M <= 32) moe2_go<PT, EPI, 2>(p, nsplit, st);
+  else if (p.M <= 48) moe2_go<PT, EPI, 3>(p, nsplit, st);
+  else moe2_go<PT, EPI, 4>(p, nsplit, st);
+}
+
 template <int PT>
 static void moe_launch_pt(int epi, const MoeGemvParams& p, int nsplit, hipStream_t st) {
+  static const bool v1 = [] { const char* e = getenv("MIPIPE_MOE_V"); return e && atoi(e) == 1; }();
+  if (!v1 && p.M >= 1 && p.M <= 64) {   // every expert's rows fit one pass of <= 4 row groups
+    if (epi == EPI_SWIGLU) moe2_mt<PT, EPI_SWIGLU>(p, nsplit, st);
+    else moe2_mt<PT, EPI_ATOMIC>(p, nsplit, st);
+    return;
+  }
   dim3 grid(p.ntiles, nsplit, p.E);
   if (epi == EPI_SWIGLU) hipLaunchKernelGGL((mpk::moe_gemv_kernel<PT, EPI_SWIGLU>), grid, dim3(64), 0, st, p);
   else hipLaunchKernelGGL((mpk::moe_gemv_kernel<PT, EPI_ATOMIC>), grid, dim3(64), 0, st, p);

@@ -557,7 +557,9 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
 
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
   const int E = cfg_.n_expert, k = cfg_.n_expert_used, d = cfg_.d_model, F = cfg_.d_ff;
-  gemv(L.ex.router, EPI_STORE, xn_, Kd_, M, moe_logits_, 64, nullptr, 0, E, false, st);
+  // router logits [M][E]: one 16-row tile, so split-K over the super-blocks (atomics into the
+  // buffer the ffn RMSNorm cleared) instead of one serial workgroup (28.5 us -> a few us per layer)
+  gemv(L.ex.router, EPI_ATOMIC, xn_, Kd_, M, moe_logits_, 64, nullptr, 0, E, true, st);
   MoeRouteParams rp{};
   rp.logits = moe_logits_; rp.ld = 64; rp.M = M; rp.E = E; rp.k = k;
   rp.counts = moe_counts_; rp.lists = moe_lists_; rp.list_cap = scratch_rows_ * k; rp.weights = moe_w_;
@@ -567,7 +569,7 @@ void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
   gp.ntiles = (int)L.ex.gateup.dims.ntiles; gp.nsb = (int)L.ex.gateup.dims.nsb;
   gp.X = xn_; gp.ldx = Kd_; gp.x_per_slot = 0; gp.k = k;
   gp.counts = moe_counts_; gp.lists = moe_lists_; gp.list_cap = rp.list_cap; gp.E = E;
-  gp.H = moe_h_; gp.ldh = Kff_; gp.n_valid = F;
+  gp.H = moe_h_; gp.ldh = Kff_; gp.n_valid = F; gp.M = M;
   launch_moe_gemv(L.ex.gateup.ptype, EPI_SWIGLU, gp, 1, st);
   MoeGemvParams dp = gp;
   dp.W = L.ex.down.d; dp.estride = L.ex.down_stride;
@@ -576,7 +578,10 @@ void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
   dp.Y = x; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
   // only ~k/E of the expert grid is busy: size the split for the active experts
   const int active = std::min(E, M * k);
-  const int nsplit = std::max(1, std::min(dp.nsb / 4, 4096 / std::max(1, dp.ntiles * active)));
+  // v1 (prefill, M > 64): one tile per 1-wave workgroup, ~4096 of them; v2 (decode): 8-tile
+  // workgroups, ~1024 of them across the active experts
+  const int nsplit = M <= 64 ? std::max(1, std::min(dp.nsb / 4, 1024 / std::max(1, (dp.ntiles + 7) / 8 * active)))
+                             : std::max(1, std::min(dp.nsb / 4, 4096 / std::max(1, dp.ntiles * active)));
   launch_moe_gemv(L.ex.down.ptype, EPI_ATOMIC, dp, nsplit, st);
 }
 
@@ -633,7 +638,8 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     }
   }
   gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
-  launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+  // MoE: the same launch clears the router logits, which the router GEMV then accumulates split-K
+  launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
   if (L.moe) {
     moe_ffn(L, M, st, x);
     return;

@@ -39,7 +39,9 @@ inline int gemv_auto_split(int ntiles, int nsb, int M, int epi) {
   const int target_waves = (M > 32 ? 2048 : 4096) / tpw;
   const int waves = (ntiles + tpw - 1) / tpw;
   int s = (target_waves + waves - 1) / waves;
-  const int smax = nsb / 4 > 1 ? nsb / 4 : 1;
+  // >= 4 super-blocks per split, except for a handful of tiles (MoE router: one tile), where
+  // the serial super-block loop of a single workgroup would dominate
+  const int smax = ntiles <= 4 ? nsb : (nsb / 4 > 1 ? nsb / 4 : 1);
   return s < 1 ? 1 : (s > smax ? smax : s);
 }
 void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, int ldo, hipStream_t st);
@@ -166,6 +168,7 @@ struct MoeGemvParams {
   const float* weights;
   int n_valid;
   int sb_per_split;      // set by the launcher
+  int M = 0;             // tokens of the call (bound on rows per expert); 1..64 -> workgroup-shared x kernel
 };
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
 void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st);
