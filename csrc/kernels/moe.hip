@@ -176,6 +176,9 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
   __syncthreads();
   const f16* xrow0 = &xs[0][r * MOE_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
   const f16* xrow1 = &xs[1][r * MOE_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
+  // row groups holding routed rows (uniform over the workgroup): with ~M k / E rows per expert,
+  // most experts need 1-2 of the MT groups sized for the worst case
+  const int mte = (rows + 15) >> 4;
   auto step = [&](const int sl, const int cur) {
     const int buf = (cur - sbA) & 1;
     const f16* xr = buf ? xrow1 : xrow0;
@@ -185,13 +188,13 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 8 * s), b[s], acc[mt]);
+        if (mt == 0 || mt < mte) acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 8 * s), b[s], acc[mt]);
     D::template dequant<1>(ring[sl], b, lane);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 32 + 8 * s), b[s], acc[mt]);
+        if (mt == 0 || mt < mte) acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 32 + 8 * s), b[s], acc[mt]);
     store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
     issue(sl, min(cur + NSLOT, last));
     __syncthreads();
