@@ -556,18 +556,28 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
 }
 
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
+  // prompt chunks run in slices of <= 64 tokens, so every slice takes the workgroup-shared MoE
+  // GEMV (weights streamed once per 64 tokens, not once per 16 routed rows as in v1)
+  const bool v1 = [] { const char* e = getenv("MIPIPE_MOE_V"); return e && atoi(e) == 1; }();
+  const int step = v1 ? M : 64;
+  for (int r0 = 0; r0 < M; r0 += step) moe_ffn_rows(L, r0, std::min(step, M - r0), st, x);
+}
+
+void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x) {
   const int E = cfg_.n_expert, k = cfg_.n_expert_used, d = cfg_.d_model, F = cfg_.d_ff;
+  const f16* xn = xn_ + (size_t)r0 * Kd_;
+  float* logits = moe_logits_ + (size_t)r0 * 64;
   // router logits [M][E]: one 16-row tile, so split-K over the super-blocks (atomics into the
   // buffer the ffn RMSNorm cleared) instead of one serial workgroup (28.5 us -> a few us per layer)
-  gemv(L.ex.router, EPI_ATOMIC, xn_, Kd_, M, moe_logits_, 64, nullptr, 0, E, true, st);
+  gemv(L.ex.router, EPI_ATOMIC, xn, Kd_, M, logits, 64, nullptr, 0, E, true, st);
   MoeRouteParams rp{};
-  rp.logits = moe_logits_; rp.ld = 64; rp.M = M; rp.E = E; rp.k = k;
+  rp.logits = logits; rp.ld = 64; rp.M = M; rp.E = E; rp.k = k;
   rp.counts = moe_counts_; rp.lists = moe_lists_; rp.list_cap = scratch_rows_ * k; rp.weights = moe_w_;
   launch_moe_route(rp, st);
   MoeGemvParams gp{};
   gp.W = L.ex.gateup.d; gp.estride = L.ex.gateup_stride;
   gp.ntiles = (int)L.ex.gateup.dims.ntiles; gp.nsb = (int)L.ex.gateup.dims.nsb;
-  gp.X = xn_; gp.ldx = Kd_; gp.x_per_slot = 0; gp.k = k;
+  gp.X = xn; gp.ldx = Kd_; gp.x_per_slot = 0; gp.k = k;
   gp.counts = moe_counts_; gp.lists = moe_lists_; gp.list_cap = rp.list_cap; gp.E = E;
   gp.H = moe_h_; gp.ldh = Kff_; gp.n_valid = F; gp.M = M;
   launch_moe_gemv(L.ex.gateup.ptype, EPI_SWIGLU, gp, 1, st);
@@ -575,11 +585,11 @@ void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
   dp.W = L.ex.down.d; dp.estride = L.ex.down_stride;
   dp.ntiles = (int)L.ex.down.dims.ntiles; dp.nsb = (int)L.ex.down.dims.nsb;
   dp.X = moe_h_; dp.ldx = Kff_; dp.x_per_slot = 1; dp.H = nullptr; dp.ldh = 0;
-  dp.Y = x; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
+  dp.Y = x + (size_t)r0 * d; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
   // only ~k/E of the expert grid is busy: size the split for the active experts
   const int active = std::min(E, M * k);
-  // v1 (prefill, M > 64): one tile per 1-wave workgroup, ~4096 of them; v2 (decode): 8-tile
-  // workgroups, ~1024 of them across the active experts
+  // v1 (M > 64): one tile per 1-wave workgroup, ~4096 of them; v2: 8-tile workgroups, ~1024 of
+  // them across the active experts
   const int nsplit = M <= 64 ? std::max(1, std::min(dp.nsb / 4, 1024 / std::max(1, (dp.ntiles + 7) / 8 * active)))
                              : std::max(1, std::min(dp.nsb / 4, 4096 / std::max(1, dp.ntiles * active)));
   launch_moe_gemv(L.ex.down.ptype, EPI_ATOMIC, dp, nsplit, st);

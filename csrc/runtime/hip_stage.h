@@ -123,6 +123,7 @@ class HipStage : public Stage {
   void layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* kvlen, const int32_t* slot,
                      bool decode, hipStream_t st);
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
+  void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
             int n_valid, bool allow_split, hipStream_t st);
   void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
