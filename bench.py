@@ -69,7 +69,7 @@ def main():
     n_mb = args.n_mb or world
     max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
     cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
-               prefill_chunk=256, graphs=not args.no_graphs, split="cost", seed=1234)
+               prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
     for kv in args.set:
         k, v = kv.split("=", 1)
         cfg[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)

@@ -83,7 +83,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   B_ = std::max(1, j.get_int("mb_size", 1));
   if (B_ > 64) throw std::runtime_error("mb_size > 64 not supported (the decode GEMV holds at most 4 MFMA row groups)");
   max_ctx_ = (int)round_up(std::max(64, j.get_int("max_ctx", 2048)), 64);
-  chunk_ = std::max(16, j.get_int("prefill_chunk", 256));
+  chunk_ = std::max(16, j.get_int("prefill_chunk", 512));
   const std::string ftype = j.get_str("ftype", "Q4_K_M");
   const uint64_t seed = (uint64_t)j.get_num("seed", 1234);
 

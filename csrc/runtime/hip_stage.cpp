@@ -530,7 +530,11 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
                     int n_valid, bool allow_split, hipStream_t st) {
   // up to 64 rows (decode micro-batches, short prompt chunks): the dequant GEMV, 1-4 MFMA row
   // groups per weight fragment; longer prompt chunks: MFMA GEMM, weights read once per 64 rows
-  if (M > 64 && opt_.prefill_gemm) {
+  // exception: the large gate/up GEMVs that run two tiles per wave (>= 192 workgroups of 16
+  // tiles) beat the 64x64-tile GEMM per 64 rows (70B: 4 x 73.6 us vs 410 us per 256-row chunk;
+  // profiles/r1g_prefill_gemm_vs_gemv.txt)
+  const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
+  if (M > 64 && opt_.prefill_gemm && !wide_swiglu) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;

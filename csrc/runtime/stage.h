@@ -19,7 +19,7 @@ struct StageOptions {
   int n_mb = 1;             // micro-batches in flight
   int mb_size = 1;          // sequences per micro-batch
   int max_ctx = 2048;       // KV capacity per sequence (multiple of 64)
-  int prefill_chunk = 256;  // max tokens per prefill chunk
+  int prefill_chunk = 512;  // max tokens per prefill chunk (8B: 31.5k prompt tok/s vs 24.3k at 256)
   bool use_graphs = true;
   int attn_split_len = 0;   // decode flash-decoding split length (multiple of 128; 0 = auto)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
