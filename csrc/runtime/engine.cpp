@@ -82,7 +82,10 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   M_ = std::max(1, j.get_int("n_mb", 1));
   B_ = std::max(1, j.get_int("mb_size", 1));
   if (B_ > 64) throw std::runtime_error("mb_size > 64 not supported (the decode GEMV holds at most 4 MFMA row groups)");
-  max_ctx_ = (int)round_up(std::max(64, j.get_int("max_ctx", 2048)), 64);
+  // max_ctx 0 or "auto": sized from HBM capacity after partitioning (below)
+  const bool auto_ctx = (j.has("max_ctx") && j["max_ctx"].is_str() && j["max_ctx"].str() == "auto") ||
+                        (j.has("max_ctx") && j["max_ctx"].is_num() && j["max_ctx"].num() == 0);
+  max_ctx_ = auto_ctx ? 2048 : (int)round_up(std::max(64, j.get_int("max_ctx", 2048)), 64);
   chunk_ = std::max(16, j.get_int("prefill_chunk", 512));
   const std::string ftype = j.get_str("ftype", "Q4_K_M");
   const uint64_t seed = (uint64_t)j.get_num("seed", 1234);
@@ -130,6 +133,42 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   }
   if (mode_ == "mp") devices[rank_] = j.get_int("device", devices[rank_]);
   for (int s = 0; s < S_; ++s) specs_[s].device = devices[s];
+  if (auto_ctx) {
+    // KV sized from HBM (288 GB per MI355X): every rank derives the same value from
+    // the partition and the device capacity alone (no exchange needed in mp mode): the heaviest
+    // stage's weights (+ embedding on stage 0, head on the last) and the most layers per stage
+    // bound the per-slot context; kv_frac of the card, minus a reserve for activations/scratch.
+    const double frac = j.get_num("kv_frac", 0.9);
+    double cap_bytes = 64.0 * (1 << 30);   // CPU backend: 64 GiB
+    if (!cpu_) {
+      size_t fr = 0, tot = 0;
+      HIP_OK(hipSetDevice(devices[mode_ == "mp" ? rank_ : 0]));
+      HIP_OK(hipMemGetInfo(&fr, &tot));
+      cap_bytes = (double)tot;
+    }
+    const double embd_bytes = gguf_ && gguf_->tensor("token_embd.weight")
+                                  ? (double)gguf_->tensor("token_embd.weight")->nbytes : head_cost;
+    double wmax = 0;
+    int lmax = 1;
+    for (auto& sp : specs_) {
+      double w = 0;
+      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li];
+      if (sp.first()) w += embd_bytes;
+      if (sp.last()) w += head_cost;
+      wmax = std::max(wmax, w);
+      lmax = std::max(lmax, sp.layer_end - sp.layer_begin);
+    }
+    const double per_tok = (double)lmax * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : 2.0);
+    const double reserve = 4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4;
+    const double budget = frac * cap_bytes - wmax - reserve;
+    long ctx = budget > 0 ? (long)(budget / (per_tok * M_ * B_)) : 0;
+    const long train = cfg_.n_ctx_train > 0 ? cfg_.n_ctx_train : 131072;
+    ctx = std::min(ctx, std::min(train, (long)j.get_int("max_ctx_cap", 1 << 20)));
+    if (ctx < 64) throw std::runtime_error("max_ctx auto: no HBM left for the KV cache");
+    max_ctx_ = (int)(ctx / 64 * 64);
+    MP_LOGI("max_ctx auto: %d tokens per sequence (%d slots, %.1f GiB KV per stage of %d layers; device %.0f GiB)",
+            max_ctx_, M_ * B_, per_tok * max_ctx_ * M_ * B_ / 1073741824.0, lmax, cap_bytes / 1073741824.0);
+  }
   for (auto& sp : specs_)
     MP_LOGI("partition: stage %d <- layers [%d, %d) (%d layers)%s%s", sp.stage, sp.layer_begin, sp.layer_end,
             sp.layer_end - sp.layer_begin, sp.first() ? " +embd" : "", sp.last() ? " +head" : "");

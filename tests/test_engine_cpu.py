@@ -328,3 +328,13 @@ def test_cpu_prefix_cache_multiturn(native, model_dir, stages):
         c2, _ = eng.generate([p2], 9)
         assert eng.health()["prefix_reused_tokens"] == 0
     assert o2 == c2
+
+
+def test_cpu_max_ctx_auto(native, model_dir):
+    """max_ctx 0 (llama.cpp -c 0): sized from memory, capped by the model's training context."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with Engine(gguf=path, backend="cpu", max_ctx=0, mb_size=2) as eng:
+        assert eng.info["max_ctx"] == cfg.n_ctx_train
+        out, _ = eng.generate([[5, 6, 7]], 4)
+        assert len(out[0]) == 4

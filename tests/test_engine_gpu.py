@@ -342,3 +342,21 @@ def test_long_context_matches_reference(cuda, native, model_dir):
             rl = ref.forward([tok], pos)[-1].numpy()
             pos += 1
             assert nmse(lg, rl) < 1e-4, (step, nmse(lg, rl))
+
+
+def test_max_ctx_auto_fills_hbm(cuda, native):
+    """max_ctx "auto" sizes the per-stage KV cache from the card's HBM: Llama-3-8B geometry with a
+    128K training context and 64 sequence slots gets tens of thousands of tokens per sequence."""
+    from mipipe.engine import Engine
+    syn = dict(n_layer=32, d_model=4096, n_head=32, n_head_kv=8, d_ff=14336, vocab=128256, rope_base=500000.0,
+               n_ctx_train=131072)
+    total = torch.cuda.get_device_properties(0).total_memory
+    with Engine(synthetic=syn, ftype="Q4_K_M", max_ctx="auto", mb_size=64, graphs=False) as eng:
+        ctx = eng.info["max_ctx"]
+        kv = eng.info["kv_bytes_local"]
+        assert 1024 <= ctx <= 131072 and ctx % 64 == 0
+        assert kv < 0.9 * total
+        if total > 200 * (1 << 30):   # MI355X: 288 GB
+            assert kv > 0.5 * total, (ctx, kv, total)
+        eng.start([[5, 6, 7]])
+        eng.decode(2)
