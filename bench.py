@@ -49,7 +49,9 @@ def main():
     ap.add_argument("--model", default="llama3-70b", choices=sorted(MODELS))
     ap.add_argument("--ftype", default="Q4_K")
     ap.add_argument("--mb-size", type=int, default=64, help="sequences per micro-batch (<= 64; > 16 runs the decode projections on the MFMA GEMM)")
-    ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = #GPUs)")
+    ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = pipeline depth)")
+    ap.add_argument("--pp", type=int, default=0,
+                    help="pipeline depth (default: = #GPUs); --pp P < N runs N/P data-parallel pipeline replicas")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--link", default="rccl", choices=["rccl", "tcp"], help="stage-to-stage transport (N > 1)")
@@ -66,7 +68,12 @@ def main():
             sys.exit(2)
     from mipipe.parallel import init_from_torchrun
 
-    n_mb = args.n_mb or world
+    pp = args.pp or world
+    if world % pp:
+        print(f"bench.py: --pp {pp} does not divide {world} GPUs", file=sys.stderr)
+        sys.exit(2)
+    replicas = world // pp
+    n_mb = args.n_mb or pp
     max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
     cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
                prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
@@ -75,7 +82,7 @@ def main():
         cfg[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
     # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
     # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
-    eng = init_from_torchrun(link=args.link, **cfg)
+    eng = init_from_torchrun(pp=pp, link=args.link, **cfg)
     g = torch.Generator().manual_seed(0)
     prompts = torch.randint(3, MODELS[args.model]["vocab"], (n_mb * args.mb_size, args.prompt_len),
                             generator=g).tolist()
@@ -100,7 +107,7 @@ def main():
     if world > 1:
         dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
     ms, p50 = float(vals[0]), float(vals[1])
-    n_tok = args.steps * n_mb * args.mb_size
+    n_tok = args.steps * n_mb * args.mb_size * replicas
     value = n_tok / (ms / 1e3)
     if rank == 0:
         m = MODELS[args.model]
@@ -118,8 +125,9 @@ def main():
             "vs_baseline": round(value / BASELINE_TOK_S, 2) if args.model == "llama3-70b" else None,
             "dtype": "bf16-class: f16 MFMA on dequantized " + args.ftype + " weights, f32 accumulate",
             "data": "synthetic prompts, random-init weights (GGUF " + args.ftype + " blocks generated in HBM)",
-            "config": {"model": f"{m['name']} {args.ftype}", "global_batch": n_mb * args.mb_size,
-                       "seq_len": args.prompt_len, "parallelism": f"pp{world}",
+            "config": {"model": f"{m['name']} {args.ftype}", "global_batch": n_mb * args.mb_size * replicas,
+                       "seq_len": args.prompt_len,
+                       "parallelism": f"pp{pp}" if replicas == 1 else f"dp{replicas}xpp{pp}",
                        "micro_batches": n_mb, "mb_size": args.mb_size, "max_ctx": max_ctx,
                        "stages": eng.info["stages"]},
         }), flush=True)

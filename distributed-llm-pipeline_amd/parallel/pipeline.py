@@ -10,7 +10,9 @@ The pipeline itself (stage workers, links, the micro-batched piped ring) is C++
   of micro-batches for given per-stage and per-link times (D1, the piped ring).
 * init_from_torchrun: one process per GPU. It reads torchrun's RANK, WORLD_SIZE and LOCAL_RANK,
   sets up the RCCL unique ids of the ring's links over torch.distributed, and builds an
-  Engine(mode="mp"). This is the MI355X form of prima.cpp's --world/--rank launch (D11).
+  Engine(mode="mp"). This is the MI355X form of prima.cpp's --world/--rank launch (D11). With
+  pp < world it runs world/pp data-parallel replicas of a pp-stage pipeline (SURVEY.md 2.4,
+  "replica DP, e.g. 2 x PP4").
 """
 from __future__ import annotations
 
@@ -82,13 +84,18 @@ def simulate_piped_ring(stage_ms, n_mb: int, rounds: int = 16, link_ms: float = 
                 bubble=max(0.0, 1.0 - n_mb * max(stage_ms) / round_ms))
 
 
-def init_from_torchrun(**cfg):
-    """Build this rank's Engine stage of a one-process-per-GPU pipeline under torchrun.
+def init_from_torchrun(pp: int | None = None, **cfg):
+    """Build this rank's Engine stage under torchrun, with one process per GPU.
 
-    The ring has one link per rank: rank r sends to rank (r+1) % N. The sender of each link creates
-    its RCCL unique id, and the ids are exchanged with torch.distributed (backend "nccl", which is
-    RCCL on ROCm). A world size of 1 gives a local single-stage engine. Keyword arguments are engine
-    config keys (see mipipe.engine).
+    `pp` is the pipeline depth (default: the world size). The world splits into world // pp
+    independent replicas of a pp-stage pipeline: data parallelism across replicas, pipeline
+    parallelism within each. Replica g holds ranks [g*pp, (g+1)*pp). With pp = 1 every rank runs the
+    whole model on its own GPU.
+
+    Inside a replica the ring has one link per rank: stage r sends to stage (r+1) % pp. The sender
+    of each link creates its RCCL unique id, and the ids are exchanged with torch.distributed
+    (backend "nccl", which is RCCL on ROCm). Keyword arguments are engine config keys (see
+    mipipe.engine).
     """
     import torch
     import torch.distributed as dist
@@ -98,26 +105,32 @@ def init_from_torchrun(**cfg):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    pp = int(pp or world)
+    if pp < 1 or world % pp:
+        raise ValueError(f"pipeline depth {pp} does not divide the world size {world}")
+    group, stage = divmod(rank, pp)
     link = cfg.pop("link", "rccl")
-    if cfg.get("backend", "hip") == "cpu":
+    cpu = cfg.get("backend", "hip") == "cpu"
+    if cpu:
         link = "tcp"   # RCCL moves device buffers; CPU stages talk over TCP
-    if cfg.get("backend", "hip") != "cpu":
+    else:
         torch.cuda.set_device(local_rank)
-    if world == 1:
+    if world > 1 and not dist.is_initialized():
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if pp == 1:
         cfg.setdefault("mode", "local")
         cfg.setdefault("stages", 1)
         cfg.setdefault("devices", [local_rank])
         return Engine(**cfg)
-    if not dist.is_initialized():
-        if cfg.get("backend", "hip") == "cpu":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    cfg.update(mode="mp", world=world, rank=rank, device=local_rank, link=link)
+    cfg.update(mode="mp", world=pp, rank=stage, device=local_rank, link=link)
     if link == "rccl":
         ids = [None] * world
         dist.all_gather_object(ids, rccl_unique_id_hex())
-        cfg["rccl_ids"] = ids
+        cfg["rccl_ids"] = ids[group * pp:(group + 1) * pp]
     else:
-        cfg.setdefault("base_port", int(os.environ.get("MASTER_PORT", "29500")) + 11)
+        base = cfg.pop("base_port", int(os.environ.get("MASTER_PORT", "29500")) + 11)
+        cfg["base_port"] = base + group * pp   # each replica's ring on its own ports
     return Engine(**cfg)

@@ -50,10 +50,11 @@ import json, sys
 sys.path.insert(0, {repo!r})
 from mipipe.parallel import init_from_torchrun
 import torch.distributed as dist
-eng = init_from_torchrun(gguf={path!r}, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16,
+eng = init_from_torchrun(pp={pp}, gguf={path!r}, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16,
                          split="even", base_port={port})
 out, _ = eng.generate({prompts!r}, 6)
 stages = eng.info["stages"]
+last = eng.info["stages"][-1]["stage"]
 eng.close()
 dist.barrier()
 print("OUT " + json.dumps(dict(rank=dist.get_rank(), out=out, stages=stages)), flush=True)
@@ -61,7 +62,10 @@ dist.destroy_process_group()
 """
 
 
-def test_init_from_torchrun_two_processes(native, model_dir, tmp_path):
+@pytest.mark.parametrize("world,pp", [(2, 2), (4, 2), (2, 1)])
+def test_init_from_torchrun_replicas(native, model_dir, tmp_path, world, pp):
+    """world / pp data-parallel replicas of a pp-stage pipeline (CPU stages, TCP rings, gloo
+    rendezvous): every replica's last stage produces the single-process tokens."""
     from mipipe.engine import Engine
     from test_engine_cpu import free_port
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
@@ -69,12 +73,12 @@ def test_init_from_torchrun_two_processes(native, model_dir, tmp_path):
     with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16) as eng:
         ref, _ = eng.generate(prompts, 6)
     script = tmp_path / "run.py"
-    script.write_text(_SCRIPT.format(repo=REPO, path=path, prompts=prompts, port=free_port()))
+    script.write_text(_SCRIPT.format(repo=REPO, path=path, prompts=prompts, port=free_port(), pp=pp))
     mport = free_port()
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(mport))
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(mport), OMP_NUM_THREADS="2")
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=240) for p in procs]
@@ -83,5 +87,7 @@ def test_init_from_torchrun_two_processes(native, model_dir, tmp_path):
         assert p.returncode == 0, e[-2000:]
         d = json.loads([l for l in o.splitlines() if l.startswith("OUT ")][-1][4:])
         res[d["rank"]] = d
-    assert [(s["layer_begin"], s["layer_end"]) for s in res[1]["stages"]] == [(0, 2), (2, 4)]
-    assert res[1]["out"] == ref   # the last stage's process holds the generated tokens
+    for g in range(world // pp):
+        last = res[g * pp + pp - 1]
+        assert len(last["stages"]) == pp
+        assert last["out"] == ref   # the replica's last stage holds the generated tokens
