@@ -222,7 +222,9 @@ static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
   if (g_tw2) return g_tw2;
   // two tiles per wave halve the workgroups: only where >= 192 remain (70B gate/up: 224;
   // 8B gate/up would drop to 112 of 256 CUs)
-  return epi == EPI_SWIGLU && ntiles / (2 * g_nw) >= 192 ? 2 : 1;
+  // (split-free epilogues only: the split-K projections gain nothing; the Q6_K LM head at M = 64:
+  // 294 -> 266 us)
+  return (epi == EPI_SWIGLU || epi == EPI_STORE) && ntiles / (2 * g_nw) >= 192 ? 2 : 1;
 }
 static int gemv_version() {
   if (g_ver < 0) {
