@@ -360,3 +360,24 @@ def test_max_ctx_auto_fills_hbm(cuda, native):
             assert kv > 0.5 * total, (ctx, kv, total)
         eng.start([[5, 6, 7]])
         eng.decode(2)
+
+
+def test_bench_contract_line(cuda, native):
+    """bench.py prints ONE JSON line with the driver's keys (small model, few steps)."""
+    import json as _json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--model", "tinyllama", "--ftype", "Q4_K_M",
+                        "--steps", "3", "--warmup", "1", "--mb-size", "4", "--prompt-len", "16"],
+                       capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = _json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["value"] > 0
+    assert d["config"]["parallelism"] == "pp1" and d["config"]["global_batch"] == 4
