@@ -432,6 +432,27 @@ int mp_engine_start(void* h, const int32_t* prompt_tokens, const int32_t* lens, 
   return 0;
   API_CATCH(-1)
 }
+// continuous batching: prefill prompts into the given sequence slots between decode rounds
+int mp_engine_admit(void* h, const int32_t* slots, const int32_t* prompt_tokens, const int32_t* lens, int n_seq) {
+  API_TRY
+  std::vector<std::vector<int32_t>> prompts;
+  std::vector<int> sl;
+  size_t off = 0;
+  for (int i = 0; i < n_seq; ++i) {
+    prompts.emplace_back(prompt_tokens + off, prompt_tokens + off + lens[i]);
+    off += lens[i];
+    sl.push_back(slots[i]);
+  }
+  static_cast<Engine*>(h)->admit(sl, prompts);
+  return 0;
+  API_CATCH(-1)
+}
+int mp_engine_release(void* h, int slot) {
+  API_TRY
+  static_cast<Engine*>(h)->release(slot);
+  return 0;
+  API_CATCH(-1)
+}
 const char* mp_engine_decode(void* h, int k) {
   API_TRY
   StepStats ss = static_cast<Engine*>(h)->decode_steps(k);
@@ -448,9 +469,9 @@ const char* mp_engine_decode(void* h, int k) {
 int mp_engine_tokens(void* h, int32_t* out, int n_seq, int cap) {
   API_TRY
   auto t = static_cast<Engine*>(h)->tokens();
-  int n = cap;
+  int n = 0;   // longest sequence (rows padded with -1: admitted sequences are shorter)
   for (int i = 0; i < n_seq && i < (int)t.size(); ++i) {
-    n = std::min<int>(n, (int)t[i].size());
+    n = std::max<int>(n, std::min<int>(cap, (int)t[i].size()));
     for (int j = 0; j < cap; ++j) out[(size_t)i * cap + j] = j < (int)t[i].size() ? t[i][j] : -1;
   }
   return n;

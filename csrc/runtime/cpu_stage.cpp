@@ -528,8 +528,15 @@ void CpuStage::copy_verify_tokens(int mb, int32_t* host, int n) {
   std::memcpy(host, vtok_[mb].data(), (size_t)n * 4);
 }
 
-void CpuStage::prefill_finish(int mb, hipStream_t) {
-  if (spec_.last()) head(mb, opt_.mb_size, last_h_[mb].data(), tok_[mb].data(), 1000003ULL + (uint64_t)mb);
+void CpuStage::prefill_finish(int mb, hipStream_t, const std::vector<int>* rows) {
+  if (!spec_.last()) return;
+  if (!rows) {
+    head(mb, opt_.mb_size, last_h_[mb].data(), tok_[mb].data(), 1000003ULL + (uint64_t)mb);
+    return;
+  }
+  std::vector<int32_t> t(opt_.mb_size, 0);
+  head(mb, opt_.mb_size, last_h_[mb].data(), t.data(), 1000003ULL + (uint64_t)mb);
+  for (int b : *rows) tok_[mb][b] = t[b];
 }
 
 void CpuStage::decode(int mb, hipStream_t) {

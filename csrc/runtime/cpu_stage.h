@@ -41,7 +41,7 @@ class CpuStage : public Stage {
   int32_t* prompt_buf() override { return prompt_.data(); }
   void set_positions(int mb, const std::vector<int32_t>& pos) override;
   void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
-  void prefill_finish(int mb, hipStream_t st) override;
+  void prefill_finish(int mb, hipStream_t st, const std::vector<int>* rows = nullptr) override;
   void copy_verify_tokens(int mb, int32_t* host, int n) override;
   void decode(int mb, hipStream_t st) override;
   const float* logits_ptr() const override { return logits_.data(); }

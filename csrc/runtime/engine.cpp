@@ -426,7 +426,7 @@ void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
       }
       case Item::PREFILL_END: {
         if (last) {
-          span(w, nullptr, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, nullptr); });
+          span(w, nullptr, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, nullptr, it.rows.empty() ? nullptr : &it.rows); });
           std::memcpy(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4);
         }
         if (S_ > 1) {
@@ -444,7 +444,7 @@ void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
         span(w, nullptr, 0, "decode mb" + std::to_string(mb), [&] { st.decode(mb, nullptr); });
         if (last) {
           w.tok_t.push_back(now_ms());
-          std::memcpy(out_host_ + ((size_t)(it.round + 1) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4);
+          std::memcpy(out_host_ + ((size_t)((it.round + 1) % rounds_cap_) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4);
         }
         if (S_ > 1) {
           if (!last) send(mb, st.act(mb), (size_t)B_ * d4, "act");
@@ -510,7 +510,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
       }
       case Item::PREFILL_END: {
         if (last) {
-          span(w, cs, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, cs); });
+          span(w, cs, 0, "prefill_head mb" + std::to_string(mb), [&] { st.prefill_finish(mb, cs, it.rows.empty() ? nullptr : &it.rows); });
           HIP_OK(hipMemcpyAsync(out_host_ + (size_t)mb * B_, st.tokens(mb), (size_t)B_ * 4, hipMemcpyDeviceToHost,
                                 cs));
         }
@@ -528,7 +528,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         if (last) {
           const size_t ev_i = (size_t)(it.round - rounds_done_) * M_ + mb;
           if (ev_i < w.tok_ev.size()) HIP_OK(hipEventRecord(w.tok_ev[ev_i], cs));
-          HIP_OK(hipMemcpyAsync(out_host_ + ((size_t)(it.round + 1) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4,
+          HIP_OK(hipMemcpyAsync(out_host_ + ((size_t)((it.round + 1) % rounds_cap_) * M_ + mb) * B_, st.tokens(mb), (size_t)B_ * 4,
                                 hipMemcpyDeviceToHost, cs));
         }
         if (S_ > 1) {
@@ -690,6 +690,9 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   gen_.assign(prompts.size(), {});
   rounds_done_ = 0;
   resumable_ = true;
+  base_round_.assign((size_t)M_ * B_, 0);
+  active_.assign((size_t)M_ * B_, 0);
+  for (size_t i = 0; i < prompts.size(); ++i) active_[i] = 1;
   std::vector<Item> items;
   for (auto& w : workers_) {
     Stage& st = *w->stage;
@@ -718,43 +721,10 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
       }
     }
   }
-  // packed prefill: the prompts of a micro-batch are cut into chunks of up to chunk_ rows that may
-  // hold several sequences, so each projection reads its weights once per chunk (not per sequence)
-  for (int mb = 0; mb < M_; ++mb) {
-    Item it{Item::PREFILL};
-    it.mb = mb;
-    auto flush = [&] {
-      if (it.T > 0) items.push_back(it);
-      it.segs.clear();
-      it.T = 0;
-    };
-    for (int b = 0; b < B_; ++b) {
-      const size_t i = (size_t)mb * B_ + b;
-      if (i >= prompts.size()) continue;
-      const int n = (int)prompts[i].size();
-      // prefix cache: the slot's KV already holds the tokens of slot_toks_[i]; only the part after
-      // the common prefix is prefilled (at least the last prompt token, whose row feeds the head)
-      int reuse = 0;
-      if (prefix_cache_ && i < slot_toks_.size()) {
-        const auto& c = slot_toks_[i];
-        const size_t lim = std::min(c.size(), (size_t)n - 1);
-        while ((size_t)reuse < lim && c[reuse] == prompts[i][reuse]) ++reuse;
-      }
-      reused_tokens_ += reuse;
-      for (int p0 = reuse; p0 < n;) {
-        const int take = std::min(chunk_ - it.T, n - p0);
-        PrefillSeg sg;
-        sg.b = b; sg.p0 = p0; sg.T = take; sg.last = p0 + take >= n;
-        it.segs.push_back(sg);
-        it.T += take;
-        p0 += take;
-        if (it.T == chunk_ || !packed_prefill_) flush();
-      }
-    }
-    flush();
-    Item e{Item::PREFILL_END};
-    e.mb = mb;
-    items.push_back(e);
+  {
+    std::vector<size_t> seqs(prompts.size());
+    std::iota(seqs.begin(), seqs.end(), (size_t)0);
+    items = prefill_items(seqs, false);
   }
   slot_toks_.clear();   // KV content unknown until this prefill has completed
   run_all(items);
@@ -771,7 +741,8 @@ void Engine::refresh_slot_cache() {
   slot_toks_ = prompts_;
   if (!resumable_ || !owns_first() || !owns_last()) return;
   for (size_t i = 0; i < slot_toks_.size() && i < gen_.size(); ++i) {
-    const size_t n = std::min(gen_[i].size(), (size_t)rounds_done_);
+    const int since = rounds_done_ - (i < base_round_.size() ? base_round_[i] : 0);
+    const size_t n = std::min(gen_[i].size(), (size_t)std::max(0, since));
     slot_toks_[i].insert(slot_toks_[i].end(), gen_[i].begin(), gen_[i].begin() + n);
   }
 }
@@ -794,7 +765,8 @@ Json Engine::save_state(const std::string& dir) {
   const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_);
   // tokens already in each slot's KV: prompt + generated - 1 (the newest token is the next input)
   std::vector<int> n_tok((size_t)M_ * B_, 0);
-  for (size_t i = 0; i < prompts_.size(); ++i) n_tok[i] = (int)prompts_[i].size() + rounds_done_;
+  for (size_t i = 0; i < prompts_.size(); ++i)
+    if (i < active_.size() && active_[i]) n_tok[i] = slot_pos(i);
   size_t total = 0;
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
@@ -841,6 +813,13 @@ Json Engine::save_state(const std::string& dir) {
     }
     sj["prompts"] = ps;
     sj["generated"] = gs;
+    Json br = Json::array(), ac = Json::array();
+    for (size_t i = 0; i < prompts_.size(); ++i) {
+      br.push(i < base_round_.size() ? base_round_[i] : 0);
+      ac.push(i < active_.size() && active_[i] ? 1 : 0);
+    }
+    sj["base_round"] = br;
+    sj["active"] = ac;
     std::ofstream f(dir + "/session.json", std::ios::trunc);
     f << sj.dump() << "\n";
     if (!f) throw std::runtime_error("save_state: cannot write session.json");
@@ -876,6 +855,12 @@ Json Engine::load_state(const std::string& dir) {
   }
   rounds_done_ = sj.get_int("rounds_done", 0);
   if ((int)prompts_.size() > M_ * B_ || gen_.size() != prompts_.size()) throw std::runtime_error("load_state: bad session");
+  base_round_.assign((size_t)M_ * B_, 0);
+  active_.assign((size_t)M_ * B_, 0);
+  for (size_t i = 0; i < prompts_.size(); ++i) {
+    base_round_[i] = sj.has("base_round") ? (int)sj["base_round"].arr()[i].num() : 0;
+    active_[i] = sj.has("active") ? (char)sj["active"].arr()[i].num() : 1;
+  }
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
     if (!cpu_) HIP_OK(hipSetDevice(wp->device));
@@ -901,12 +886,9 @@ Json Engine::load_state(const std::string& dir) {
       kv += nb;
     }
     st.set_sample_step((uint64_t)h.get_num("sample_step", 0));
-    for (int mb = 0; mb < M_; ++mb) {   // next decode position: prompt + rounds (idle rows advance too)
-      std::vector<int32_t> pos(B_, rounds_done_);
-      for (int b = 0; b < B_; ++b) {
-        const size_t i = (size_t)mb * B_ + b;
-        if (i < prompts_.size()) pos[b] += (int)prompts_[i].size();
-      }
+    for (int mb = 0; mb < M_; ++mb) {   // next decode position: prompt + rounds since admission
+      std::vector<int32_t> pos(B_);
+      for (int b = 0; b < B_; ++b) pos[b] = slot_pos((size_t)mb * B_ + b);
       st.set_positions(mb, pos);
     }
     if (st.spec().first()) {
@@ -947,12 +929,141 @@ Json Engine::load_state(const std::string& dir) {
   return r;
 }
 
+
+// packed prefill of sequences `seqs` (slot indices): each micro-batch's prompts are cut into chunks
+// of up to chunk_ rows that may hold several sequences, so each projection reads its weights once
+// per chunk (not per sequence).  start(): every micro-batch gets a PREFILL_END (head over all its
+// rows); admission: only the micro-batches of admitted slots, restricted to their rows.
+std::vector<Item> Engine::prefill_items(const std::vector<size_t>& seqs, bool admission) {
+  std::vector<Item> items;
+  std::vector<std::vector<size_t>> by_mb(M_);
+  for (size_t i : seqs) by_mb[i / B_].push_back(i);
+  for (int mb = 0; mb < M_; ++mb) {
+    if (admission && by_mb[mb].empty()) continue;
+    std::sort(by_mb[mb].begin(), by_mb[mb].end());
+    Item it{Item::PREFILL};
+    it.mb = mb;
+    auto flush = [&] {
+      if (it.T > 0) items.push_back(it);
+      it.segs.clear();
+      it.T = 0;
+    };
+    for (size_t i : by_mb[mb]) {
+      const int b = (int)(i % B_);
+      const int n = (int)prompts_[i].size();
+      // prefix cache: the slot's KV already holds the tokens of slot_toks_[i]; only the part after
+      // the common prefix is prefilled (at least the last prompt token, whose row feeds the head)
+      int reuse = 0;
+      if (prefix_cache_ && i < slot_toks_.size()) {
+        const auto& c = slot_toks_[i];
+        const size_t lim = std::min(c.size(), (size_t)n - 1);
+        while ((size_t)reuse < lim && c[reuse] == prompts_[i][reuse]) ++reuse;
+      }
+      reused_tokens_ += reuse;
+      for (int p0 = reuse; p0 < n;) {
+        const int take = std::min(chunk_ - it.T, n - p0);
+        PrefillSeg sg;
+        sg.b = b; sg.p0 = p0; sg.T = take; sg.last = p0 + take >= n;
+        it.segs.push_back(sg);
+        it.T += take;
+        p0 += take;
+        if (it.T == chunk_ || !packed_prefill_) flush();
+      }
+    }
+    flush();
+    Item e{Item::PREFILL_END};
+    e.mb = mb;
+    if (admission)
+      for (size_t i : by_mb[mb]) e.rows.push_back((int)(i % B_));
+    items.push_back(e);
+  }
+  return items;
+}
+
+void Engine::push_positions(int mb) {
+  std::vector<int32_t> pos(B_);
+  for (int b = 0; b < B_; ++b) pos[b] = slot_pos((size_t)mb * B_ + b);
+  for (auto& w : workers_) {
+    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    w->stage->set_positions(mb, pos);
+  }
+}
+
+void Engine::release(int slot) {
+  if (slot >= 0 && slot < (int)active_.size()) active_[slot] = 0;
+}
+
+void Engine::admit(const std::vector<int>& slots, const std::vector<std::vector<int32_t>>& prompts) {
+  if (!started_) throw std::runtime_error("admit before start");
+  if (!resumable_) throw std::runtime_error("admit after speculative decoding");
+  if (slots.size() != prompts.size()) throw std::runtime_error("admit: one prompt per slot");
+  const size_t NS = (size_t)M_ * B_;
+  if (prompts_.size() < NS) { prompts_.resize(NS); gen_.resize(NS); }
+  base_round_.resize(NS, 0);
+  active_.resize(NS, 0);
+  std::vector<size_t> seqs;
+  std::vector<char> mbs(M_, 0);
+  for (size_t k = 0; k < slots.size(); ++k) {
+    const int i = slots[k];
+    if (i < 0 || (size_t)i >= NS) throw std::runtime_error("admit: bad slot");
+    if (active_[i]) throw std::runtime_error("admit: slot " + std::to_string(i) + " is busy");
+    if (prompts[k].empty() || (int)prompts[k].size() >= max_ctx_) throw std::runtime_error("bad prompt length");
+    prompts_[i] = prompts[k];
+    gen_[i].clear();
+    base_round_[i] = rounds_done_;
+    active_[i] = 1;
+    seqs.push_back((size_t)i);
+    mbs[i / B_] = 1;
+  }
+  for (auto& w : workers_) {
+    Stage& st = *w->stage;
+    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    if (st.spec().first())
+      for (size_t i : seqs) {
+        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
+        else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4,
+                              hipMemcpyHostToDevice));
+      }
+  }
+  for (int mb = 0; mb < M_; ++mb)
+    if (mbs[mb]) push_positions(mb);
+  std::vector<Item> items = prefill_items(seqs, true);
+  slot_toks_.clear();
+  run_all(items);
+  if (owns_last())
+    for (size_t i : seqs) gen_[i].push_back(out_host_[i]);
+  // the head pushed a token into the penalty window of every row of these micro-batches: re-seed
+  // them from the host (prompt + accepted tokens)
+  for (auto& w : workers_)
+    if (w->stage->spec().last())
+      for (int mb = 0; mb < M_; ++mb)
+        if (mbs[mb]) {
+          std::vector<std::vector<int32_t>> hs;
+          for (int b = 0; b < B_; ++b) {
+            const size_t i = (size_t)mb * B_ + b;
+            std::vector<int32_t> q = prompts_[i];
+            q.insert(q.end(), gen_[i].begin(), gen_[i].end());
+            hs.push_back(q);
+          }
+          w->stage->set_history(mb, hs);
+        }
+  refresh_slot_cache();
+}
+
 StepStats Engine::decode_steps(int k) {
   if (!started_) throw std::runtime_error("decode_steps before start");
-  size_t max_prompt = 0;
-  for (auto& p : prompts_) max_prompt = std::max(max_prompt, p.size());
-  if (rounds_done_ + k + 1 >= rounds_cap_ || (int)max_prompt + rounds_done_ + k + 1 > max_ctx_)
-    throw std::runtime_error("context capacity exhausted (prompt + generated tokens > max_ctx)");
+  if (k + 1 >= rounds_cap_) throw std::runtime_error("decode_steps: too many rounds in one call");
+  // running sequences must fit their slot's KV pages; idle rows (which still compute) restart at
+  // position 0 before they could run past them
+  for (size_t i = 0; i < (size_t)M_ * B_; ++i) {
+    const bool act = i < active_.size() && active_[i];
+    if (slot_pos(i) + k + 1 <= max_ctx_) continue;
+    if (act) throw std::runtime_error("context capacity exhausted (prompt + generated tokens > max_ctx)");
+    if (i < prompts_.size()) prompts_[i].clear();
+    if (base_round_.size() < (size_t)M_ * B_) base_round_.resize((size_t)M_ * B_, 0);
+    base_round_[i] = rounds_done_;
+    push_positions((int)(i / B_));
+  }
   for (auto& w : workers_)
     if (w->stage->spec().last() && cpu_) {
       w->tok_t.clear();
@@ -988,7 +1099,7 @@ StepStats Engine::decode_steps(int k) {
   if (owns_last())
     for (int r = 0; r < k; ++r)
       for (size_t i = 0; i < prompts_.size(); ++i) {
-        const int32_t t = out_host_[(size_t)(rounds_done_ + r + 1) * M_ * B_ + i];
+        const int32_t t = out_host_[(size_t)((rounds_done_ + r + 1) % rounds_cap_) * M_ * B_ + i];
         gen_[i].push_back(t);
         if (on_token) on_token((int)i, t);
       }

@@ -38,6 +38,7 @@ struct Item {
   int T = 0;                      // PREFILL: total rows of the packed chunk
   std::vector<PrefillSeg> segs;   // PREFILL: sequences (segments) packed into the chunk
   int round = 0;
+  std::vector<int> rows;          // PREFILL_END of an admission: only these rows get a new token
 };
 
 struct StepStats {
@@ -66,6 +67,18 @@ class Engine {
   StepStats decode_steps(int k);
   // generated tokens so far per sequence (valid where the last stage lives)
   std::vector<std::vector<int32_t>> tokens() const;
+
+  // Continuous batching: between decode rounds, prefill new sequences into the
+  // given sequence slots (slot = mb * mb_size + row) while the other slots keep their state; each
+  // admitted slot gets its first token like start().  release() marks a slot idle (its row keeps
+  // computing garbage until re-admitted; its position is recycled before it could leave the slot's
+  // KV pages).  Every process of a multi-process pipeline must make the same calls.
+  void admit(const std::vector<int>& slots, const std::vector<std::vector<int32_t>>& prompts);
+  void release(int slot);
+  int32_t last_token(int slot) const { return slot < (int)gen_.size() && !gen_[slot].empty() ? gen_[slot].back() : -1; }
+  int slot_position(int slot) const { return slot_pos((size_t)slot); }
+  bool started() const { return started_; }
+  bool slot_active(int slot) const { return slot >= 0 && slot < (int)active_.size() && active_[slot]; }
 
   Json generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict,
                 std::vector<std::vector<int32_t>>* out);
@@ -155,6 +168,14 @@ class Engine {
   std::vector<std::vector<int32_t>> slot_toks_;
   long reused_tokens_ = 0;
   void refresh_slot_cache();
+  // per slot: the round at which its sequence was admitted, and whether one is running
+  std::vector<int> base_round_;
+  std::vector<char> active_;
+  int slot_pos(size_t i) const {
+    return (i < prompts_.size() ? (int)prompts_[i].size() : 0) + rounds_done_ - (i < base_round_.size() ? base_round_[i] : 0);
+  }
+  void push_positions(int mb);
+  std::vector<Item> prefill_items(const std::vector<size_t>& seqs, bool admission);
   double load_ms_ = 0;
 };
 

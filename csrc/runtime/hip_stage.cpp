@@ -737,8 +737,15 @@ void HipStage::copy_verify_tokens(int mb, int32_t* host, int n) {
   HIP_OK(hipMemcpy(host, vtok_ + (size_t)mb * opt_.prefill_chunk, (size_t)n * 4, hipMemcpyDeviceToHost));
 }
 
-void HipStage::prefill_finish(int mb, hipStream_t st) {
-  if (spec_.last()) head(mb, opt_.mb_size, last_h_[mb], tok_[mb], 1000003ULL + (uint64_t)mb, st);
+void HipStage::prefill_finish(int mb, hipStream_t st, const std::vector<int>* rows) {
+  if (!spec_.last()) return;
+  if (!rows) {
+    head(mb, opt_.mb_size, last_h_[mb], tok_[mb], 1000003ULL + (uint64_t)mb, st);
+    return;
+  }
+  if (!tok_tmp_) tok_tmp_ = (int32_t*)dmalloc((size_t)std::max(opt_.mb_size, 16) * 4);
+  head(mb, opt_.mb_size, last_h_[mb], tok_tmp_, 1000003ULL + (uint64_t)mb, st);
+  for (int b : *rows) HIP_OK(hipMemcpyAsync(tok_[mb] + b, tok_tmp_ + b, 4, hipMemcpyDeviceToDevice, st));
 }
 
 void HipStage::decode_eager(int mb, hipStream_t st) {

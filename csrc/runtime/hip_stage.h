@@ -93,7 +93,7 @@ class HipStage : public Stage {
 
   // packed prefill chunk (see Stage::prefill) and the head over the kept last rows
   void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) override;
-  void prefill_finish(int mb, hipStream_t st) override;
+  void prefill_finish(int mb, hipStream_t st, const std::vector<int>* rows = nullptr) override;
   void copy_verify_tokens(int mb, int32_t* host, int n) override;
 
   // One decode step for micro-batch mb (graph replay if captured).
@@ -171,6 +171,7 @@ class HipStage : public Stage {
   std::vector<float*> act_;
   std::vector<int32_t*> tok_, pos_, kvlen_, slot_;
   int32_t* step_ = nullptr;
+  int32_t* tok_tmp_ = nullptr;   // row-selective prefill_finish
   // repetition-penalty windows (last stage): [n_mb][mb_size][hist_n_] token ring, -1 = empty,
   // and the per-row count of accepted tokens (ring position)
   int32_t* hist_ = nullptr;

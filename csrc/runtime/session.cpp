@@ -151,6 +151,88 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
   return res;
 }
 
+void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
+  if (!eng_.owns_first() || !eng_.owns_last()) throw std::runtime_error("serve: needs every stage in this process");
+  struct Live {
+    Served s;
+    GenResult res;
+    Utf8Acc acc;
+    int step = 0;
+    double t0 = 0, t1 = 0;
+  };
+  const int cap = capacity(), max_ctx = eng_.max_ctx();
+  std::vector<std::unique_ptr<Live>> live(cap);
+  auto consume = [&](int slot, int32_t t) -> bool {   // false: the request is finished
+    Live& L = *live[slot];
+    GenResult& r = L.res;
+    if (L.step >= L.s.req.n_predict) { r.stop = "length"; return false; }
+    if (is_eog(t)) { r.stop = "eog"; return false; }
+    r.tokens.push_back(t);
+    r.n_gen++;
+    const std::string p = L.acc.push(piece(t));
+    r.text += p;
+    ++L.step;
+    if (!p.empty() && L.s.req.on_piece && !L.s.req.on_piece(p)) { r.stop = "cancelled"; return false; }
+    if (L.step >= L.s.req.n_predict) { r.stop = "length"; return false; }
+    if (eng_.slot_position(slot) + 1 >= max_ctx) { r.stop = "context"; return false; }
+    return true;
+  };
+  auto finish = [&](int slot) {
+    Live& L = *live[slot];
+    if (!L.acc.buf.empty()) {
+      L.res.text += L.acc.buf;
+      if (L.s.req.on_piece && L.res.stop != "cancelled") L.s.req.on_piece(L.acc.buf);
+    }
+    L.res.decode_ms = now_ms() - L.t1;
+    if (L.s.done) L.s.done(L.res);
+    eng_.release(slot);
+    live[slot].reset();
+  };
+  for (;;) {
+    int free = 0;
+    for (auto& l : live) free += l ? 0 : 1;
+    std::vector<Served> fresh = free ? next(free) : std::vector<Served>{};
+    if (!fresh.empty()) {
+      if ((int)fresh.size() > free) throw std::runtime_error("serve: more requests than free slots");
+      std::vector<int> slots;
+      std::vector<std::vector<int32_t>> prompts;
+      const bool idle = free == cap;
+      for (auto& f : fresh) {
+        int sl = 0;
+        while (live[sl] || std::find(slots.begin(), slots.end(), sl) != slots.end()) ++sl;
+        std::vector<int32_t> pr = encode(f.req.prompt);
+        if ((int)pr.size() >= max_ctx) pr.erase(pr.begin(), pr.end() - (max_ctx / 2));
+        auto L = std::make_unique<Live>();
+        L->s = std::move(f);
+        L->res.n_prompt = (int)pr.size();
+        L->t0 = now_ms();
+        live[sl] = std::move(L);
+        slots.push_back(sl);
+        prompts.push_back(std::move(pr));
+      }
+      // nothing running: a plain start() of slots 0..n-1 (resets the engine's rounds)
+      if (idle && slots.back() == (int)slots.size() - 1) eng_.start(prompts);
+      else eng_.admit(slots, prompts);
+      const double t = now_ms();
+      for (int sl : slots) {
+        Live& L = *live[sl];
+        L.t1 = t;
+        L.res.prefill_ms = t - L.t0;
+        if (L.s.req.n_predict <= 0 || !consume(sl, eng_.last_token(sl))) finish(sl);
+      }
+    }
+    bool any = false;
+    for (auto& l : live) any = any || (bool)l;
+    if (!any) {
+      if (fresh.empty()) return;
+      continue;
+    }
+    eng_.decode_steps(1);
+    for (int sl = 0; sl < cap; ++sl)
+      if (live[sl] && !consume(sl, eng_.last_token(sl))) finish(sl);
+  }
+}
+
 std::string Session::perf_summary(const GenResult& r, double load_ms) {
   char b[1024];
   const int ng = std::max(0, r.n_gen - 1);   // the first token comes out of the prefill

@@ -48,6 +48,16 @@ class Session {
 
   // runs up to capacity() requests together (one sequence slot each)
   std::vector<GenResult> run(std::vector<GenRequest>& reqs);
+
+  // Continuous batching (single-process pipelines): between decode rounds, `next(free)` is asked
+  // for up to `free` new requests (non-blocking), which are admitted into idle sequence slots while
+  // the running ones keep decoding; `done(request, result)` fires as each request finishes (EOG,
+  // n_predict, cancellation, context).  Returns when nothing runs and next() has nothing.
+  struct Served {
+    GenRequest req;
+    std::function<void(GenResult&)> done;
+  };
+  void serve(const std::function<std::vector<Served>(int free)>& next);
   // llama.cpp-style summary lines (prompt eval / eval / total)
   static std::string perf_summary(const GenResult& r, double load_ms);
 

@@ -58,8 +58,10 @@ class Stage {
   // stage embeds the tokens from prompt_buf(); for a segment with `last` set, the last stage
   // keeps the final row's hidden state for prefill_finish().
   virtual void prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t st) = 0;
-  // last stage: LM head + sampling over the kept rows -> tokens(mb)[b] for every sequence of mb
-  virtual void prefill_finish(int mb, hipStream_t st) = 0;
+  // last stage: LM head + sampling over the kept rows -> tokens(mb)[b] for every sequence of mb;
+  // with `rows`, only those rows' tokens change (continuous batching admits sequences into some
+  // rows while the others are mid-generation)
+  virtual void prefill_finish(int mb, hipStream_t st, const std::vector<int>* rows = nullptr) = 0;
   virtual void decode(int mb, hipStream_t st) = 0;
   // last stage, after a prefill() of verify segments of micro-batch mb: the greedy next token after
   // each of the chunk's n rows (row order = segment order) -> host

@@ -126,6 +126,7 @@ struct Server {
   std::mutex eng_mu;         // engine swaps (restart / load) vs /health and /metrics readers
   bool ready = false;        // start-up finished (later logs are not replayed to new requests)
   bool mock = false;
+  bool continuous = true;    // continuous batching (--no-continuous: one batch per engine run)
   int mock_delay_ms = 2;
   int capacity = 1;
   int default_n = 200;
@@ -222,6 +223,106 @@ ModelSlot* acquire_model(Server& S, const std::string& name) {
   return m;
 }
 
+// per-request bookkeeping once a generation ends (both scheduling modes)
+void record_result(Server& S, Job& j, const GenResult& r, double load_ms) {
+  j.result = r;
+  const std::string perf = Session::perf_summary(r, load_ms);
+  j.push({"log", perf});
+  fputs(perf.c_str(), stderr);
+  std::lock_guard<std::mutex> l(S.metrics.mu);
+  S.metrics.completed++;
+  if (r.stop == "cancelled") S.metrics.cancelled++;
+  S.metrics.prompt_tokens += r.n_prompt;
+  S.metrics.gen_tokens += r.n_gen;
+  if (r.decode_ms > 0 && r.n_gen > 1) {
+    S.metrics.last_decode_tok_s = (r.n_gen - 1) * 1e3 / r.decode_ms;
+    S.metrics.add_latency(r.decode_ms / (r.n_gen - 1));
+  }
+  if (r.prefill_ms > 0) S.metrics.last_prefill_tok_s = r.n_prompt * 1e3 / r.prefill_ms;
+}
+
+// the engine is poisoned (aborted links, failed stage): rebuild it; injected faults are a one-shot
+// test hook and are not re-armed
+void restart_if_failed(Server& S, ModelSlot* slot) {
+  if (!slot || !slot->eng || slot->eng->health().get_bool("ok", true)) return;
+  slot->cfg["fault"] = Json::object();
+  try {
+    load_slot(S, *slot);
+    slot->restarts++;
+    MP_LOGW("orchestrator: engine of model %s restarted after a fault (%d restarts)", slot->name.c_str(),
+            slot->restarts);
+  } catch (const std::exception& e2) {
+    MP_LOGE("orchestrator: engine restart failed: %s", e2.what());
+  }
+}
+
+// Continuous batching (default): requests for `model` are admitted into free sequence slots between
+// decode rounds while the running ones keep generating; each finishes (and frees its slot) on its own.
+void serve_model(Server& S, ModelSlot* slot, const std::string& model) {
+  auto next = [&](int free) {
+    std::vector<std::shared_ptr<Job>> taken;
+    {
+      std::lock_guard<std::mutex> l(S.jobs_mu);
+      for (auto it = S.pending.begin(); it != S.pending.end() && (int)taken.size() < free;) {
+        if ((*it)->model == model) {
+          taken.push_back(*it);
+          it = S.pending.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    std::vector<Session::Served> out;
+    for (auto& j : taken) {
+      {
+        std::lock_guard<std::mutex> l(S.active_mu);
+        S.active.push_back(j);
+      }
+      j->push({"log", "orchestrator: request accepted (continuous batching, " + std::to_string(free) + " free slots)\n"});
+      for (auto& sl : S.startup_logs) j->push({"log", sl});
+      Session::Served sv;
+      sv.req.prompt = j->prompt;
+      sv.req.n_predict = j->n_predict;
+      Job* jp = j.get();
+      sv.req.on_piece = [jp](const std::string& p) {
+        if (jp->cancelled) return false;
+        jp->push({"token", p});
+        return true;
+      };
+      std::shared_ptr<Job> keep = j;
+      sv.done = [&S, slot, keep](GenResult& r) {
+        record_result(S, *keep, r, slot->eng->load_ms());
+        {
+          std::lock_guard<std::mutex> l(S.active_mu);
+          S.active.erase(std::remove(S.active.begin(), S.active.end(), keep), S.active.end());
+        }
+        keep->finish();
+      };
+      out.push_back(std::move(sv));
+    }
+    return out;
+  };
+  try {
+    slot->sess->serve(next);
+  } catch (const std::exception& e) {
+    MP_LOGE("generation failed: %s", e.what());
+    std::vector<std::shared_ptr<Job>> left;
+    {
+      std::lock_guard<std::mutex> l(S.active_mu);
+      left.swap(S.active);
+    }
+    {
+      std::lock_guard<std::mutex> l(S.metrics.mu);
+      S.metrics.errors += left.size();
+    }
+    for (auto& j : left) {
+      j->push({"log", std::string("error: ") + e.what() + "\n"});
+      j->finish();
+    }
+    restart_if_failed(S, slot);
+  }
+}
+
 void generation_loop(Server& S) {
   while (!S.stop) {
     std::vector<std::shared_ptr<Job>> batch;
@@ -250,6 +351,10 @@ void generation_loop(Server& S) {
         j->finish();
         continue;
       }
+    }
+    if (!S.mock && S.continuous && slot->cfg.get_int("draft_max", 0) <= 0) {
+      serve_model(S, slot, model);
+      continue;
     }
     {
       // the oldest request's model; later requests for other models keep their place in the queue
@@ -290,23 +395,7 @@ void generation_loop(Server& S) {
         }
         res = slot->sess->run(reqs);
       }
-      for (size_t i = 0; i < batch.size(); ++i) {
-        auto& j = batch[i];
-        j->result = res[i];
-        const std::string perf = Session::perf_summary(res[i], slot ? slot->eng->load_ms() : 0.0);
-        j->push({"log", perf});
-        fputs(perf.c_str(), stderr);
-        std::lock_guard<std::mutex> l(S.metrics.mu);
-        S.metrics.completed++;
-        if (res[i].stop == "cancelled") S.metrics.cancelled++;
-        S.metrics.prompt_tokens += res[i].n_prompt;
-        S.metrics.gen_tokens += res[i].n_gen;
-        if (res[i].decode_ms > 0 && res[i].n_gen > 1) {
-          S.metrics.last_decode_tok_s = (res[i].n_gen - 1) * 1e3 / res[i].decode_ms;
-          S.metrics.add_latency(res[i].decode_ms / (res[i].n_gen - 1));
-        }
-        if (res[i].prefill_ms > 0) S.metrics.last_prefill_tok_s = res[i].n_prompt * 1e3 / res[i].prefill_ms;
-      }
+      for (size_t i = 0; i < batch.size(); ++i) record_result(S, *batch[i], res[i], slot ? slot->eng->load_ms() : 0.0);
     } catch (const std::exception& e) {
       MP_LOGE("generation failed: %s", e.what());
       {
@@ -314,19 +403,7 @@ void generation_loop(Server& S) {
         S.metrics.errors += batch.size();
       }
       for (auto& j : batch) j->push({"log", std::string("error: ") + e.what() + "\n"});
-      if (slot && slot->eng && !slot->eng->health().get_bool("ok", true)) {
-        // the engine is poisoned (aborted links, failed stage): rebuild it; injected faults are
-        // a one-shot test hook and are not re-armed
-        slot->cfg["fault"] = Json::object();
-        try {
-          load_slot(S, *slot);
-          slot->restarts++;
-          MP_LOGW("orchestrator: engine of model %s restarted after a fault (%d restarts)", slot->name.c_str(),
-                  slot->restarts);
-        } catch (const std::exception& e2) {
-          MP_LOGE("orchestrator: engine restart failed: %s", e2.what());
-        }
-      }
+      restart_if_failed(S, slot);
     }
     {
       std::lock_guard<std::mutex> l(S.active_mu);
@@ -773,6 +850,7 @@ int main(int argc, char** argv) {
       else if (a == "--alias") alias = val();
       else if (a == "--model-alias") aliases.push_back(val());
       else if (a == "--max-models") S.max_models = std::max(1, std::atoi(val().c_str()));
+      else if (a == "--no-continuous") S.continuous = false;
       else if (a == "-h" || a == "--help") { usage(); exit(0); }
       else return false;
       return true;

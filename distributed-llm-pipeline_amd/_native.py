@@ -75,6 +75,8 @@ _SIGS = {
     "mp_engine_spec_generate": ([c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p], c_char_p),
     "mp_engine_bench": ([c_void_p, c_int, c_int, c_int], c_char_p),
     "mp_engine_start": ([c_void_p, c_void_p, c_void_p, c_int], c_int),
+    "mp_engine_admit": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int], c_int),
+    "mp_engine_release": ([c_void_p, c_int], c_int),
     "mp_engine_decode": ([c_void_p, c_int], c_char_p),
     "mp_engine_tokens": ([c_void_p, c_void_p, c_int, c_int], c_int),
     "mp_engine_logits": ([c_void_p, c_int, c_void_p, c_int], c_int),

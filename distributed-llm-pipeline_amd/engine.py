@@ -75,13 +75,26 @@ class Engine:
         self._n_seq = len(prompts)
         N.check(N.lib().mp_engine_start(self._h, flat.ctypes.data, lens.ctypes.data, len(prompts)), "start")
 
+    def admit(self, slots, prompts):
+        """Continuous batching: between decode rounds, prefill `prompts` into the idle sequence slots
+        `slots` (slot = micro-batch * mb_size + row); the other slots keep generating."""
+        flat, lens = self._flat(prompts)
+        sl = np.asarray(slots, np.int32)
+        N.check(N.lib().mp_engine_admit(self._h, sl.ctypes.data, flat.ctypes.data, lens.ctypes.data, len(prompts)),
+                "admit")
+        self._n_seq = self.n_seq_cap
+
+    def release(self, slot: int):
+        """Mark a slot idle (its sequence is finished); it can be admitted again."""
+        N.check(N.lib().mp_engine_release(self._h, int(slot)), "release")
+
     def decode(self, k: int):
         return N.jcall(N.lib().mp_engine_decode, self._h, k, what="decode")
 
     def tokens(self, cap: int = 4096):
         out = np.full((self._n_seq, cap), -1, np.int32)
         n = N.check(N.lib().mp_engine_tokens(self._h, out.ctypes.data, self._n_seq, cap), "tokens")
-        return out[:, :n].tolist()
+        return [[t for t in row if t >= 0] for row in out[:, :n].tolist()]
 
     def bench(self, prompt_len: int, warmup: int, steps: int):
         return N.jcall(N.lib().mp_engine_bench, self._h, prompt_len, warmup, steps, what="bench")

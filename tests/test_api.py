@@ -303,3 +303,35 @@ def test_cli_state_save_and_resume(native_bins, tiny_gguf, tmp_path):
         assert r.returncode == 0, r.stderr.decode(errors="replace")
     assert b"state saved" in a.stderr and b"resumed" in b.stderr
     assert full.stdout == a.stdout.rstrip(b"\n") + b.stdout
+
+
+def test_continuous_batching_admits_mid_generation(native_bins, tiny_gguf):
+    """With continuous batching a short request that arrives while a long one is generating is
+    admitted into a free slot and finishes first; both texts equal the single-request (CLI) texts."""
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-c", "512", "-ngl", "0", "--no-display-prompt"]
+    pl, ps = "The pipeline sends activations", "Once upon a time"
+    def cli(p, n):
+        out = subprocess.run(base + ["-p", p, "-n", str(n)], capture_output=True, timeout=120).stdout
+        return out.decode("utf-8", errors="replace").rstrip("\n")
+    ref_long, ref_short = cli(pl, 200), cli(ps, 8)
+    s = Orchestrator("-m", tiny_gguf, "-ngl", "0", "-c", "512", "--mb-size", "2", "--micro-batches", "2",
+                     "--threads", "2")
+    try:
+        done = {}
+
+        def go(name, prompt, n):
+            r = httpx.post(s.url + "/completion", json={"prompt": prompt, "n_predict": n}, timeout=120).json()
+            done[name] = (time.time(), r["content"])
+
+        t_long = threading.Thread(target=go, args=("long", pl, 200))
+        t_long.start()
+        time.sleep(0.3)   # the long request is decoding
+        t_short = threading.Thread(target=go, args=("short", ps, 8))
+        t_short.start()
+        t_short.join()
+        t_long.join()
+        assert done["short"][1] == ref_short
+        assert done["long"][1] == ref_long
+        assert done["short"][0] < done["long"][0]   # admitted mid-stream, not queued behind the long run
+    finally:
+        s.close()

@@ -338,3 +338,35 @@ def test_cpu_max_ctx_auto(native, model_dir):
         assert eng.info["max_ctx"] == cfg.n_ctx_train
         out, _ = eng.generate([[5, 6, 7]], 4)
         assert len(out[0]) == 4
+
+
+@pytest.mark.parametrize("stages", [1, 2])
+def test_cpu_continuous_batching(native, model_dir, stages):
+    """Sequences admitted into free slots between decode rounds (and a released slot re-used)
+    generate exactly what each would generate alone."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(11)
+    P = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 30, 5, 17, 12)]
+    alone = []
+    with Engine(gguf=path, backend="cpu", max_ctx=128, prefill_chunk=16) as eng:
+        for p in P:
+            o, _ = eng.generate([p], 10)
+            alone.append(o[0])
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=2, mb_size=2, prefill_chunk=16, stages=stages,
+                split="even") as eng:
+        eng.start([P[0], P[1]])                 # slots 0, 1
+        eng.decode(3)
+        eng.admit([2, 3], [P[2], P[3]])         # mid-stream, other micro-batch
+        eng.decode(5)
+        t = eng.tokens()
+        assert t[0][:9] == alone[0][:9] and t[1][:9] == alone[1][:9]
+        assert t[2][:6] == alone[2][:6] and t[3][:6] == alone[3][:6]
+        eng.release(0)
+        eng.admit([0], [P[4]])                  # re-use a slot whose neighbour (slot 1) keeps going
+        eng.decode(4)
+        t = eng.tokens()
+        assert t[0][:5] == alone[4][:5]
+        assert t[1][:10] == alone[1][:10] and t[2][:10] == alone[2][:10]
+        with pytest.raises(RuntimeError):
+            eng.admit([1], [P[0]])              # busy slot

@@ -381,3 +381,31 @@ def test_bench_contract_line(cuda, native):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["value"] > 0
     assert d["config"]["parallelism"] == "pp1" and d["config"]["global_batch"] == 4
+
+
+@pytest.mark.parametrize("stages", [1, 2])
+def test_continuous_batching(cuda, native, model_dir, stages):
+    """HIP stages: sequences admitted between decode rounds (row-selective head, ring tokens,
+    per-slot positions) and a recycled slot generate what each generates alone."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(12)
+    P = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 30, 5, 17, 12)]
+    alone = []
+    with Engine(gguf=path, max_ctx=128, prefill_chunk=16) as eng:
+        for p in P:
+            o, _ = eng.generate([p], 10)
+            alone.append(o[0])
+    kw = dict(gguf=path, max_ctx=128, n_mb=2, mb_size=2, prefill_chunk=16, stages=stages,
+              devices=[0] * stages, link="local", split="even")
+    with Engine(**kw) as eng:
+        eng.start([P[0], P[1]])
+        eng.decode(3)
+        eng.admit([2, 3], [P[2], P[3]])
+        eng.decode(5)
+        eng.release(0)
+        eng.admit([0], [P[4]])
+        eng.decode(4)
+        t = eng.tokens()
+    assert t[1][:10] == alone[1][:10] and t[2][:10] == alone[2][:10] and t[3][:10] == alone[3][:10]
+    assert t[0][:5] == alone[4][:5]
