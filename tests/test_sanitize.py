@@ -32,7 +32,8 @@ def fuzz_bin():
 
 
 def run(bin_, mode, paths):
-    r = subprocess.run([bin_, mode] + list(paths), capture_output=True, text=True, env=ENV, timeout=120)
+    r = subprocess.run([bin_, mode] + list(paths), capture_output=True, text=True, errors="replace", env=ENV,
+                       timeout=120)
     report = r.stderr
     assert "AddressSanitizer" not in report and "runtime error" not in report, report[-3000:]
     assert r.returncode == 0, (r.returncode, report[-2000:])
