@@ -7,6 +7,8 @@
 #include <cstring>
 #include <exception>
 #include <fstream>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <sys/stat.h>
 #include <numeric>
 #include <stdexcept>
@@ -133,6 +135,9 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   }
   if (mode_ == "mp") devices[rank_] = j.get_int("device", devices[rank_]);
   for (int s = 0; s < S_; ++s) specs_[s].device = devices[s];
+  // --gpu-mem (prima.cpp): per-GPU memory budget in GiB; caps the auto KV sizing and
+  // is checked against every stage's weights + KV below (--force downgrades the failure to a warning)
+  const double gpu_mem = j.get_num("gpu_mem_gib", 0.0) * 1073741824.0;
   if (auto_ctx) {
     // KV sized from HBM (288 GB per MI355X): every rank derives the same value from
     // the partition and the device capacity alone (no exchange needed in mp mode): the heaviest
@@ -146,6 +151,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       HIP_OK(hipMemGetInfo(&fr, &tot));
       cap_bytes = (double)tot;
     }
+    if (gpu_mem > 0) cap_bytes = std::min(cap_bytes, gpu_mem);
     const double embd_bytes = gguf_ && gguf_->tensor("token_embd.weight")
                                   ? (double)gguf_->tensor("token_embd.weight")->nbytes : head_cost;
     double wmax = 0;
@@ -172,6 +178,45 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   for (auto& sp : specs_)
     MP_LOGI("partition: stage %d <- layers [%d, %d) (%d layers)%s%s", sp.stage, sp.layer_begin, sp.layer_end,
             sp.layer_end - sp.layer_begin, sp.first() ? " +embd" : "", sp.last() ? " +head" : "");
+
+  if (gpu_mem > 0) {
+    const double embd_b = gguf_ && gguf_->tensor("token_embd.weight")
+                              ? (double)gguf_->tensor("token_embd.weight")->nbytes : head_cost;
+    for (auto& sp : specs_) {
+      if (mode_ == "mp" && sp.stage != rank_) continue;
+      double w = 0;
+      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li];
+      if (sp.first()) w += embd_b;
+      if (sp.last()) w += head_cost;
+      const double kv = (double)(sp.layer_end - sp.layer_begin) * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() *
+                        (cpu_ ? 4.0 : 2.0) * max_ctx_ * M_ * B_;
+      if (w + kv > gpu_mem) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "stage %d needs %.2f GiB (weights %.2f + KV %.2f) > --gpu-mem %.2f GiB", sp.stage,
+                 (w + kv) / 1073741824.0, w / 1073741824.0, kv / 1073741824.0, gpu_mem / 1073741824.0);
+        if (!j.get_bool("force", false)) throw std::runtime_error(std::string(msg) + " (use --force to proceed)");
+        MP_LOGW("%s; --force: proceeding", msg);
+      }
+    }
+  }
+  // --prefetch: ask the kernel to read ahead the mmap'd GGUF ranges of the layers this
+  // process uploads, so page-in overlaps the partition / allocation work instead of the upload loop
+  if (gguf_ && j.get_bool("prefetch", false)) {
+    const long pg = sysconf(_SC_PAGESIZE);
+    size_t advised = 0;
+    for (auto& t : gguf_->tensors()) {
+      int li = -1;
+      if (t.name.compare(0, 4, "blk.") == 0) li = std::atoi(t.name.c_str() + 4);
+      bool mine = mode_ != "mp";
+      for (auto& sp : specs_)
+        if (sp.stage == rank_ || mode_ != "mp")
+          mine = mine || (li >= 0 ? li >= sp.layer_begin && li < sp.layer_end : sp.first() || sp.last());
+      if (!mine || !t.nbytes) continue;
+      const uintptr_t a = (uintptr_t)t.data & ~(uintptr_t)(pg - 1);
+      if (madvise((void*)a, (uintptr_t)t.data + t.nbytes - a, MADV_WILLNEED) == 0) advised += t.nbytes;
+    }
+    MP_LOGI("prefetch: madvise(WILLNEED) on %.2f GiB of GGUF tensor data", advised / 1073741824.0);
+  }
 
   StageOptions so;
   so.n_mb = M_;

@@ -91,6 +91,8 @@ inline void print_common_usage(FILE* f) {
           "  --no-prefix-cache         prefill every request in full (no KV reuse of a common prefix)\n"
           "  --world N --rank R        one process per stage (multi-process / multi-host)\n"
           "  --next HOST --master HOST --base-port P   TCP ring neighbours (prima.cpp style)\n"
+          "  --gpu-mem GiB [--force]   per-GPU memory budget (caps auto KV; fail if a stage exceeds it)\n"
+          "  --prefetch                madvise(WILLNEED) the GGUF ranges this process uploads\n"
           "  --rpc host:port,...       accepted for llama-cli parity: hosts of the stage processes\n"
           "logging:\n"
           "  --verbose, --log-file FILE, --trace FILE (Chrome trace of the pipeline)\n");
@@ -145,6 +147,9 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--rank") rank = std::atoi(val().c_str());
     else if (a == "--next") next = val();
     else if (a == "--master") master = val();
+    else if (a == "--prefetch") e["prefetch"] = true;
+    else if (a == "--gpu-mem") e["gpu_mem_gib"] = std::atof(val().c_str());
+    else if (a == "--force") e["force"] = true;
     else if (a == "--base-port") e["base_port"] = std::atoi(val().c_str());
     else if (a == "--rpc") rpc = val();
     else if (a == "--device") e["device"] = std::atoi(val().c_str());

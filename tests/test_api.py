@@ -335,3 +335,16 @@ def test_continuous_batching_admits_mid_generation(native_bins, tiny_gguf):
         assert done["short"][0] < done["long"][0]   # admitted mid-stream, not queued behind the long run
     finally:
         s.close()
+
+
+def test_cli_gpu_mem_force_prefetch(native_bins, tiny_gguf):
+    """prima.cpp launch flags: --gpu-mem budget check, --force, --prefetch."""
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-p", "abc", "-n", "4", "-c", "128", "-ngl", "0",
+            "--stages", "2", "--gpu-mem", "0.00001"]
+    r = subprocess.run(base, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpu-mem" in r.stderr and "--force" in r.stderr
+    r = subprocess.run(base + ["--force", "--prefetch", "--verbose"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "proceeding" in r.stderr and "prefetch: madvise" in r.stderr
+    r = subprocess.run(base[:-2] + ["--gpu-mem", "64"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
