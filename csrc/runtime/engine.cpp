@@ -7,6 +7,8 @@
 #include <cstring>
 #include <exception>
 #include <fstream>
+#include <limits>
+#include <map>
 #include <sys/mman.h>
 #include <unistd.h>
 #include <sys/stat.h>
@@ -154,25 +156,38 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     if (gpu_mem > 0) cap_bytes = std::min(cap_bytes, gpu_mem);
     const double embd_bytes = gguf_ && gguf_->tensor("token_embd.weight")
                                   ? (double)gguf_->tensor("token_embd.weight")->nbytes : head_cost;
-    double wmax = 0;
-    int lmax = 1;
+    // stages sharing a GPU (single-GPU PP emulation, devices 0,0,..) share its memory: size from
+    // the device carrying the most layers / weights, summed over its stages (mp mode: one GPU per
+    // rank, every rank derives the same value)
+    std::map<int, double> dev_w;
+    std::map<int, int> dev_l, dev_n;
     for (auto& sp : specs_) {
       double w = 0;
       for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li];
       if (sp.first()) w += embd_bytes;
       if (sp.last()) w += head_cost;
-      wmax = std::max(wmax, w);
-      lmax = std::max(lmax, sp.layer_end - sp.layer_begin);
+      const int key = mode_ == "mp" ? sp.stage : devices[sp.stage];
+      dev_w[key] += w;
+      dev_l[key] += sp.layer_end - sp.layer_begin;
+      dev_n[key] += 1;
     }
-    const double per_tok = (double)lmax * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : 2.0);
-    const double reserve = 4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4;
-    const double budget = frac * cap_bytes - wmax - reserve;
-    long ctx = budget > 0 ? (long)(budget / (per_tok * M_ * B_)) : 0;
+    long ctx = std::numeric_limits<long>::max();
+    double per_tok = 0;
+    int lmax = 1;
+    for (auto& e : dev_w) {
+      const int layers = std::max(1, dev_l[e.first]);
+      const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : 2.0);
+      const double reserve =
+          dev_n[e.first] * (4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4);
+      const double budget = frac * cap_bytes - e.second - reserve;
+      const long c = budget > 0 ? (long)(budget / (pt * M_ * B_)) : 0;
+      if (c < ctx) { ctx = c; per_tok = pt; lmax = layers; }
+    }
     const long train = cfg_.n_ctx_train > 0 ? cfg_.n_ctx_train : 131072;
     ctx = std::min(ctx, std::min(train, (long)j.get_int("max_ctx_cap", 1 << 20)));
     if (ctx < 64) throw std::runtime_error("max_ctx auto: no HBM left for the KV cache");
     max_ctx_ = (int)(ctx / 64 * 64);
-    MP_LOGI("max_ctx auto: %d tokens per sequence (%d slots, %.1f GiB KV per stage of %d layers; device %.0f GiB)",
+    MP_LOGI("max_ctx auto: %d tokens per sequence (%d slots, %.1f GiB KV on the GPU holding %d layers; device %.0f GiB)",
             max_ctx_, M_ * B_, per_tok * max_ctx_ * M_ * B_ / 1073741824.0, lmax, cap_bytes / 1073741824.0);
   }
   for (auto& sp : specs_)
@@ -180,8 +195,11 @@ Engine::Engine(const Json& j) : jcfg_(j) {
             sp.layer_end - sp.layer_begin, sp.first() ? " +embd" : "", sp.last() ? " +head" : "");
 
   if (gpu_mem > 0) {
+    // --gpu-mem is per GPU: add up weights + KV of every stage this process places on a device
     const double embd_b = gguf_ && gguf_->tensor("token_embd.weight")
                               ? (double)gguf_->tensor("token_embd.weight")->nbytes : head_cost;
+    std::map<int, std::pair<double, double>> need;   // device -> (weights, kv)
+    std::map<int, std::string> who;
     for (auto& sp : specs_) {
       if (mode_ == "mp" && sp.stage != rank_) continue;
       double w = 0;
@@ -190,10 +208,20 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       if (sp.last()) w += head_cost;
       const double kv = (double)(sp.layer_end - sp.layer_begin) * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() *
                         (cpu_ ? 4.0 : 2.0) * max_ctx_ * M_ * B_;
-      if (w + kv > gpu_mem) {
-        char msg[256];
-        snprintf(msg, sizeof msg, "stage %d needs %.2f GiB (weights %.2f + KV %.2f) > --gpu-mem %.2f GiB", sp.stage,
-                 (w + kv) / 1073741824.0, w / 1073741824.0, kv / 1073741824.0, gpu_mem / 1073741824.0);
+      auto& e = need[devices[sp.stage]];
+      e.first += w;
+      e.second += kv;
+      std::string& ws = who[devices[sp.stage]];
+      ws += (ws.empty() ? "" : ",") + std::to_string(sp.stage);
+    }
+    for (auto& e : need) {
+      const double w = e.second.first, k = e.second.second;
+      if (w + k > gpu_mem) {
+        char msg[320];
+        snprintf(msg, sizeof msg,
+                 "GPU %d (stage %s) needs %.3f MiB (weights %.3f + KV %.3f) > --gpu-mem %.3f MiB",
+                 e.first, who[e.first].c_str(), (w + k) / 1048576.0, w / 1048576.0, k / 1048576.0,
+                 gpu_mem / 1048576.0);
         if (!j.get_bool("force", false)) throw std::runtime_error(std::string(msg) + " (use --force to proceed)");
         MP_LOGW("%s; --force: proceeding", msg);
       }
@@ -784,6 +812,10 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
 // stage lives, so a multi-process pipeline caches prompts only (every rank must agree on reuse).
 void Engine::refresh_slot_cache() {
   slot_toks_ = prompts_;
+  // a released slot's KV is not guaranteed (load_state restores active slots only; live idle rows
+  // keep overwriting theirs): never offer it for prefix reuse
+  for (size_t i = 0; i < slot_toks_.size(); ++i)
+    if (i < active_.size() && !active_[i]) slot_toks_[i].clear();
   if (!resumable_ || !owns_first() || !owns_last()) return;
   for (size_t i = 0; i < slot_toks_.size() && i < gen_.size(); ++i) {
     const int since = rounds_done_ - (i < base_round_.size() ? base_round_[i] : 0);
@@ -899,12 +931,30 @@ Json Engine::load_state(const std::string& dir) {
     gen_.push_back(v);
   }
   rounds_done_ = sj.get_int("rounds_done", 0);
-  if ((int)prompts_.size() > M_ * B_ || gen_.size() != prompts_.size()) throw std::runtime_error("load_state: bad session");
+  // session.json is untrusted input: validate every index and size before it reaches a buffer
+  if (prompts_.empty() || (int)prompts_.size() > M_ * B_ || gen_.size() != prompts_.size() || rounds_done_ < 0)
+    throw std::runtime_error("load_state: bad session");
+  if ((sj.has("base_round") && sj["base_round"].arr().size() != prompts_.size()) ||
+      (sj.has("active") && sj["active"].arr().size() != prompts_.size()))
+    throw std::runtime_error("load_state: bad session (base_round / active size)");
+  auto check_ids = [&](const std::vector<int32_t>& v) {
+    for (int32_t t : v)
+      if (t < 0 || t >= cfg_.vocab) throw std::runtime_error("load_state: token id out of range");
+  };
+  for (size_t i = 0; i < prompts_.size(); ++i) {
+    if (prompts_[i].empty() || (int)prompts_[i].size() >= max_ctx_)
+      throw std::runtime_error("load_state: prompt length out of range");
+    check_ids(prompts_[i]);
+    check_ids(gen_[i]);
+  }
   base_round_.assign((size_t)M_ * B_, 0);
   active_.assign((size_t)M_ * B_, 0);
   for (size_t i = 0; i < prompts_.size(); ++i) {
     base_round_[i] = sj.has("base_round") ? (int)sj["base_round"].arr()[i].num() : 0;
     active_[i] = sj.has("active") ? (char)sj["active"].arr()[i].num() : 1;
+    if (base_round_[i] < 0 || base_round_[i] > rounds_done_)
+      throw std::runtime_error("load_state: bad session (base_round)");
+    if (active_[i] && slot_pos(i) >= max_ctx_) throw std::runtime_error("load_state: sequence longer than max_ctx");
   }
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
@@ -921,8 +971,12 @@ Json Engine::load_state(const std::string& dir) {
     const uint8_t* kv = reinterpret_cast<const uint8_t*>(raw.data()) + nl + 1;
     const uint8_t* end = reinterpret_cast<const uint8_t*>(raw.data()) + raw.size();
     const auto& lens = h["n_tok"].arr();
+    if ((int)lens.size() != M_ * B_) throw std::runtime_error("load_state: bad n_tok in " + path);
     for (size_t i = 0; i < lens.size(); ++i) {
       const int n = (int)lens[i].num();
+      // the stage file must describe exactly the KV the session implies (active slots only)
+      const int want = i < prompts_.size() && active_[i] ? slot_pos(i) : 0;
+      if (n != want) throw std::runtime_error("load_state: " + path + " KV length disagrees with session.json");
       if (n <= 0) continue;
       if (n >= max_ctx_) throw std::runtime_error("load_state: sequence longer than max_ctx");
       const size_t nb = st.kv_state_bytes(n);
@@ -941,7 +995,10 @@ Json Engine::load_state(const std::string& dir) {
       if ((int)toks.size() != M_ * B_) throw std::runtime_error("load_state: missing first-stage tokens");
       std::vector<int32_t> t(B_);
       for (int mb = 0; mb < M_; ++mb) {
-        for (int b = 0; b < B_; ++b) t[b] = (int32_t)toks[(size_t)mb * B_ + b].num();
+        for (int b = 0; b < B_; ++b) {
+          t[b] = (int32_t)toks[(size_t)mb * B_ + b].num();
+          if (t[b] < 0 || t[b] >= cfg_.vocab) throw std::runtime_error("load_state: token id out of range");
+        }
         if (cpu_) std::memcpy(st.tokens(mb), t.data(), (size_t)B_ * 4);
         else HIP_OK(hipMemcpy(st.tokens(mb), t.data(), (size_t)B_ * 4, hipMemcpyHostToDevice));
       }

@@ -37,6 +37,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cerrno>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -70,6 +72,7 @@ struct Job {
   std::string prompt;
   std::string model;   // "" = the default model
   int n_predict = 200;
+  double enqueued_ms = 0;   // fairness between models (serve_model)
   std::mutex mu;
   std::condition_variable cv;
   std::deque<Event> q;
@@ -144,6 +147,9 @@ struct Server {
   Metrics metrics;
   std::atomic<bool> stop{false};
   std::atomic<int> connections{0};
+  // a request for another model that has waited this long stops admission into the model being
+  // served; its live requests drain and the generation loop switches models (no starvation)
+  double switch_after_ms = 2000;
 };
 
 Server* g_srv = nullptr;
@@ -259,10 +265,17 @@ void restart_if_failed(Server& S, ModelSlot* slot) {
 // Continuous batching (default): requests for `model` are admitted into free sequence slots between
 // decode rounds while the running ones keep generating; each finishes (and frees its slot) on its own.
 void serve_model(Server& S, ModelSlot* slot, const std::string& model) {
+  const double turn_start = now_ms();
   auto next = [&](int free) {
     std::vector<std::shared_ptr<Job>> taken;
     {
       std::lock_guard<std::mutex> l(S.jobs_mu);
+      // each model gets a turn of at least switch_after_ms before another model's waiting request
+      // can end it (otherwise two busy models would hand the turn back and forth, admitting nothing)
+      const double now = now_ms();
+      if (now - turn_start > S.switch_after_ms)
+        for (auto& pj : S.pending)
+          if (pj->model != model && now - pj->enqueued_ms > S.switch_after_ms) return std::vector<Session::Served>{};
       for (auto it = S.pending.begin(); it != S.pending.end() && (int)taken.size() < free;) {
         if ((*it)->model == model) {
           taken.push_back(*it);
@@ -324,6 +337,8 @@ void serve_model(Server& S, ModelSlot* slot, const std::string& model) {
 }
 
 void generation_loop(Server& S) {
+  std::string last_model;
+  bool have_last = false;
   while (!S.stop) {
     std::vector<std::shared_ptr<Job>> batch;
     ModelSlot* slot = nullptr;
@@ -332,8 +347,19 @@ void generation_loop(Server& S) {
       std::unique_lock<std::mutex> l(S.jobs_mu);
       S.jobs_cv.wait_for(l, std::chrono::milliseconds(200), [&] { return !S.pending.empty() || S.stop; });
       if (S.pending.empty()) continue;
+      // the oldest request's model, except that the oldest request of ANOTHER model than the one
+      // served last goes first once it has waited switch_after_ms (serve_model stopped for it)
       model = S.pending.front()->model;
+      const double now = now_ms();
+      if (have_last)
+        for (auto& pj : S.pending)
+          if (pj->model != last_model && now - pj->enqueued_ms > S.switch_after_ms) {
+            model = pj->model;
+            break;
+          }
     }
+    last_model = model;
+    have_last = true;
     int cap = S.capacity;
     if (!S.mock) {
       try {
@@ -475,22 +501,23 @@ void respond(int fd, int code, const std::string& ctype, const std::string& body
 
 void respond_text(int fd, int code, const std::string& msg) { respond(fd, code, "text/plain; charset=utf-8", msg); }
 
-bool read_request(int fd, Request& r) {
+// 1 = request read, 0 = connection closed / oversized, -1 = malformed (answer 400)
+int read_request(int fd, Request& r) {
   std::string buf;
   char tmp[8192];
   size_t hdr_end = std::string::npos;
   while ((hdr_end = buf.find("\r\n\r\n")) == std::string::npos) {
     ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
-    if (n <= 0) return false;
+    if (n <= 0) return 0;
     buf.append(tmp, (size_t)n);
-    if (buf.size() > (1 << 20)) return false;
+    if (buf.size() > (1 << 20)) return 0;
   }
   const std::string head = buf.substr(0, hdr_end);
   r.body = buf.substr(hdr_end + 4);
   size_t eol = head.find("\r\n");
   const std::string line = head.substr(0, eol);
   size_t a = line.find(' '), b = line.rfind(' ');
-  if (a == std::string::npos || b == a) return false;
+  if (a == std::string::npos || b == a) return 0;
   r.method = line.substr(0, a);
   std::string target = line.substr(a + 1, b - a - 1);
   r.version = line.substr(b + 1);
@@ -510,15 +537,24 @@ bool read_request(int fd, Request& r) {
     }
     pos = e + 2;
   }
-  const size_t cl = r.header("content-length").empty() ? 0 : std::stoul(r.header("content-length"));
-  if (cl > (8u << 20)) return false;
+  size_t cl = 0;
+  const std::string clh = r.header("content-length");
+  if (!clh.empty()) {
+    // strict decimal: a malformed or out-of-range value is a 400, never an exception on this thread
+    errno = 0;
+    char* end = nullptr;
+    const unsigned long long v = std::strtoull(clh.c_str(), &end, 10);
+    if (clh[0] < '0' || clh[0] > '9' || errno == ERANGE || !end || *end != '\0') return -1;
+    if (v > (8ull << 20)) return 0;
+    cl = (size_t)v;
+  }
   while (r.body.size() < cl) {
     ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
-    if (n <= 0) return false;
+    if (n <= 0) return 0;
     r.body.append(tmp, (size_t)n);
   }
   r.body.resize(cl);
-  return true;
+  return 1;
 }
 
 std::string mime_of(const std::string& p) {
@@ -617,6 +653,7 @@ std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n, const s
   fflush(stdout);
   {
     std::lock_guard<std::mutex> l(S.jobs_mu);
+    job->enqueued_ms = now_ms();
     S.pending.push_back(job);
   }
   S.jobs_cv.notify_all();
@@ -759,7 +796,9 @@ void handle_conn(Server& S, int fd, std::string peer) {
   S.connections++;
   Request r;
   r.peer = peer;
-  if (read_request(fd, r)) {
+  const int rr = read_request(fd, r);
+  if (rr < 0) respond_text(fd, 400, "Bad Request: invalid Content-Length");
+  if (rr > 0) {
     try {
       if (r.method == "OPTIONS") {
         respond(fd, 204, "", "");
@@ -851,6 +890,7 @@ int main(int argc, char** argv) {
       else if (a == "--model-alias") aliases.push_back(val());
       else if (a == "--max-models") S.max_models = std::max(1, std::atoi(val().c_str()));
       else if (a == "--no-continuous") S.continuous = false;
+      else if (a == "--model-switch-ms") S.switch_after_ms = std::atof(val().c_str());
       else if (a == "-h" || a == "--help") { usage(); exit(0); }
       else return false;
       return true;

@@ -117,6 +117,23 @@ def test_errors_and_cors(mock_srv):
     assert r.status_code == 204 and r.headers["access-control-allow-origin"] == "*"
 
 
+def test_malformed_content_length_is_400_and_server_survives(mock_srv):
+    # a bad Content-Length used to throw on the connection thread (std::terminate)
+    for val in (b"abc", b"99999999999999999999999", b"-5", b"12x"):
+        with socket.create_connection(("127.0.0.1", mock_srv.port), timeout=10) as c:
+            c.sendall(b"POST /chat HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: " + val +
+                      b"\r\n\r\n{}")
+            resp = b""
+            while True:
+                d = c.recv(4096)
+                if not d:
+                    break
+                resp += d
+        assert resp.startswith(b"HTTP/1.1 400"), resp[:80]
+    assert mock_srv.proc.poll() is None
+    assert httpx.get(mock_srv.url + "/health", timeout=5).status_code == 200
+
+
 def test_static_panel(mock_srv):
     r = httpx.get(mock_srv.url + "/")
     assert r.status_code == 200 and "text/html" in r.headers["content-type"]
@@ -259,6 +276,42 @@ def test_multi_model_registry(native_bins, model_dir, tiny_gguf):
         assert post({"prompt": prompt, "model": "nope"}).status_code == 404
     finally:
         s.close()
+
+
+def test_other_model_not_starved_under_continuous_load(native_bins, model_dir, tiny_gguf):
+    """steady traffic to model a must not hold off a request for model b forever: after
+    --model-switch-ms the serve loop stops admitting a's requests, drains, and switches."""
+    other, _ = make_model(model_dir, "tiny-gqa", "Q8_0", seed=5)
+    s = Orchestrator("-m", tiny_gguf, "--alias", "a", "--model-alias", "b=" + other, "--max-models", "2",
+                     "-ngl", "0", "-n", "64", "-c", "256", "--mb-size", "2", "--model-switch-ms", "300")
+    stop = threading.Event()
+    errors = []
+
+    def hammer():
+        while not stop.is_set():
+            try:
+                r = httpx.post(s.url + "/completion", json={"prompt": "abc", "n_predict": 48, "model": "a"},
+                               timeout=120)
+                if r.status_code != 200:
+                    errors.append(r.status_code)
+            except Exception as e:   # noqa: BLE001
+                errors.append(repr(e))
+    try:
+        th = [threading.Thread(target=hammer) for _ in range(4)]
+        for t in th:
+            t.start()
+        time.sleep(1.0)   # model a is now continuously busy
+        t0 = time.time()
+        rb = httpx.post(s.url + "/completion", json={"prompt": "abc", "n_predict": 4, "model": "b"}, timeout=120)
+        waited = time.time() - t0
+        assert rb.status_code == 200 and rb.json()["tokens_predicted"] >= 1
+        assert waited < 60, waited
+    finally:
+        stop.set()
+        for t in th:
+            t.join(timeout=120)
+        s.close()
+    assert not errors, errors[:3]
 
 
 def test_engine_restart_after_fault(native_bins, tiny_gguf):

@@ -308,6 +308,60 @@ def test_cpu_checkpoint_rejects_other_shape(native, model_dir, tmp_path):
             eng.load_state(str(tmp_path / "st"))
 
 
+def test_cpu_released_slot_not_reused_after_load_state(native, model_dir, tmp_path):
+    """after start / release / save / load, a prompt sharing the released slot's old
+    prefix must not reuse its (never restored) KV: the output equals a fresh engine's."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(21)
+    A = [int(t) for t in rng.integers(3, cfg.vocab, 27)]
+    B = [int(t) for t in rng.integers(3, cfg.vocab, 9)]
+    kw = dict(gguf=path, backend="cpu", max_ctx=128, mb_size=2, prefill_chunk=16)
+    A2 = A + [int(t) for t in rng.integers(3, cfg.vocab, 4)]
+    with Engine(**kw) as eng:
+        fresh, _ = eng.generate([A2, B], 6)
+    with Engine(**kw) as eng:
+        eng.start([A, B])
+        eng.decode(3)
+        eng.release(0)
+        eng.save_state(str(tmp_path / "st"))
+    with Engine(**kw) as eng:
+        eng.load_state(str(tmp_path / "st"))
+        out, _ = eng.generate([A2, B], 6)
+    assert out[0] == fresh[0]
+
+
+def test_cpu_load_state_rejects_corrupt_session(native, model_dir, tmp_path):
+    """session.json / stage files are untrusted: bad sizes, lengths and ids fail cleanly."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    kw = dict(gguf=path, backend="cpu", max_ctx=64, mb_size=2, prefill_chunk=16)
+    with Engine(**kw) as eng:
+        eng.start([[5, 6, 7], [8, 9]])
+        eng.decode(2)
+        eng.save_state(str(tmp_path / "st"))
+    good = json.loads((tmp_path / "st" / "session.json").read_text())
+
+    def corrupt(fn):
+        j = json.loads(json.dumps(good))
+        fn(j)
+        (tmp_path / "st" / "session.json").write_text(json.dumps(j))
+        with Engine(**kw) as eng:
+            with pytest.raises(RuntimeError, match="load_state"):
+                eng.load_state(str(tmp_path / "st"))
+
+    corrupt(lambda j: j.update(active=[1]))                       # size mismatch
+    corrupt(lambda j: j.update(base_round=[0, 0, 0]))
+    corrupt(lambda j: j["prompts"].__setitem__(0, list(range(3, 3 + 70))))   # longer than max_ctx
+    corrupt(lambda j: j["prompts"].__setitem__(1, [8, cfg.vocab + 5]))      # id out of range
+    corrupt(lambda j: j["generated"].__setitem__(0, [-1, 2, 3]))
+    corrupt(lambda j: j["prompts"].__setitem__(0, [5, 6, 7, 8]))            # KV length disagrees
+    corrupt(lambda j: j.update(base_round=[5, 0]))                           # admitted in the future
+    (tmp_path / "st" / "session.json").write_text(json.dumps(good))
+    with Engine(**kw) as eng:
+        eng.load_state(str(tmp_path / "st"))
+
+
 @pytest.mark.parametrize("stages", [1, 2])
 def test_cpu_prefix_cache_multiturn(native, model_dir, stages):
     """Multi-turn: the second request re-sends prompt + reply + new text; with the prefix cache the
@@ -370,3 +424,29 @@ def test_cpu_continuous_batching(native, model_dir, stages):
         assert t[1][:10] == alone[1][:10] and t[2][:10] == alone[2][:10]
         with pytest.raises(RuntimeError):
             eng.admit([1], [P[0]])              # busy slot
+
+
+def test_cpu_gpu_mem_sums_stages_sharing_a_device(native, model_dir):
+    """--gpu-mem is per GPU, so stages emulated on one device add up."""
+    import re
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    kw = dict(gguf=path, backend="cpu", max_ctx=256, mb_size=2, stages=2, split="even")
+
+    def need(devices, gib):
+        try:
+            with Engine(devices=devices, gpu_mem_gib=gib, **kw):
+                return None
+        except RuntimeError as e:
+            m = re.search(r"GPU (\d+) \(stage ([\d,]+)\) needs ([\d.]+) MiB", str(e))
+            assert m, str(e)
+            return m.group(2), float(m.group(3))
+
+    stages, total = need([0, 0], 1e-9)
+    assert stages == "0,1"
+    s0, a0 = need([0, 1], 1e-9)
+    assert s0 == "0" and a0 < total
+    budget_mib = max(a0, total - a0) * 1.02
+    assert budget_mib < total
+    assert need([0, 1], budget_mib / 1024) is None      # each GPU fits alone
+    assert need([0, 0], budget_mib / 1024)[0] == "0,1"  # together they do not
