@@ -220,6 +220,35 @@ __global__ __launch_bounds__(256) void f32_to_f16_kernel(const float* x, int ldx
   if (j < n) y[(size_t)m * ldy + j] = (f16)x[(size_t)m * ldx + j];
 }
 
+// stage-boundary activation wire format (engine "act_dtype"): f32 residual rows <-> f16 / bf16
+// (2 bytes per element on xGMI).  4 elements per thread, round-to-nearest-even by
+// the hardware convert (a NaN stays a NaN).
+template <int OUT>
+__global__ __launch_bounds__(256) void act_pack_kernel(const float* __restrict__ x, void* __restrict__ y, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    const float4 v = *reinterpret_cast<const float4*>(x + i);
+    if constexpr (OUT == 1) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<h4*>(reinterpret_cast<f16*>(y) + i) = h4{(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+    } else {
+      typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<b4*>(reinterpret_cast<__bf16*>(y) + i) = b4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    }
+  } else {
+    for (int64_t k = i; k < n; ++k) {
+      if constexpr (OUT == 1) reinterpret_cast<f16*>(y)[k] = (f16)x[k];
+      else reinterpret_cast<__bf16*>(y)[k] = (__bf16)x[k];
+    }
+  }
+}
+template <int IN>
+__global__ __launch_bounds__(256) void act_unpack_kernel(const void* __restrict__ y, float* __restrict__ x, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  for (int64_t k = i; k < i + 4 && k < n; ++k)
+    x[k] = IN == 1 ? (float)reinterpret_cast<const f16*>(y)[k] : (float)reinterpret_cast<const __bf16*>(y)[k];
+}
+
 __global__ void prefill_meta_kernel(int32_t* pos, int32_t* kvlen, int32_t* slot, int p0, int T, int s) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < T) { pos[i] = p0 + i; kvlen[i] = p0 + i + 1; slot[i] = s; }
@@ -259,6 +288,18 @@ void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStrea
 
 void launch_swiglu(const float* gu, int ld, int F, int M, f16* h, int ldh, hipStream_t st) {
   hipLaunchKernelGGL(mpk::swiglu_kernel, dim3((F + 255) / 256, M), dim3(256), 0, st, gu, ld, F, h, ldh);
+}
+
+void launch_act_pack(const float* x, void* y, int64_t n, int dtype, hipStream_t st) {
+  const dim3 grid((unsigned)((n + 1023) / 1024));
+  if (dtype == ACT_F16) hipLaunchKernelGGL(mpk::act_pack_kernel<1>, grid, dim3(256), 0, st, x, y, n);
+  else if (dtype == ACT_BF16) hipLaunchKernelGGL(mpk::act_pack_kernel<2>, grid, dim3(256), 0, st, x, y, n);
+}
+
+void launch_act_unpack(const void* y, float* x, int64_t n, int dtype, hipStream_t st) {
+  const dim3 grid((unsigned)((n + 1023) / 1024));
+  if (dtype == ACT_F16) hipLaunchKernelGGL(mpk::act_unpack_kernel<1>, grid, dim3(256), 0, st, y, x, n);
+  else if (dtype == ACT_BF16) hipLaunchKernelGGL(mpk::act_unpack_kernel<2>, grid, dim3(256), 0, st, y, x, n);
 }
 
 void launch_f32_to_f16(const float* x, int ldx, int n, int M, f16* y, int ldy, hipStream_t st) {

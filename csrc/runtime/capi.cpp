@@ -3,6 +3,8 @@
 // error code / nullptr.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -16,6 +18,7 @@
 #include "log.h"
 #include "pack.h"
 #include "tokenizer.h"
+#include "transport.h"
 
 using namespace mp;
 
@@ -175,7 +178,6 @@ int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const voi
   API_CATCH(-1)
 }
 
-void mp_set_gemv_wpb(int w) { set_gemv_wpb(w); }
 void mp_set_gemv_tpw(int t) { set_gemv_tpw(t); }
 
 int mp_init_packed(void* W, size_t nbytes, int ptype, float scale, uint64_t seed, void* stream) {
@@ -509,6 +511,77 @@ int mp_rccl_unique_id(uint8_t* out128) {
   API_TRY
   return rccl_unique_id(out128);
   API_CATCH(-1)
+}
+
+// RCCL transport self-test (ws = 1): a 1-rank communicator on `device` and the
+// engine's RcclLink looping every size in `sizes` back to itself (grouped ncclSend/ncclRecv on one
+// stream), `iters` times each, checking every byte.  Returns a JSON report.
+const char* mp_rccl_selftest(int device, const int64_t* sizes, int n_sizes, int iters) {
+  API_TRY
+  HIP_OK(hipSetDevice(device));
+  std::vector<void*> comms;
+  std::string err;
+  if (!rccl_init_all({device}, &comms, &err)) throw std::runtime_error("RCCL init failed: " + err);
+  RcclLink link(comms[0], 0, 0, device);
+  hipStream_t st;
+  HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  Json rep = Json::object();
+  rep["rccl_version"] = std::string(rccl_version_string());
+  Json res = Json::array();
+  int64_t maxb = 0;
+  for (int i = 0; i < n_sizes; ++i) maxb = std::max<int64_t>(maxb, sizes[i]);
+  void *src = nullptr, *dst = nullptr;
+  HIP_OK(hipMalloc(&src, std::max<int64_t>(maxb, 16)));
+  HIP_OK(hipMalloc(&dst, std::max<int64_t>(maxb, 16)));
+  std::vector<uint8_t> h(maxb), back(maxb);
+  bool ok = true;
+  for (int i = 0; i < n_sizes; ++i) {
+    const size_t b = (size_t)sizes[i];
+    double ms = 0;
+    for (int it = 0; it < iters; ++it) {
+      for (size_t k = 0; k < b; ++k) h[k] = (uint8_t)((k * 131 + it * 7 + i) & 0xFF);
+      HIP_OK(hipMemcpy(src, h.data(), b, hipMemcpyHostToDevice));
+      HIP_OK(hipMemset(dst, 0, b));
+      const auto t0 = std::chrono::steady_clock::now();
+      rccl_group_begin();
+      link.send(src, b, st);
+      link.recv(dst, b, st);
+      rccl_group_end();
+      HIP_OK(hipStreamSynchronize(st));
+      ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      HIP_OK(hipMemcpy(back.data(), dst, b, hipMemcpyDeviceToHost));
+      if (std::memcmp(back.data(), h.data(), b) != 0) ok = false;
+    }
+    Json r = Json::object();
+    r["bytes"] = (double)b;
+    r["avg_ms"] = ms / std::max(1, iters);
+    res.push(r);
+  }
+  rep["results"] = res;
+  rep["ok"] = ok;
+  rep["bytes_sent"] = (double)link.bytes_sent;
+  rep["msgs_sent"] = (double)link.msgs_sent;
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipStreamDestroy(st);
+  g_str = rep.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
+}
+
+// can RCCL put `n` ranks of one communicator on these devices (e.g. the same GPU twice)?
+const char* mp_rccl_probe_devices(const int* devices, int n) {
+  API_TRY
+  std::vector<void*> comms;
+  std::string err;
+  const bool ok = rccl_init_all(std::vector<int>(devices, devices + n), &comms, &err);
+  for (void* c : comms) rccl_comm_destroy(c);
+  Json r = Json::object();
+  r["ok"] = ok;
+  r["error"] = err;
+  g_str = r.dump();
+  return g_str.c_str();
+  API_CATCH(nullptr)
 }
 
 }  // extern "C"

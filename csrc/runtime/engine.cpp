@@ -295,6 +295,36 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   }
   build_links(j);
   for (auto& l : links_) l->set_timeout(j.get_num("link_timeout_s", 600.0));
+  // Stage-boundary wire format: the residual stream is f32 inside a stage; between
+  // GPUs it travels as bf16 by default over RCCL (half the xGMI bytes: 16 KiB per 70B token), f32
+  // elsewhere (LocalLink emulation and TCP keep PP=S bitwise equal to PP=1).  Every rank derives
+  // the same choice from the shared config.
+  {
+    const std::string ad = j.get_str("act_dtype", "auto");
+    const std::string lk = S_ > 1 ? std::string(links_.empty() ? "none" : links_.front()->kind()) : "none";
+    if (ad == "auto") act_dtype_ = (!cpu_ && lk == "rccl") ? ACT_BF16 : ACT_F32;
+    else if (ad == "f32") act_dtype_ = ACT_F32;
+    else if (ad == "f16") act_dtype_ = ACT_F16;
+    else if (ad == "bf16") act_dtype_ = ACT_BF16;
+    else throw std::runtime_error("act_dtype must be auto, f32, f16 or bf16");
+    if (cpu_) act_dtype_ = ACT_F32;
+    if (act_dtype_ != ACT_F32 && S_ > 1) {
+      const size_t wb = (size_t)std::max(chunk_, B_) * cfg_.d_model * 2;
+      for (auto& w : workers_) {
+        HIP_OK(hipSetDevice(w->device));
+        for (int mb = 0; mb < M_; ++mb) {
+          void *o = nullptr, *i = nullptr;
+          HIP_OK(hipMalloc(&o, wb));
+          HIP_OK(hipMalloc(&i, wb));
+          w->wire_out.push_back(o);
+          w->wire_in.push_back(i);
+        }
+      }
+    }
+    if (S_ > 1)
+      MP_LOGI("stage boundary: %s activations, %.1f KiB per token", act_dtype_ == ACT_F32 ? "f32" : act_dtype_ == ACT_F16 ? "f16" : "bf16",
+              cfg_.d_model * (act_dtype_ == ACT_F32 ? 4 : 2) / 1024.0);
+  }
   rounds_cap_ = max_ctx_ + 2;
   if (cpu_) {
     out_vec_.resize((size_t)rounds_cap_ * M_ * B_);
@@ -323,6 +353,8 @@ Engine::~Engine() {
       continue;
     }
     (void)hipSetDevice(w->device);
+    for (void* p : w->wire_out) (void)hipFree(p);
+    for (void* p : w->wire_in) (void)hipFree(p);
     for (auto e : w->comp_ev) (void)hipEventDestroy(e);
     for (auto e : w->sent_ev) (void)hipEventDestroy(e);
     for (auto e : w->recv_ev) (void)hipEventDestroy(e);
@@ -359,9 +391,9 @@ void Engine::build_links(const Json& j) {
       } else if (kind == "rccl") {
         void *ca, *cb;
         rccl_make_pair(specs_[a].device, specs_[b].device, &ca, &cb);
-        links_.emplace_back(new RcclLink(ca, 0, specs_[a].device));   // sender end
+        links_.emplace_back(new RcclLink(ca, 0, 1, specs_[a].device));   // sender end (rank 0 -> 1)
         Link* snd = links_.back().get();
-        links_.emplace_back(new RcclLink(cb, 1, specs_[b].device));   // receiver end
+        links_.emplace_back(new RcclLink(cb, 1, 0, specs_[b].device));   // receiver end
         Link* rcv = links_.back().get();
         workers_[a]->out = snd;
         workers_[b]->in = rcv;
@@ -371,7 +403,7 @@ void Engine::build_links(const Json& j) {
         workers_[b]->in = links_.back().get();
       }
     }
-    MP_LOGI("links: %d x %s (act %.1f KiB/token, ring %d B/token)", S_, kind.c_str(), cfg_.d_model * 4 / 1024.0, 4);
+    MP_LOGI("links: %d x %s (token ring %d B per sequence)", S_, kind.c_str(), 4);
   } else if (cpu_ || j.get_str("link", "rccl") == "tcp") {
     // one TCP connection per link: receiver of link l (rank l+1) listens on base_port + l,
     // sender (rank l) connects to hosts[l+1].  Accept runs on a helper thread so the ring cannot
@@ -416,8 +448,10 @@ void Engine::build_links(const Json& j) {
     for (int l : {std::min(in_l, out_l), std::max(in_l, out_l)}) {
       auto id = unhex(ids[l].str());
       const bool sender = (l == out_l);
-      void* c = rccl_init_rank(id.data(), sender ? 0 : 1, w.device);
-      links_.emplace_back(new RcclLink(c, sender ? 0 : 1, w.device));
+      // a 2-rank communicator per link direction (rank 0 sends, rank 1 receives): every link is
+      // its own FIFO, so the ring cannot deadlock on RCCL's per-communicator ordering
+      void* c = rccl_init_rank(id.data(), 2, sender ? 0 : 1, w.device);
+      links_.emplace_back(new RcclLink(c, sender ? 0 : 1, sender ? 1 : 0, w.device));
       if (sender) w.out = links_.back().get();
       else w.in = links_.back().get();
     }
@@ -550,13 +584,18 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
     HIP_OK(hipEventSynchronize(w.tr_base));
     w.tr_base_ms = now_ms();
   }
+  const bool wire = act_dtype_ != ACT_F32;
   auto recv_into = [&](int mb, void* buf, size_t bytes) {
     if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(w.recv_st, w.sent_ev[mb], 0));
     HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
     HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
-    span(w, w.recv_st, 2, "recv act mb" + std::to_string(mb), [&] { w.in->recv(buf, bytes, w.recv_st); });
+    // 2-byte wire: receive into the staging buffer, widen to the f32 residual on the compute stream
+    void* dst = wire ? w.wire_in[mb] : buf;
+    const size_t nb = wire ? bytes / 2 : bytes;
+    span(w, w.recv_st, 2, "recv act mb" + std::to_string(mb), [&] { w.in->recv(dst, nb, w.recv_st); });
     HIP_OK(hipEventRecord(w.recv_ev[mb], w.recv_st));
     HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
+    if (wire) launch_act_unpack(dst, static_cast<float*>(buf), (int64_t)(bytes / 4), act_dtype_, cs);
   };
   auto send_from = [&](int mb, const void* buf, size_t bytes) {
     if (fault_hook(w, "send")) return;
@@ -566,6 +605,13 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
          [&] { w.out->send(buf, bytes, w.send_st); });
     HIP_OK(hipEventRecord(w.sent_ev[mb], w.send_st));
     w.sent_valid[mb] = true;
+  };
+  // activations: narrowed to the wire format on the compute stream (the previous send of this
+  // micro-batch's staging buffer is complete: the compute stream waited for sent_ev[mb])
+  auto send_act = [&](int mb, const float* buf, size_t bytes) {
+    if (!wire) return send_from(mb, buf, bytes);
+    launch_act_pack(buf, w.wire_out[mb], (int64_t)(bytes / 4), act_dtype_, cs);
+    send_from(mb, w.wire_out[mb], bytes / 2);
   };
   for (const Item& it : items) {
     const int mb = it.mb;
@@ -578,7 +624,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
         else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
         span(w, cs, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T),
              [&] { st.prefill(mb, it.segs, cs); });
-        if (!last) send_from(mb, st.act(mb), bytes);
+        if (!last) send_act(mb, st.act(mb), bytes);
         break;
       }
       case Item::PREFILL_END: {
@@ -605,7 +651,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
                                 hipMemcpyDeviceToHost, cs));
         }
         if (S_ > 1) {
-          if (!last) send_from(mb, st.act(mb), (size_t)B_ * d4);
+          if (!last) send_act(mb, st.act(mb), (size_t)B_ * d4);
           else send_from(mb, st.tokens(mb), (size_t)B_ * 4);
           if (first) post_ring_recv(w, mb);
         }

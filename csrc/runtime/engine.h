@@ -126,6 +126,8 @@ class Engine {
     hipEvent_t tr_base = nullptr;
     double tr_base_ms = 0;
     int device = 0;
+    // act_dtype != f32: per micro-batch device staging of the 2-byte wire format
+    std::vector<void*> wire_out, wire_in;
   };
 
   void build_links(const Json& cfg);
@@ -156,6 +158,7 @@ class Engine {
   bool cpu_ = false;
   bool trace_ = false, failed_ = false;
   bool packed_prefill_ = true;   // several sequences per prefill chunk (config "packed_prefill")
+  int act_dtype_ = 0;            // stage-boundary activation wire format (ActDtype; config "act_dtype")
   double trace_t0_ = 0, watchdog_s_ = 600;
   std::vector<std::string> trace_events_;
   Json fault_;

@@ -15,7 +15,7 @@ struct GemvParams {
   const uint8_t* W;      // T16-packed weights
   const f16* X;          // activations [M][ldx] (K_pad columns, zero tail)
   int ldx;
-  int M;                 // rows of X (<= 32 for gemv)
+  int M;                 // rows of X (<= 64 for gemv)
   float* Y;              // EPI_STORE / EPI_ATOMIC destination [M][ldy]
   int ldy;
   f16* H;                // EPI_SWIGLU destination [M][ldh]
@@ -25,8 +25,7 @@ struct GemvParams {
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
-void set_gemv_wpb(int waves_per_block);   // 1 or 2 (tuning knob)
-void set_gemv_tpw(int tiles_per_wave);    // 0 = auto, 1, 2, 4 (tuning knob)
+void set_gemv_tpw(int tiles_per_wave);    // M > 32 tiles per wave: 0 = auto, 1, 2 (tuning knob)
 int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)
 // Cold-weight sweep on MI355X (tools/gemv_bench.py, 70B shapes): ~4096 tile-waves per launch
@@ -141,6 +140,10 @@ void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStrea
 
 // standalone SwiGLU: h[m][j] = silu(g[m][j]) * u[m][j]   (g,u f32; h f16)
 void launch_swiglu(const float* gu, int ld, int F, int M, f16* h, int ldh, hipStream_t st);
+// stage-boundary activation wire format: f32 residual <-> f16 / bf16 (n elements, contiguous)
+enum ActDtype : int { ACT_F32 = 0, ACT_F16 = 1, ACT_BF16 = 2 };
+void launch_act_pack(const float* x, void* y, int64_t n, int dtype, hipStream_t st);
+void launch_act_unpack(const void* y, float* x, int64_t n, int dtype, hipStream_t st);
 // f32 -> f16 row conversion (used when an activation feeds a GEMM directly)
 void launch_f32_to_f16(const float* x, int ldx, int n, int M, f16* y, int ldy, hipStream_t st);
 

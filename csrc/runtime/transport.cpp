@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -114,39 +115,54 @@ void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- RCCL
-RcclLink::RcclLink(void* comm, int my_rank, int device) : comm_(comm), rank_(my_rank), dev_(device) {}
+RcclLink::RcclLink(void* comm, int my_rank, int peer, int device, bool owns_comm)
+    : comm_(comm), rank_(my_rank), peer_(peer), dev_(device), owns_(owns_comm) {}
 RcclLink::~RcclLink() {
-  if (comm_) ncclCommDestroy((ncclComm_t)comm_);
+  if (comm_ && owns_) ncclCommDestroy((ncclComm_t)comm_);
 }
 void RcclLink::abort() {
-  if (comm_) { ncclCommAbort((ncclComm_t)comm_); comm_ = nullptr; }
+  if (comm_ && owns_) ncclCommAbort((ncclComm_t)comm_);
+  comm_ = nullptr;
 }
 void RcclLink::send(const void* buf, size_t bytes, hipStream_t st) {
-  if (rank_ != 0) throw std::runtime_error("RcclLink: receiver end cannot send");
-  NCCL_OK(ncclSend(buf, bytes, ncclUint8, 1, (ncclComm_t)comm_, st));
+  if (!comm_) throw std::runtime_error("RcclLink: aborted");
+  NCCL_OK(ncclSend(buf, bytes, ncclUint8, peer_, (ncclComm_t)comm_, st));
   bytes_sent += bytes;
   ++msgs_sent;
 }
 void RcclLink::recv(void* buf, size_t bytes, hipStream_t st) {
-  if (rank_ != 1) throw std::runtime_error("RcclLink: sender end cannot recv");
-  NCCL_OK(ncclRecv(buf, bytes, ncclUint8, 0, (ncclComm_t)comm_, st));
+  if (!comm_) throw std::runtime_error("RcclLink: aborted");
+  NCCL_OK(ncclRecv(buf, bytes, ncclUint8, peer_, (ncclComm_t)comm_, st));
+}
+
+bool rccl_init_all(const std::vector<int>& devices, std::vector<void*>* comms, std::string* err) {
+  std::vector<ncclComm_t> c(devices.size());
+  std::vector<int> devs(devices);
+  const ncclResult_t r = ncclCommInitAll(c.data(), (int)devs.size(), devs.data());
+  if (r != ncclSuccess) {
+    if (err) *err = ncclGetErrorString(r);
+    return false;
+  }
+  comms->assign(c.begin(), c.end());
+  return true;
 }
 
 void rccl_make_pair(int dev_a, int dev_b, void** comm_a, void** comm_b) {
-  ncclComm_t comms[2];
-  int devs[2] = {dev_a, dev_b};
-  NCCL_OK(ncclCommInitAll(comms, 2, devs));
-  *comm_a = comms[0];
-  *comm_b = comms[1];
+  std::vector<void*> c;
+  std::string err;
+  if (!rccl_init_all({dev_a, dev_b}, &c, &err)) throw std::runtime_error("RCCL error: " + err);
+  *comm_a = c[0];
+  *comm_b = c[1];
 }
 
-void* rccl_init_rank(const uint8_t* id128, int rank, int device) {
+void* rccl_init_rank(const uint8_t* id128, int nranks, int rank, int device) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  if (nranks < 1 || rank < 0 || rank >= nranks) throw std::runtime_error("rccl_init_rank: bad rank / nranks");
   ncclUniqueId id;
   std::memcpy(&id, id128, 128);
   HIP_OK(hipSetDevice(device));
   ncclComm_t c;
-  NCCL_OK(ncclCommInitRank(&c, 2, id, rank));
+  NCCL_OK(ncclCommInitRank(&c, nranks, id, rank));
   return c;
 }
 
@@ -155,6 +171,19 @@ int rccl_unique_id(uint8_t* out128) {
   NCCL_OK(ncclGetUniqueId(&id));
   std::memcpy(out128, &id, 128);
   return 0;
+}
+
+void rccl_group_begin() { NCCL_OK(ncclGroupStart()); }
+void rccl_group_end() { NCCL_OK(ncclGroupEnd()); }
+void rccl_comm_destroy(void* comm) {
+  if (comm) ncclCommDestroy((ncclComm_t)comm);
+}
+const char* rccl_version_string() {
+  static char buf[32];
+  int v = 0;
+  ncclGetVersion(&v);
+  snprintf(buf, sizeof buf, "%d.%d.%d", v / 10000, (v / 100) % 100, v % 100);
+  return buf;
 }
 
 // ---------------------------------------------------------------- TCP

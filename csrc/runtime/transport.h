@@ -78,28 +78,40 @@ class HostLink : public Link {
 };
 
 // ---------------------------------------------------------------- RcclLink
-struct RcclComm;  // opaque (ncclComm_t)
+// One direction between this rank and `peer` of an RCCL communicator (ncclSend / ncclRecv on
+// the caller's stream).  The communicator may be a 2-rank one per link (the default pipeline
+// wiring: one FIFO per direction), or any larger communicator; peer == own rank is a self loop
+// (ws = 1 tests), whose send and recv must be issued inside one rccl_group_begin/end pair.
 class RcclLink : public Link {
  public:
-  // rank 0 = sender, rank 1 = receiver of this direction
-  RcclLink(void* nccl_comm, int my_rank, int device);
+  RcclLink(void* nccl_comm, int my_rank, int peer, int device, bool owns_comm = true);
   ~RcclLink() override;
   void send(const void* buf, size_t bytes, hipStream_t st) override;
   void recv(void* buf, size_t bytes, hipStream_t st) override;
   const char* kind() const override { return "rccl"; }
   void abort() override;
+  int rank() const { return rank_; }
+  int peer() const { return peer_; }
 
  private:
   void* comm_;
-  int rank_;
+  int rank_, peer_;
   [[maybe_unused]] int dev_;
+  bool owns_;
 };
 
+// creates the communicator ends of `n` devices inside one process (ncclCommInitAll); returns false
+// (and sets *err) when RCCL refuses the device list (e.g. the same GPU twice)
+bool rccl_init_all(const std::vector<int>& devices, std::vector<void*>* comms, std::string* err);
 // creates the two ends of a link between devices a -> b inside one process (ncclCommInitAll)
 void rccl_make_pair(int dev_a, int dev_b, void** comm_a, void** comm_b);
-// multi-process: init this rank's end from a 128-byte unique id (rank 0 = sender)
-void* rccl_init_rank(const uint8_t* id128, int rank, int device);
+// multi-process: init this rank's end of an `nranks` communicator from a 128-byte unique id
+void* rccl_init_rank(const uint8_t* id128, int nranks, int rank, int device);
 int rccl_unique_id(uint8_t* out128);
+void rccl_group_begin();
+void rccl_group_end();
+void rccl_comm_destroy(void* comm);
+const char* rccl_version_string();
 
 // ---------------------------------------------------------------- TcpLink
 class TcpLink : public Link {

@@ -81,19 +81,34 @@ _SIGS = {
     "mp_engine_tokens": ([c_void_p, c_void_p, c_int, c_int], c_int),
     "mp_engine_logits": ([c_void_p, c_int, c_void_p, c_int], c_int),
     "mp_rccl_unique_id": ([c_void_p], c_int),
-    "mp_set_gemv_wpb": ([c_int], None),
+    "mp_rccl_selftest": ([c_int, c_void_p, c_int, c_int], c_char_p),
+    "mp_rccl_probe_devices": ([c_void_p, c_int], c_char_p),
     "mp_set_gemv_tpw": ([c_int], None),
     "mp_init_packed": ([c_void_p, ctypes.c_size_t, c_int, c_float, ctypes.c_uint64, c_void_p], c_int),
     "mp_tok_pretokenize": ([c_char_p, c_int], c_char_p),
 }
 
 
+def _make(*extra, quiet=True):
+    cmd = ["make", "-C", REPO_DIR, "-j", str(min(16, os.cpu_count() or 4)), *extra]
+    return subprocess.run(cmd, capture_output=quiet, text=True)
+
+
 def build(force: bool = False, quiet: bool = True) -> str:
-    """Compile the native library in-tree with hipcc (gfx950)."""
-    if os.path.exists(LIB_PATH) and not force:
-        return LIB_PATH
-    cmd = ["make", "-C", REPO_DIR, "-j", str(min(16, os.cpu_count() or 4))]
-    r = subprocess.run(cmd, capture_output=quiet, text=True)
+    """Compile the native library in-tree with hipcc (gfx950).
+
+    Staleness is make's business (it tracks every kernel / runtime source and header): `make -q`
+    tells whether the in-tree library is current, and an out-of-date one is rebuilt rather than
+    tested against newer sources."""
+    if not force and os.path.exists(LIB_PATH) and os.environ.get("MIPIPE_LIB"):
+        return LIB_PATH   # an explicitly selected A/B build is used as is
+    if not force and os.path.exists(LIB_PATH):
+        try:
+            if _make("-q", "all", quiet=True).returncode == 0:
+                return LIB_PATH
+        except OSError:   # no make on this machine: use what is there
+            return LIB_PATH
+    r = _make(quiet=quiet)
     if r.returncode != 0:
         raise RuntimeError("native build failed:\n" + (r.stdout or "")[-4000:] + (r.stderr or "")[-4000:])
     return LIB_PATH

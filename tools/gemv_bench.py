@@ -27,19 +27,16 @@ def main():
     ap.add_argument("--shapes", default="70b.qkv,70b.o,70b.gateup,70b.down,70b.head")
     ap.add_argument("--types", default="Q4_K")
     ap.add_argument("--M", default="1,16")
-    ap.add_argument("--tpw", default="1,2,4")
+    ap.add_argument("--tpw", default="0", help="tiles per wave at M > 32: 0 auto, 1, 2")
     ap.add_argument("--splits", default="auto")
     ap.add_argument("--iters", type=int, default=24)
     ap.add_argument("--target", type=int, default=2048)
     ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 store, 1 atomic): timing probes")
-    ap.add_argument("--probe", type=int, default=0, help="3: loads only, 4: weight+x loads, 5: dequant+MFMA without x loads")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for sname in a.shapes.split(","):
         n, k, epi = SHAPES[sname]
-        if a.probe:
-            epi = a.probe
         if a.epi >= 0:
             epi = a.epi
         for tname in a.types.split(","):
@@ -61,7 +58,7 @@ def main():
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
                 for tpw in [int(t) for t in a.tpw.split(",")]:
                     L.mp_set_gemv_tpw(tpw)
-                    waves = (ntiles + tpw - 1) // tpw
+                    waves = (ntiles + max(tpw, 1) - 1) // max(tpw, 1)
                     if epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
                         splits = [1]
                     elif a.splits == "auto":
