@@ -226,6 +226,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
   const float* row = p.qkv + (size_t)t * p.ldqkv;
   const float2* cs = p.rope_cs + (size_t)pos * hd2;
   const int32_t* bt = p.block_table + (size_t)slot * p.max_pages;
+  // deferred RMSNorm of the projection GEMV: value i of q|k|v = nrs * row[i] + bias[i]
+  const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
+  auto qkv_at = [&](int i) { return p.bias ? fmaf(nrs, row[i], p.bias[i]) : nrs * row[i]; };
 
   const int start = z * p.split_len;
   const int end = min(start + p.split_len, kvlen);
@@ -237,20 +240,20 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
   // 1. append the new token's K (rotated) and V to the cache (the split that will read it)
   if (start <= pos && pos < end) {
     const int page = bt[pos >> 6], idx = pos & 63;
-    const float* kr = row + p.Hq * p.hd + kvh * p.hd;
-    const float* vr = row + (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
+    const int kr = p.Hq * p.hd + kvh * p.hd;
+    const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
     f16* kd = p.k_cache + (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
     f16* vd = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
     for (int j = threadIdx.x; j < DP / 2; j += 256) {
       half2_t o = {(f16)0.f, (f16)0.f};
       if (j < hd2) {
-        const float x0 = kr[2 * j], x1 = kr[2 * j + 1];
+        const float x0 = qkv_at(kr + 2 * j), x1 = qkv_at(kr + 2 * j + 1);
         const float2 c = cs[j];
         o = half2_t{(f16)(x0 * c.x - x1 * c.y), (f16)(x0 * c.y + x1 * c.x)};
       }
       *reinterpret_cast<half2_t*>(kd + 2 * j) = o;
     }
-    for (int d = threadIdx.x; d < DP; d += 256) vd[(size_t)d * 64] = (f16)(d < p.hd ? vr[d] : 0.f);
+    for (int d = threadIdx.x; d < DP; d += 256) vd[(size_t)d * 64] = (f16)(d < p.hd ? qkv_at(vr + d) : 0.f);
     __threadfence_block();
     __syncthreads();
   }
@@ -268,12 +271,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
       half8_t v = {};
       if (rvalid) {
         const int d0 = 32 * kk + 8 * q4;
-        const float* qr = row + (size_t)h * p.hd;
+        const int qr = h * p.hd;
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const int d = d0 + j;
           if (d < p.hd) {
-            const float x0 = qr[d], x1 = qr[d + 1];
+            const float x0 = qkv_at(qr + d), x1 = qkv_at(qr + d + 1);
             const float2 c = cs[d >> 1];
             v[j] = (f16)((x0 * c.x - x1 * c.y) * p.q_scale);
             v[j + 1] = (f16)((x0 * c.y + x1 * c.x) * p.q_scale);
@@ -377,7 +380,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     }
   }
   if (n_act == 1) return;
-  // 4. last arriver of this (token, kv head) merges the splits
+  // 4. last arriver of this (token, kv head) merges the splits.
+  // Hand-off invariant (MI355X_MICROARCH.md 'Valid forms', first row of the sc1 table, measured on
+  // gfx950 / ROCm 7.2 rather than guaranteed by the memory model): EVERY store of the partials is an
+  // agent-scope relaxed (sc1, write-through) store, every storing wave drains them (vmcnt(0)) before
+  // the workgroup barrier, ONE lane then adds to ONE unsharded counter, the workgroup whose add
+  // returned n_act - 1 is the last arriver, and EVERY load of the partials below is an sc1 load
+  // (ld_sc1), issued after the barrier that the adding wave joins.  Changing any of these (plain
+  // stores or loads, a flag store instead of the counter, a read before the barrier) needs the
+  // agent release/acquire fences instead.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -36,6 +36,36 @@ __device__ __forceinline__ half2_t h2hi(half2_t v) { return half2_t{v.y, v.y}; }
 __device__ __forceinline__ half2_t h2splat(float v) { f16 h = (f16)v; return half2_t{h, h}; }
 __device__ __forceinline__ half2_t h2c(float v) { return half2_t{(f16)v, (f16)v}; }
 
+// Weight sources for Deq<PT>::load (offsets in bytes from the chunk start).
+//   PtrSrc: flat global loads.
+//   BufSrc: raw buffer loads through a wave-uniform descriptor over [base, base + num_records):
+//           a load past the range returns zeros WITHOUT touching memory, so a fixed-depth
+//           prefetch ring can run past the end of a wave's super-block range at no HBM cost
+//           (the loads stay unconditional: path-independent vmcnt).
+struct PtrSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ u32x4 q16nt(int o) const { return ld16_nt(p + o); }
+  __device__ __forceinline__ u32x4 q16(int o) const { return ld16(p + o); }
+  __device__ __forceinline__ uint32_t q4nt(int o) const { return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p + o)); }
+  __device__ __forceinline__ uint32_t q4(int o) const { return *reinterpret_cast<const uint32_t*>(p + o); }
+  __device__ __forceinline__ u32x2 q8nt(int o) const { return __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p + o)); }
+  __device__ __forceinline__ uint32_t q2(int o) const { return *reinterpret_cast<const uint16_t*>(p + o); }
+};
+struct BufSrc {
+  __amdgpu_buffer_rsrc_t r;
+  int base;   // chunk offset within the descriptor's range
+  __device__ __forceinline__ u32x4 q16nt(int o) const { return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, base + o, 0, 2)); }
+  __device__ __forceinline__ u32x4 q16(int o) const { return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, base + o, 0, 0)); }
+  __device__ __forceinline__ uint32_t q4nt(int o) const { return __builtin_amdgcn_raw_buffer_load_b32(r, base + o, 0, 2); }
+  __device__ __forceinline__ uint32_t q4(int o) const { return __builtin_amdgcn_raw_buffer_load_b32(r, base + o, 0, 0); }
+  __device__ __forceinline__ u32x2 q8nt(int o) const { return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, base + o, 0, 2)); }
+  __device__ __forceinline__ uint32_t q2(int o) const { return __builtin_amdgcn_raw_buffer_load_b16(r, base + o, 0, 0); }
+};
+// gfx9 raw-buffer descriptor word 3 (DATA_FORMAT 32, no swizzle)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
 template <int PT> struct Deq;
 
 struct Consts { uint32_t mlo, mhi, mag_hi, mag_lo; };
@@ -74,10 +104,12 @@ __device__ __forceinline__ void kquarter_scales(const u32x4& hdr, int lane, half
 template <> struct Deq<P_Q4_K> {
   static constexpr int CB = chunk_bytes(P_Q4_K);
   struct Raw { u32x4 q0, q1, hdr; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
-    r.q0 = ld16_nt(c + lane * 16);
-    r.q1 = ld16_nt(c + 1024 + lane * 16);
-    r.hdr = ld16(c + 2048 + (lane & 15) * 16);
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+    r.q0 = c.q16nt(lane * 16);
+    r.q1 = c.q16nt(1024 + lane * 16);
+    r.hdr = c.q16(2048 + (lane & 15) * 16);
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
@@ -101,12 +133,14 @@ template <> struct Deq<P_Q4_K> {
 template <> struct Deq<P_Q5_K> {
   static constexpr int CB = chunk_bytes(P_Q5_K);
   struct Raw { u32x4 q0, q1, hdr; uint32_t qh0, qh1; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
-    r.q0 = ld16_nt(c + lane * 16);
-    r.q1 = ld16_nt(c + 1024 + lane * 16);
-    r.qh0 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(c + 2048 + lane * 4));
-    r.qh1 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(c + 2048 + 256 + lane * 4));
-    r.hdr = ld16(c + 2560 + (lane & 15) * 16);
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+    r.q0 = c.q16nt(lane * 16);
+    r.q1 = c.q16nt(1024 + lane * 16);
+    r.qh0 = c.q4nt(2048 + lane * 4);
+    r.qh1 = c.q4nt(2048 + 256 + lane * 4);
+    r.hdr = c.q16(2560 + (lane & 15) * 16);
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
@@ -136,14 +170,16 @@ template <> struct Deq<P_Q5_K> {
 template <> struct Deq<P_Q6_K> {
   static constexpr int CB = chunk_bytes(P_Q6_K);
   struct Raw { u32x4 q0, q1; u32x2 qh0, qh1; uint32_t sc, d; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
-    r.q0 = ld16_nt(c + lane * 16);
-    r.q1 = ld16_nt(c + 1024 + lane * 16);
-    r.qh0 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(c + 2048 + lane * 8));
-    r.qh1 = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(c + 2048 + 512 + lane * 8));
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+    r.q0 = c.q16nt(lane * 16);
+    r.q1 = c.q16nt(1024 + lane * 16);
+    r.qh0 = c.q8nt(2048 + lane * 8);
+    r.qh1 = c.q8nt(2048 + 512 + lane * 8);
     // int8 scales of this lane's 16-wide sub-blocks 4g..4g+3: dword g of the row's 16 scales
-    r.sc = *reinterpret_cast<const uint32_t*>(c + 3072 + (lane & 15) * 16 + 4 * (lane >> 4));
-    r.d = *reinterpret_cast<const uint16_t*>(c + 3328 + (lane & 15) * 2);
+    r.sc = c.q4(3072 + (lane & 15) * 16 + 4 * (lane >> 4));
+    r.d = c.q2(3328 + (lane & 15) * 2);
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
@@ -176,12 +212,14 @@ template <> struct Deq<P_Q6_K> {
 template <> struct Deq<P_Q8_0> {
   static constexpr int CB = chunk_bytes(P_Q8_0);
   struct Raw { u32x4 a0, a1, b0, b1; uint32_t dd; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
-    r.a0 = ld16_nt(c + lane * 32);
-    r.a1 = ld16_nt(c + lane * 32 + 16);
-    r.b0 = ld16_nt(c + 2048 + lane * 32);
-    r.b1 = ld16_nt(c + 2048 + lane * 32 + 16);
-    r.dd = *reinterpret_cast<const uint32_t*>(c + 4096 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+    r.a0 = c.q16nt(lane * 32);
+    r.a1 = c.q16nt(lane * 32 + 16);
+    r.b0 = c.q16nt(2048 + lane * 32);
+    r.b1 = c.q16nt(2048 + lane * 32 + 16);
+    r.dd = c.q4(4096 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
@@ -205,10 +243,12 @@ template <> struct Deq<P_Q8_0> {
 template <> struct Deq<P_Q4_0> {
   static constexpr int CB = chunk_bytes(P_Q4_0);
   struct Raw { u32x4 q0, q1; uint32_t dd; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
-    r.q0 = ld16_nt(c + lane * 16);
-    r.q1 = ld16_nt(c + 1024 + lane * 16);
-    r.dd = *reinterpret_cast<const uint32_t*>(c + 2048 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+    r.q0 = c.q16nt(lane * 16);
+    r.q1 = c.q16nt(1024 + lane * 16);
+    r.dd = c.q4(2048 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
@@ -230,9 +270,11 @@ template <> struct Deq<P_Q4_0> {
 template <> struct Deq<P_F16> {
   static constexpr int CB = chunk_bytes(P_F16);
   struct Raw { u32x4 v[8]; };
-  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) {
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = ld16_nt(c + i * 1024 + lane * 16);
+    for (int i = 0; i < 8; ++i) r.v[i] = c.q16nt(i * 1024 + lane * 16);
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {

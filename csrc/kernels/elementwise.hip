@@ -199,6 +199,78 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* logits, int l
   }
 }
 
+// Two-level argmax: grid (nchunk, M) workgroups each reduce one chunk of a row, publish a
+// (value, index) partial and count in; the last arriver of the row reduces the nchunk partials.
+// (One 1024-thread workgroup per row read 513 KB of Llama-3 logits in 38 us at M = 1.)
+// Hand-off per MI355X_MICROARCH.md 'Valid forms': plain partial store by one lane -> agent release
+// fence -> asm vmcnt(0) -> relaxed agent counter add; the last arriver (told by the value its add
+// returned) -> agent acquire fence -> vmcnt(0) -> barrier -> plain loads.  Ties -> lowest index.
+__device__ __forceinline__ bool am_better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
+
+__global__ __launch_bounds__(256) void argmax2_kernel(const float* logits, int ld, int n, int chunk,
+                                                      float2* part, int32_t* counters, int32_t* tok) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ int last;
+  const int m = blockIdx.y, c = blockIdx.x, nchunk = gridDim.x;
+  const float* r = logits + (size_t)m * ld;
+  const int i0 = c * chunk, i1 = min(n, i0 + chunk);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = i0 + threadIdx.x * 4; i < i1; i += 1024) {
+    if (i + 4 <= i1 && ((ld | i0) & 3) == 0) {
+      const float4 v = *reinterpret_cast<const float4*>(r + i);
+      if (am_better(v.x, i, bv, bi)) { bv = v.x; bi = i; }
+      if (am_better(v.y, i + 1, bv, bi)) { bv = v.y; bi = i + 1; }
+      if (am_better(v.z, i + 2, bv, bi)) { bv = v.z; bi = i + 2; }
+      if (am_better(v.w, i + 3, bv, bi)) { bv = v.w; bi = i + 3; }
+    } else {
+      for (int k = i; k < i + 4 && k < i1; ++k)
+        if (am_better(r[k], k, bv, bi)) { bv = r[k]; bi = k; }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (am_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; ++k)
+      if (am_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
+    part[(size_t)m * nchunk + c] = make_float2(bv, __int_as_float(bi));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(counters + m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == nchunk - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= 64) return;
+  bv = -INFINITY;
+  bi = 0x7fffffff;
+  for (int k = threadIdx.x; k < nchunk; k += 64) {
+    const float2 pv = part[(size_t)m * nchunk + k];
+    if (am_better(pv.x, __float_as_int(pv.y), bv, bi)) { bv = pv.x; bi = __float_as_int(pv.y); }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (am_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  if (threadIdx.x == 0) {
+    tok[m] = bi == 0x7fffffff ? 0 : bi;
+    __hip_atomic_store(counters + m, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
   const int i = threadIdx.x;
   if (i < M) { const int p = pos[i] + 1; pos[i] = p; kvlen[i] = p + 1; }
@@ -278,8 +350,18 @@ void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {
   hipLaunchKernelGGL(mpk::rope_kv_kernel, dim3(p.M, (p.Hq + 2 * p.Hkv + 3) / 4), dim3(256), 0, st, p);
 }
 
-void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::argmax_kernel, dim3(M), dim3(1024), 0, st, logits, ld, n, tokens);
+void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st, const ArgmaxScratch* sc) {
+  if (!sc || M > sc->rows) {
+    hipLaunchKernelGGL(mpk::argmax_kernel, dim3(M), dim3(1024), 0, st, logits, ld, n, tokens);
+    return;
+  }
+  // ~2K logits per 256-thread workgroup, at most kArgmaxChunks per row
+  int nchunk = (n + 2047) / 2048;
+  nchunk = nchunk < 1 ? 1 : nchunk > kArgmaxChunks ? kArgmaxChunks : nchunk;
+  const int chunk = (((n + nchunk - 1) / nchunk) + 3) & ~3;
+  nchunk = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(mpk::argmax2_kernel, dim3(nchunk, M), dim3(256), 0, st, logits, ld, n, chunk,
+                     reinterpret_cast<float2*>(sc->part), sc->counters, tokens);
 }
 
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {

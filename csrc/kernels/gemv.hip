@@ -57,6 +57,7 @@ static void read_env() {
   if (g_env) return;
   g_env = true;
   if (const char* w = getenv("MIPIPE_GEMV_NW")) g_nw = atoi(w) == 4 ? 4 : 8;
+
   if (const char* w = getenv("MIPIPE_GEMV2_TW")) g_tw2 = atoi(w) == 2 ? 2 : atoi(w) == 1 ? 1 : 0;
 }
 static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
@@ -75,8 +76,10 @@ void set_gemv_tpw(int t) {
 }
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
+  read_env();
   if (nsplit < 1) nsplit = 1;
   if (p.M < 1 || p.M > 64) throw std::runtime_error("launch_gemv: M must be 1..64 (longer chunks: launch_gemm)");
+  if (p.Xf && p.M > 4) throw std::runtime_error("launch_gemv: the fused RMSNorm takes M <= 4");
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
   launch_gemv2(ptype, epi, p, nsplit, g_nw, gemv2_tw(p.M, epi, p.ntiles), st);

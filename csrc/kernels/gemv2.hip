@@ -35,52 +35,90 @@ constexpr int G2_LDX = 256 + 8;
 // TW weight tiles per wave share every A fragment read from LDS (and a workgroup of NW waves then
 // stages x once for NW * TW tiles): at M = 64 one tile per wave reads 14x more bytes of x (LDS and
 // L2 -> CU) than of weights.
-template <int PT, int EPI, int NW, int NSLOT, int MT, int TW>
+template <int PT, int EPI, int NW, int NSLOT, int MT, int TW, bool NORM>
 __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int NT = NW * 64;
   constexpr int XC = 512 * MT;   // 16 B x chunks per super-block
+  static_assert(!NORM || (MT == 1 && TW == 1), "fused RMSNorm: one row group, M <= 4");
   __shared__ __attribute__((aligned(16))) f16 xs[2][16 * MT * G2_LDX];
+  __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int tile0 = (blockIdx.x * NW + wave) * TW;
   const int sbA = blockIdx.y * p.sb_per_split;
   const int sbB = min(sbA + p.sb_per_split, p.nsb);
   if (sbA >= sbB) return;   // uniform over the workgroup
-  const uint8_t* wt[TW];
+  // each tile's super-block range [sbA, sbB) as a buffer descriptor: ring slots past the end of
+  // the range load zeros without memory traffic (v1 re-loaded the clamped last super-block: up to
+  // NSLOT - 1 redundant chunk loads per wave at 2-4 super-blocks per split)
+  __amdgpu_buffer_rsrc_t wsrc[TW];
 #pragma unroll
-  for (int t = 0; t < TW; ++t) wt[t] = p.W + (size_t)min(tile0 + t, p.ntiles - 1) * p.nsb * CB;
+  for (int t = 0; t < TW; ++t) {
+    const int tl = __builtin_amdgcn_readfirstlane(tile0 + t);
+    const int nb = tl < p.ntiles ? sbB - sbA : 0;
+    wsrc[t] = make_rsrc(p.W + ((size_t)min(tl, p.ntiles - 1) * p.nsb + sbA) * CB, (uint32_t)(nb * CB));
+  }
   const int M = p.M;
 
   // x staging: 16 MT rows x 256 k per super-block = 512 MT chunks of 16 B; thread t owns chunks t, t+NT..
   // The x chunks of super-block j are loaded TOGETHER with its weights (register rings of NSLOT),
   // NSLOT steps ahead, and copied to LDS one step before use: every vmcnt wait then leaves the
   // loads of the NSLOT-1 later super-blocks in flight.
+  // NORM (deferred RMSNorm): the chunk is 8 f32 of the residual row plus 8 of gamma; LDS gets
+  // f16(x * gamma) and the thread accumulates sum(x^2) of its row while staging, so the per-row
+  // factor rsqrt(mean(x^2) + eps) is applied to the accumulators at the end (STORE / SWIGLU: every
+  // workgroup staged the whole row) or by the consumer from the published per-split partial sums
+  // (ATOMIC: p.ssq, the decode attention).  (gamma staged in LDS instead of the register ring took
+  // 199 VGPRs against 164: the compiler kept the per-step LDS gamma reads live across steps.)
   constexpr int XCH = (XC + NT - 1) / NT;
-  u32x4 xv[NSLOT][XCH];
+  constexpr int XW = NORM ? 4 : 1;   // NORM: x (2 x 16 B f32) + gamma (2 x 16 B f32)
+  u32x4 xv[NSLOT][XCH][XW];
   typename D::Raw ring[NSLOT][TW];
   const int last = sbB - 1;
   auto issue = [&](const int sl, const int sb) {
 #pragma unroll
-    for (int t = 0; t < TW; ++t) D::load(ring[sl][t], wt[t] + (size_t)sb * CB, lane);
+    for (int t = 0; t < TW; ++t) D::load(ring[sl][t], BufSrc{wsrc[t], (sb - sbA) * CB}, lane);
+    const int sbx = min(sb, last);
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       const int c = tid + NT * j;
       if (c < XC) {
         const int row = c >> 5, col = (c & 31) * 8;
-        xv[sl][j] = row < M ? *reinterpret_cast<const u32x4*>(p.X + (size_t)row * p.ldx + (size_t)sb * 256 + col)
-                            : u32x4{0u, 0u, 0u, 0u};
+        if constexpr (NORM) {
+          const int k = sbx * 256 + col;
+          const bool in = row < M && k < p.d_norm;
+          const float* src = p.Xf + (size_t)row * p.ldxf + k;
+          xv[sl][j][0] = in ? *reinterpret_cast<const u32x4*>(src) : u32x4{0u, 0u, 0u, 0u};
+          xv[sl][j][1] = in ? *reinterpret_cast<const u32x4*>(src + 4) : u32x4{0u, 0u, 0u, 0u};
+          xv[sl][j][2] = in ? *reinterpret_cast<const u32x4*>(p.gamma + k) : u32x4{0u, 0u, 0u, 0u};
+          xv[sl][j][3] = in ? *reinterpret_cast<const u32x4*>(p.gamma + k + 4) : u32x4{0u, 0u, 0u, 0u};
+        } else {
+          xv[sl][j][0] = row < M ? *reinterpret_cast<const u32x4*>(p.X + (size_t)row * p.ldx + (size_t)sbx * 256 + col)
+                                 : u32x4{0u, 0u, 0u, 0u};
+        }
       }
     }
   };
-  auto store_x = [&](const int sl, const int buf) {
+  float ssn = 0.f;   // NORM: this thread's partial sum(x^2) of its row (c = tid: one row per thread)
+  auto store_x = [&](const int sl, const int buf, const bool count) {
 #pragma unroll
     for (int j = 0; j < XCH; ++j) {
       const int c = tid + NT * j;
       if (c < XC) {
         const int row = c >> 5, col = (c & 31) * 8;
-        *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + (col ^ x_qswap(row))]) = xv[sl][j];
+        u32x4 v;
+        if constexpr (NORM) {
+          const float4 a = __builtin_bit_cast(float4, xv[sl][j][0]), b = __builtin_bit_cast(float4, xv[sl][j][1]);
+          const float4 ga = __builtin_bit_cast(float4, xv[sl][j][2]), gb = __builtin_bit_cast(float4, xv[sl][j][3]);
+          if (count) ssn += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+          v = __builtin_bit_cast(u32x4, half8_t{(f16)(a.x * ga.x), (f16)(a.y * ga.y), (f16)(a.z * ga.z), (f16)(a.w * ga.w),
+                                                (f16)(b.x * gb.x), (f16)(b.y * gb.y), (f16)(b.z * gb.z), (f16)(b.w * gb.w)});
+        } else {
+          v = xv[sl][j][0];
+        }
+        *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + (col ^ x_qswap(row))]) = v;
       }
     }
   };
@@ -91,8 +129,8 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, min(sbA + sl, last));
-  store_x(0, 0);
+  for (int sl = 0; sl < NSLOT; ++sl) issue(sl, sbA + sl);
+  store_x(0, 0, true);
   __syncthreads();
 
   // rows >= M are zero in LDS (their outputs are never stored)
@@ -123,8 +161,8 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 #pragma unroll
         for (int t = 0; t < TW; ++t) acc[t][mt] = mfma16x16x32(a, b[t][s], acc[t][mt]);
       }
-    store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
-    issue(sl, min(cur + NSLOT, last));
+    store_x((sl + 1) % NSLOT, buf ^ 1, cur + 1 < sbB);   // x(cur + 1), loaded NSLOT - 1 steps ago
+    issue(sl, cur + NSLOT);
     __syncthreads();
   };
   int sb = sbA;
@@ -135,6 +173,25 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
 #pragma unroll
   for (int sl = 0; sl < NSLOT - 1; ++sl)   // tail (< NSLOT super-blocks; uniform over the workgroup)
     if (sb + sl < sbB) step(sl, sb + sl);
+  if constexpr (NORM) {
+    // rows r < M <= 4 are staged by threads [32 r, 32 r + 32): reduce over those 32 lanes
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ssn += __shfl_xor(ssn, o);
+    if ((tid & 31) == 0 && (tid >> 5) < 4) red[tid >> 5] = ssn;
+    __syncthreads();
+    if constexpr (EPI == EPI_ATOMIC) {
+      // publish this split's partial sum of squares (one tile group per split adds it)
+      if (p.ssq && blockIdx.x == 0 && tid < M) atomicAdd(p.ssq + tid, red[tid]);
+    } else {
+      // the workgroup staged the whole row: scale its rows' accumulators by rsqrt(mean + eps)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 4 * g + i;
+        const float rs = m < M ? rsqrtf(red[m < 4 ? m : 0] / (float)p.d_norm + p.eps) : 0.f;
+        acc[0][0][i] *= rs;
+      }
+    }
+  }
   // lane holds C[m = 16 mt + 4g + i][n = 16*tile + r]
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
@@ -153,17 +210,27 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
       } else {
         const int n = tile * 16 + r;
         if (n < p.n_valid) {
+          const float bias = (p.bias && blockIdx.y == 0) ? p.bias[n] : 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int m = 16 * mt + 4 * g + i;
             if (m < M) {
               float* dst = p.Y + (size_t)m * p.ldy + n;
-              if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[t][mt][i]);
-              else *dst = acc[t][mt][i];
+              if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[t][mt][i] + bias);
+              else *dst = acc[t][mt][i] + bias;
             }
           }
         }
       }
+    }
+  }
+  if (p.zero) {   // side job: clear zero_n floats (e.g. the consumed q|k|v split-K accumulator)
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y, b = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t per = ((p.zero_n + nb - 1) / nb + 3) & ~(int64_t)3;
+    const int64_t z0 = b * per, z1 = min(p.zero_n, z0 + per);
+    for (int64_t i = z0 + tid * 4; i < z1; i += NT * 4) {
+      if (i + 4 <= z1) *reinterpret_cast<float4*>(p.zero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      else for (int64_t k = i; k < z1; ++k) p.zero[k] = 0.f;
     }
   }
 }
@@ -174,6 +241,14 @@ namespace mp {
 
 template <int PT, int EPI, int NW, int TW>
 static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
+  if constexpr (TW == 1) {
+    if (p.Xf) {   // fused RMSNorm: M <= 4 (checked by launch_gemv)
+      constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+      hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS, 1, 1, true>), dim3((p.ntiles + NW - 1) / NW, nsplit),
+                         dim3(NW * 64), 0, st, p);
+      return;
+    }
+  }
   // super-blocks in flight per wave: 4, fewer for the fat chunks so the kernel stays within
   // 128 VGPRs (4 waves per SIMD = two 8-wave workgroups per CU); two row groups (M <= 32) hold
   // twice the x ring, so one slot less
@@ -181,15 +256,15 @@ static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
   const dim3 block(NW * 64);
   if constexpr (TW == 1) {
     const dim3 grid((p.ntiles + NW - 1) / NW, nsplit);
-    if (p.M <= 16) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS, 1, 1>), grid, block, 0, st, p);
-    else if (p.M <= 32) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, (NS > 2 ? NS - 1 : 2), 2, 1>), grid, block, 0, st, p);
-    else if (p.M <= 48) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 3, 1>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 4, 1>), grid, block, 0, st, p);
+    if (p.M <= 16) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS, 1, 1, false>), grid, block, 0, st, p);
+    else if (p.M <= 32) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, (NS > 2 ? NS - 1 : 2), 2, 1, false>), grid, block, 0, st, p);
+    else if (p.M <= 48) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 3, 1, false>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 4, 1, false>), grid, block, 0, st, p);
   } else {
     // wide row groups only (M > 32), where the A-fragment traffic dominates
     const dim3 grid((p.ntiles + NW * TW - 1) / (NW * TW), nsplit);
-    if (p.M <= 48) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 3, TW>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 4, TW>), grid, block, 0, st, p);
+    if (p.M <= 48) hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 3, TW, false>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, 4, TW, false>), grid, block, 0, st, p);
   }
 }
 

@@ -196,6 +196,24 @@ int mp_op_unpack(int ptype, const void* W, int ntiles, int nsb, void* out, int l
   API_CATCH(-1)
 }
 
+// decode GEMV (gemv2.hip) with its optional fusions: Xf/gamma (deferred RMSNorm of the f32 rows Xf,
+// M <= 4, X unused; ATOMIC publishes sum(x^2) per row to ssq), bias (added once per output),
+// zero/zero_n (cleared after the GEMV)
+int mp_op_gemv_fused(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+                     int ldy, void* H, int ldh, int n_valid, int nsplit, const void* Xf, int ldxf, const void* gamma,
+                     float eps, int d_norm, void* ssq, const void* bias, void* zero, int64_t zero_n, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  p.Xf = (const float*)Xf; p.ldxf = ldxf; p.gamma = (const float*)gamma; p.eps = eps; p.d_norm = d_norm;
+  p.ssq = (float*)ssq; p.bias = (const float*)bias; p.zero = (float*)zero; p.zero_n = zero_n;
+  launch_gemv(ptype, epi, p, nsplit, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_rmsnorm(const void* x, int ldx, const void* w, int d, float eps, void* out, int ldo, int M, void* stream) {
   API_TRY
   launch_rmsnorm((const float*)x, ldx, (const float*)w, d, eps, (f16*)out, ldo, M, nullptr, 0, (hipStream_t)stream);
@@ -245,9 +263,11 @@ int mp_op_attention(const void* q, const void* kvlen, const void* slot, const vo
   API_CATCH(-1)
 }
 
-int mp_op_argmax(const void* logits, int ld, int n, int M, void* tokens, void* stream) {
+int mp_op_argmax(const void* logits, int ld, int n, int M, void* tokens, void* part, void* counters, void* stream) {
   API_TRY
-  launch_argmax((const float*)logits, ld, n, M, (int32_t*)tokens, (hipStream_t)stream);
+  // part [M][kArgmaxChunks][2] f32 + counters [M] zeroed int32 select the two-level kernel
+  ArgmaxScratch sc{(float*)part, (int32_t*)counters, M};
+  launch_argmax((const float*)logits, ld, n, M, (int32_t*)tokens, (hipStream_t)stream, part ? &sc : nullptr);
   HIP_OK(hipGetLastError());
   return 0;
   API_CATCH(-1)

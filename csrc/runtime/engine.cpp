@@ -256,6 +256,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
+  so.fused_norm = j.get_bool("fused_norm", false);
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);
 

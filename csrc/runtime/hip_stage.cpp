@@ -336,7 +336,10 @@ void HipStage::alloc_runtime() {
   xn_ = (f16*)zalloc((size_t)scratch_rows_ * Kd_ * 2);
   attn_ = (f16*)zalloc((size_t)scratch_rows_ * Ko_ * 2);
   h_ = (f16*)zalloc((size_t)scratch_rows_ * Kff_ * 2);
-  qkv_ = (float*)zalloc((size_t)scratch_rows_ * qkv_n_ * 4);
+  // [64 floats: per-row sum of squares of the deferred qkv RMSNorm][rows][q|k|v] f32 split-K
+  // accumulator; one contiguous range so the o-proj's zero side job clears both
+  ssq_ = (float*)zalloc((64 + (size_t)scratch_rows_ * qkv_n_) * 4);
+  qkv_ = ssq_ + 64;
   q_ = (f16*)zalloc((size_t)scratch_rows_ * Hq * Dp_ * 2);
   bool any_unfused = false;
   for (auto& L : layers_) any_unfused |= !L.fused_gateup;
@@ -354,6 +357,9 @@ void HipStage::alloc_runtime() {
   if (spec_.last()) {
     logits_ld_ = (int)round_up(cfg_.vocab, 16);
     logits_ = (float*)zalloc((size_t)B * logits_ld_ * 4);
+    am_.rows = std::max(B, opt_.prefill_chunk);
+    am_.part = (float*)zalloc((size_t)am_.rows * kArgmaxChunks * 2 * 4);
+    am_.counters = (int32_t*)zalloc((size_t)am_.rows * 4);
   }
   int split = opt_.attn_split_len;
   if (split <= 0) {
@@ -527,7 +533,7 @@ void HipStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs
 }
 
 void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
-                    int n_valid, bool allow_split, hipStream_t st) {
+                    int n_valid, bool allow_split, hipStream_t st, const GemvParams* extras) {
   // up to 64 rows (decode micro-batches, short prompt chunks): the dequant GEMV, 1-4 MFMA row
   // groups per weight fragment; longer prompt chunks: MFMA GEMM, weights read once per 64 rows
   // exception: the large gate/up GEMVs that run two tiles per wave (>= 192 workgroups of 16
@@ -543,6 +549,11 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   }
   for (int r0 = 0; r0 < M; r0 += 64) {
     GemvParams p{};
+    if (extras) {   // fused norm / bias / zero-fill: small M only (one pass of this loop)
+      p.Xf = extras->Xf; p.ldxf = extras->ldxf; p.gamma = extras->gamma; p.eps = extras->eps;
+      p.d_norm = extras->d_norm; p.bias = extras->bias; p.zero = extras->zero; p.zero_n = extras->zero_n;
+      p.ssq = extras->ssq;
+    }
     p.W = m.d;
     p.X = X + (size_t)r0 * ldx;
     p.ldx = ldx;
@@ -603,9 +614,27 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
                              const int32_t* slot, bool decode, hipStream_t st) {
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
-  launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st, L.qkv_bias, qkv_n_);
-  for (const MatSeg& s : L.qkv)
-    gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
+  // M <= 4 (fuse_norm): the RMSNorms are folded into the consuming GEMVs (gemv2.hip deferred
+  // norm).  qkv: the split-K GEMV publishes per-row sums of squares to ssq_ and the fused decode
+  // attention applies rsqrt and the bias when it reads q|k|v.  The o-proj then clears ssq_ + the
+  // q|k|v accumulator (invariant: zero outside [qkv GEMV, o-proj]; unfused forwards clear it after
+  // their last layer).
+  const bool small = fuse_norm(M);
+  const bool qkv_deferred = small && decode && opt_.fused_attn;
+  GemvParams nx{};
+  nx.Xf = x; nx.ldxf = d; nx.eps = cfg_.eps; nx.d_norm = d;
+  if (qkv_deferred) {
+    for (const MatSeg& s : L.qkv) {
+      GemvParams e = nx;
+      e.gamma = L.attn_norm;
+      e.ssq = &s == &L.qkv[0] ? ssq_ : nullptr;   // the sums of squares once per row
+      gemv(s.m, EPI_ATOMIC, nullptr, 0, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st, &e);
+    }
+  } else {
+    launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st, L.qkv_bias, qkv_n_);
+    for (const MatSeg& s : L.qkv)
+      gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
+  }
   if (decode && opt_.fused_attn) {
     DecodeAttnParams dp{};
     dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
@@ -613,6 +642,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
     dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
     dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
+    if (qkv_deferred) { dp.ssq = ssq_; dp.eps = cfg_.eps; dp.d_model = d; dp.bias = L.qkv_bias; }
     launch_attn_decode(dp, st);
   } else {
     RopeKvParams rp{};
@@ -651,26 +681,44 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       launch_attention(ap, st);
     }
   }
-  gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
+  if (small) {
+    GemvParams z{};
+    z.zero = ssq_; z.zero_n = 64 + (int64_t)M * qkv_n_;
+    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st, &z);
+  } else {
+    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
+    if (opt_.fused_norm && li + 1 == (int)layers_.size())
+      HIP_OK(hipMemsetAsync(ssq_, 0, (64 + (size_t)M * qkv_n_) * 4, st));
+  }
+  const bool ffn_fused = small && !L.moe;
   // MoE: the same launch clears the router logits, which the router GEMV then accumulates split-K
-  launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
+  if (!ffn_fused)
+    launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
   if (L.moe) {
     moe_ffn(L, M, st, x);
     return;
   }
+  GemvParams fx = nx;
+  fx.gamma = L.ffn_norm;
+  const GemvParams* fe = ffn_fused ? &fx : nullptr;
+  const f16* xin = ffn_fused ? nullptr : xn_;
   if (L.fused_gateup) {
-    gemv(L.gateup, EPI_SWIGLU, xn_, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st);
+    gemv(L.gateup, EPI_SWIGLU, xin, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st, fe);
   } else {
     const int F = cfg_.d_ff;
-    gemv(L.gate, EPI_STORE, xn_, Kd_, M, gu_, 2 * F, nullptr, 0, F, false, st);
-    gemv(L.up, EPI_STORE, xn_, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st);
+    gemv(L.gate, EPI_STORE, xin, Kd_, M, gu_, 2 * F, nullptr, 0, F, false, st, fe);
+    gemv(L.up, EPI_STORE, xin, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st, fe);
     launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
   }
   gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
 }
 
+bool HipStage::fuse_norm(int M) const { return opt_.fused_norm && M <= 4; }
+
 void HipStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st) {
   const int d = cfg_.d_model;
+  // (the LM head keeps the standalone norm: the deferred-norm GEMV variant needs ~50 more VGPRs,
+  // which halves the head's occupancy: 90.5 vs 72.7 + 4.6 us at 8B, profiles/r2h_prof_8b_mb1.txt)
   launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
   gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
   const bool pen = penalties_on() && hist_;
@@ -688,7 +736,7 @@ void HipStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t sa
     sp.seed = seed_ ^ (salt * 0x9E3779B97F4A7C15ULL); sp.step = step_; sp.tokens = tok_out;
     launch_sample(sp, st);
   } else {
-    launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st);
+    launch_argmax(logits_, logits_ld_, cfg_.vocab, M, tok_out, st, &am_);
   }
   if (pen) launch_hist_push(hist, hist_cnt_ + (size_t)mb * opt_.mb_size, hist_n_, tok_out, M, st);
 }
@@ -719,7 +767,7 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
     }
     launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, T, nullptr, 0, st);
     gemv(out_, EPI_STORE, xn_, Kd_, T, vlogits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
-    launch_argmax(vlogits_, logits_ld_, cfg_.vocab, T, vtok_ + (size_t)mb * opt_.prefill_chunk, st);
+    launch_argmax(vlogits_, logits_ld_, cfg_.vocab, T, vtok_ + (size_t)mb * opt_.prefill_chunk, st, &am_);
   } else if (spec_.last()) {
     int row = 0;
     for (const PrefillSeg& s : segs) {

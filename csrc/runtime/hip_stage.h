@@ -124,8 +124,10 @@ class HipStage : public Stage {
                      bool decode, hipStream_t st);
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
+  bool fuse_norm(int M) const;   // RMSNorm folded into the consuming GEMVs at this row count
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
-            int n_valid, bool allow_split, hipStream_t st);
+            int n_valid, bool allow_split, hipStream_t st,
+            const GemvParams* extras = nullptr);
   void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
   void ensure_hist();
   PackedMat upload_packed(int ggml_type, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row);
@@ -154,9 +156,11 @@ class HipStage : public Stage {
   int act_rows_ = 0, scratch_rows_ = 0;
 
   // scratch (shared by micro-batches: compute is serial on the stage's stream)
+  float* ssq_ = nullptr;   // [64] deferred-norm sums of squares, immediately followed by qkv_
   f16* xn_ = nullptr; float* qkv_ = nullptr; f16* q_ = nullptr; f16* attn_ = nullptr; f16* h_ = nullptr;
   float* gu_ = nullptr;   // unfused gate|up f32
   float* logits_ = nullptr; int logits_ld_ = 0;
+  ArgmaxScratch am_{nullptr, nullptr, 0};   // two-level argmax partials / arrival counters
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
   int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
   // MoE scratch

@@ -22,6 +22,20 @@ struct GemvParams {
   int ldh;
   int ntiles, nsb, sb_per_split;
   int n_valid;           // valid output columns
+  // optional fusions (gemv2.hip):
+  // deferred RMSNorm (M <= 4): X unused; the GEMV runs on f16(Xf * gamma) and accumulates
+  // sum(Xf^2) per row while staging.  STORE / SWIGLU (split-free): outputs scaled by
+  // rsqrt(mean(Xf^2) + eps).  ATOMIC: outputs left unscaled, the per-split partial sums of squares
+  // are atomically added to ssq[m] for the consumer to apply (the fused decode attention).
+  const float* Xf = nullptr;
+  int ldxf = 0;
+  const float* gamma = nullptr;
+  float eps = 0.f;
+  int d_norm = 0;                // row length of the norm (d_model; multiple of 8)
+  float* ssq = nullptr;          // ATOMIC + Xf: [M] sum of squares accumulator (zeroed by the caller)
+  const float* bias = nullptr;   // [n] added once (split 0) to STORE / ATOMIC outputs
+  float* zero = nullptr;         // side job after the GEMV: zero_n floats cleared
+  int64_t zero_n = 0;
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
@@ -110,11 +124,22 @@ struct DecodeAttnParams {
   float* o_part; float* ml_part;   // [n_split][M*Hq][Dp], [n_split][M*Hq][2]
   int32_t* counters;               // [M*Hkv] zero-initialised, self-resetting
   f16* out; int ldo;
+  // deferred RMSNorm of the qkv GEMV (nullptr: qkv already final): q|k|v = rsqrt(ssq[t] / d + eps)
+  // * qkv + bias (bias optional, [q|k|v])
+  const float* ssq = nullptr; float eps = 0.f; int d_model = 0; const float* bias = nullptr;
 };
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
 
-// greedy sampling: tokens[m] = argmax logits[m][:n]
-void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st);
+// greedy sampling: tokens[m] = argmax logits[m][:n] (lowest index on ties).  With scratch: a
+// two-level grid of (chunk, row) workgroups and a last-arriver reduce; without: one workgroup/row.
+constexpr int kArgmaxChunks = 64;
+struct ArgmaxScratch {
+  float* part;          // [rows][kArgmaxChunks][2]
+  int32_t* counters;    // [rows], zero-initialised, self-resetting
+  int rows;
+};
+void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, hipStream_t st,
+                   const ArgmaxScratch* scratch = nullptr);
 // temperature / top-k / top-p / min-p sampling with a counter-based RNG
 struct SampleParams {
   const float* logits; int ld; int n; int M;

@@ -25,6 +25,8 @@ struct StageOptions {
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
+  bool fused_norm = false;  // M <= 4 rows: deferred RMSNorm folded into the qkv / gate-up GEMVs (gemv2.hip);
+                            // off by default: 8B mb1 470.7 vs 473.7 tok/s, 70B mb1 92.5 vs 104.8 (r2i)
 };
 
 struct PrefillSeg {

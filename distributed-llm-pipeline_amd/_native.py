@@ -52,7 +52,10 @@ _SIGS = {
                        c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
     "mp_op_attention": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
-    "mp_op_argmax": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p], c_int),
+    "mp_op_argmax": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mp_op_gemv_fused": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                          c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_float, c_int, c_void_p, c_void_p,
+                          c_void_p, c_int64, c_void_p], c_int),
     "mp_op_penalize": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float, c_void_p], c_int),
     "mp_op_hist_push": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_sample": ([c_void_p, c_int, c_int, c_int, c_float, c_int, c_float, c_float, ctypes.c_uint64, c_void_p,

@@ -115,11 +115,52 @@ def embed(raw_table: torch.Tensor, ggml_type: int, d: int, tokens: torch.Tensor)
     return x
 
 
-def argmax(logits: torch.Tensor) -> torch.Tensor:
+ARGMAX_CHUNKS = 64
+
+
+def argmax(logits: torch.Tensor, two_level: bool = True) -> torch.Tensor:
+    """Greedy token per row (lowest index on ties).  two_level: (chunk, row) grid + last-arriver
+    reduce (the engine's path); otherwise one workgroup per row."""
     M, n = logits.shape
     out = torch.empty(M, dtype=torch.int32, device=logits.device)
-    N.check(N.lib().mp_op_argmax(_ptr(logits), logits.stride(0), n, M, _ptr(out), _stream()), "argmax")
+    part = cnt = None
+    if two_level:
+        part = torch.empty(M, ARGMAX_CHUNKS, 2, dtype=torch.float32, device=logits.device)
+        cnt = torch.zeros(M, dtype=torch.int32, device=logits.device)
+    N.check(N.lib().mp_op_argmax(_ptr(logits), logits.stride(0), n, M, _ptr(out), _ptr(part), _ptr(cnt),
+                                 _stream()), "argmax")
+    if cnt is not None:
+        assert int(cnt.abs().sum()) == 0, "argmax arrival counters did not reset"
     return out
+
+
+def gemv_fused(w: PackedWeight, epi: int = EPI_STORE, *, x: torch.Tensor | None = None,
+               xf: torch.Tensor | None = None, gamma: torch.Tensor | None = None, eps: float = 1e-5,
+               bias: torch.Tensor | None = None, y: torch.Tensor | None = None, nsplit: int = 1,
+               zero: torch.Tensor | None = None, ssq: torch.Tensor | None = None) -> torch.Tensor:
+    """Decode GEMV (gemv2.hip) with the fusions the engine uses at single-stream decode.
+    xf/gamma: deferred RMSNorm of the f32 rows xf (M <= 4, x unused) -- the GEMV runs on
+    f16(xf * gamma); STORE/SWIGLU outputs are scaled by rsqrt(mean(xf^2) + eps), ATOMIC outputs are
+    left unscaled and sum(xf^2) per row is added into `ssq` (f32 [M]).  bias: added once per output.
+    zero: f32 tensor cleared after the GEMV."""
+    if xf is not None:
+        assert xf.dtype == torch.float32 and xf.is_contiguous()
+        M, d = xf.shape
+    else:
+        assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
+        M, d = x.shape[0], 0
+    F = w.n // 2
+    if epi == EPI_SWIGLU:
+        h = torch.zeros(M, F, dtype=torch.float16, device=w.dev.device) if y is None else y
+        Y, ldy, H, ldh, nv = None, 0, h, h.stride(0), F
+    else:
+        y = torch.zeros(M, w.n, dtype=torch.float32, device=w.dev.device) if y is None else y
+        Y, ldy, H, ldh, nv = y, y.stride(0), None, 0, w.n
+    N.check(N.lib().mp_op_gemv_fused(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad if x is not None else 0,
+                                     M, _ptr(Y), ldy, _ptr(H), ldh, nv, nsplit, _ptr(xf), d, _ptr(gamma), eps, d,
+                                     _ptr(ssq), _ptr(bias), _ptr(zero), 0 if zero is None else zero.numel(), _stream()),
+            "gemv_fused")
+    return H if epi == EPI_SWIGLU else Y
 
 
 def sample(logits: torch.Tensor, temp: float, top_k: int = 0, top_p: float = 1.0, min_p: float = 0.0,

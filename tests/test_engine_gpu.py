@@ -44,6 +44,40 @@ def test_engine_matches_reference(cuda, native, model_dir, name, ftype):
             assert nmse(lg, rl) < 2e-4, (step, nmse(lg, rl))
 
 
+@pytest.mark.parametrize("name,ftype", [("tiny-gqa", "Q4_K_M"), ("tiny-qwen2", "Q8_0"), ("tiny-moe", "Q8_0")])
+def test_fused_norm_matches_reference(cuda, native, model_dir, name, ftype):
+    """fused_norm=true (deferred RMSNorm in the qkv / gate-up GEMVs, applied by the decode attention
+    incl. the Qwen2 q|k|v bias) against the fp32 oracle, single stream and mb 3 (prefill chunks of
+    <= 4 tokens take the fused gate/up too)."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, name, ftype)
+    ref = RefLlama.from_gguf(path)
+    prompt = [int(t) for t in np.random.default_rng(1).integers(3, cfg.vocab, 23)]
+    with Engine(gguf=path, max_ctx=256, prefill_chunk=4, graphs=True, fused_norm=True) as eng:
+        eng.start([prompt])
+        ref.reset()
+        rl = ref.forward(prompt, 0)[-1].numpy()
+        assert nmse(eng.logits()[0], rl) < 2e-4
+        pos = len(prompt)
+        for step in range(5):
+            tok = eng.tokens()[0][-1]
+            eng.decode(1)
+            rl = ref.forward([tok], pos)[-1].numpy()
+            pos += 1
+            assert nmse(eng.logits()[0], rl) < 2e-4, (step, nmse(eng.logits()[0], rl))
+    prompts = [[5, 6, 7, 8, 9], [100, 200, 300], [7] * 11]
+    with Engine(gguf=path, max_ctx=256, n_mb=1, mb_size=3, prefill_chunk=4, fused_norm=True) as eng:
+        eng.start(prompts)
+        eng.decode(2)
+        lg, toks = eng.logits(rows=3), eng.tokens()
+    for i, pr in enumerate(prompts):
+        ref.reset()
+        seq = pr + toks[i][:2]
+        rl = ref.forward(seq, 0)[-1].numpy()
+        assert nmse(lg[i], rl) < 2e-4, (i, nmse(lg[i], rl))
+
+
 def test_graph_equals_eager(cuda, native, model_dir):
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
