@@ -123,6 +123,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_TOK_S, 2) if args.model == "llama3-70b" else None,
+            # like-for-like with the reference's single-stream figure: the rate EACH sequence sees
+            "per_stream_tok_s": round(1e3 / (ms / args.steps), 2),
+            "vs_baseline_per_stream": round(1e3 / (ms / args.steps) / BASELINE_TOK_S, 2) if args.model == "llama3-70b" else None,
             "dtype": "bf16-class: f16 MFMA on dequantized " + args.ftype + " weights, f32 accumulate",
             "data": "synthetic prompts, random-init weights (GGUF " + args.ftype + " blocks generated in HBM)",
             "config": {"model": f"{m['name']} {args.ftype}", "global_batch": n_mb * args.mb_size * replicas,

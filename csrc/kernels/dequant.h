@@ -77,11 +77,9 @@ __device__ __forceinline__ Consts make_consts() {
   asm("v_mov_b32 %0, 0x54005400" : "=v"(c.mag_lo));   // 64 + q   (q at mantissa bits 4..7)
   return c;
 }
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) {
-  uint32_t d;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(m), "v"(c));
-  return d;
-}
+// plain C (the compiler emits v_and_or_b32 with the VGPR-resident masks and sees its hazards:
+// the inline-asm form cost an s_nop after most of them and re-materialised the masks per call)
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t c) { return (a & m) | c; }
 
 // Q4_K / Q5_K super-block header as packed (csrc/runtime/pack.cpp): dword 0 = (d, dmin) f16, then
 // 12 bytes holding, for each lane group g, the 24-bit word
@@ -112,12 +110,13 @@ template <> struct Deq<P_Q4_K> {
     r.hdr = c.q16(2048 + (lane & 15) * 16);
   }
   template <int H>
-  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) { dequant<H>(r, b, lane, make_consts()); }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts& k) {
     half2_t S2, M2;
     kquarter_scales(r.hdr, lane, S2, M2);   // shared by H = 0 / 1 (CSE)
     const half2_t S = H ? h2hi(S2) : h2lo(S2), M = H ? h2hi(M2) : h2lo(M2);
     const u32x4 q = H == 0 ? r.q0 : r.q1;
-    const Consts k = make_consts();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const uint32_t w = q[s], t = w >> 8;
@@ -143,13 +142,14 @@ template <> struct Deq<P_Q5_K> {
     r.hdr = c.q16(2560 + (lane & 15) * 16);
   }
   template <int H>
-  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) { dequant<H>(r, b, lane, make_consts()); }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts& k) {
     half2_t S2, M2;
     kquarter_scales(r.hdr, lane, S2, M2);
     const half2_t S = H ? h2hi(S2) : h2lo(S2), M = H ? h2hi(M2) : h2lo(M2);
     const u32x4 q = H == 0 ? r.q0 : r.q1;
     const uint32_t qh = H == 0 ? r.qh0 : r.qh1;
-    const Consts k = make_consts();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const uint32_t w = q[s], t = w >> 8;
@@ -182,7 +182,9 @@ template <> struct Deq<P_Q6_K> {
     r.d = c.q2(3328 + (lane & 15) * 2);
   }
   template <int H>
-  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) { dequant<H>(r, b, lane, make_consts()); }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts& k) {
     const f16 dh = __builtin_bit_cast(f16, (uint16_t)r.d);
     // sub-block of MFMA (H, s) = 4g + 2H + (s >> 1): bytes 2H, 2H+1 of r.sc; int8 -> f16 by the
     // exponent magic on (byte ^ 0x80) = sc + 128, minus 1152 (exact), times d (one rounding)
@@ -191,7 +193,6 @@ template <> struct Deq<P_Q6_K> {
                        half2_t{dh, dh};
     const u32x4 q = H == 0 ? r.q0 : r.q1;
     const u32x2 qh = H == 0 ? r.qh0 : r.qh1;
-    const Consts k = make_consts();
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const half2_t S = (s >> 1) ? h2hi(S2) : h2lo(S2);
@@ -222,6 +223,8 @@ template <> struct Deq<P_Q8_0> {
     r.dd = c.q4(4096 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
   }
   template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts&) { dequant<H>(r, b, lane); }
+  template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
     const half2_t off = h2c(1152.f);   // 1024 magic + 128 (bytes stored q+128)
     const half2_t S = H ? h2hi(as_h2(r.dd)) : h2lo(as_h2(r.dd));   // block 2g + H
@@ -251,9 +254,10 @@ template <> struct Deq<P_Q4_0> {
     r.dd = c.q4(2048 + (lane & 15) * 16 + 4 * (lane >> 4));   // d(2g), d(2g+1)
   }
   template <int H>
-  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) { dequant<H>(r, b, lane, make_consts()); }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts& k) {
     const u32x4 q = H == 0 ? r.q0 : r.q1;
-    const Consts k = make_consts();
     const half2_t S = H ? h2hi(as_h2(r.dd)) : h2lo(as_h2(r.dd));   // block 2g + H
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -276,6 +280,8 @@ template <> struct Deq<P_F16> {
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = c.q16nt(i * 1024 + lane * 16);
   }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts&) { dequant<H>(r, b, lane); }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
 #pragma unroll

@@ -202,9 +202,12 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* logits, int l
 // Two-level argmax: grid (nchunk, M) workgroups each reduce one chunk of a row, publish a
 // (value, index) partial and count in; the last arriver of the row reduces the nchunk partials.
 // (One 1024-thread workgroup per row read 513 KB of Llama-3 logits in 38 us at M = 1.)
-// Hand-off per MI355X_MICROARCH.md 'Valid forms': plain partial store by one lane -> agent release
-// fence -> asm vmcnt(0) -> relaxed agent counter add; the last arriver (told by the value its add
-// returned) -> agent acquire fence -> vmcnt(0) -> barrier -> plain loads.  Ties -> lowest index.
+// Hand-off per MI355X_MICROARCH.md 'Valid forms', first row of the sc1 table: the partial is ONE
+// 8-byte sc1 (agent-scope relaxed) store by the lane that then drains it (vmcnt(0)) and adds to the
+// row's counter; the last arriver (told by the value its add returned) reads every partial with
+// sc1 loads from the same wave.  (An agent release fence per workgroup wrote back the XCD L2 behind
+// every arrival: 66 us at M = 64 with the LM head's 33 MB of fresh logits dirty in L2.)
+// Ties -> lowest index.
 __device__ __forceinline__ bool am_better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
 
 __global__ __launch_bounds__(256) void argmax2_kernel(const float* logits, int ld, int n, int chunk,
@@ -241,23 +244,23 @@ __global__ __launch_bounds__(256) void argmax2_kernel(const float* logits, int l
   if (threadIdx.x == 0) {
     for (int k = 1; k < 4; ++k)
       if (am_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
-    part[(size_t)m * nchunk + c] = make_float2(bv, __int_as_float(bi));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint64_t pk = (uint64_t)__float_as_uint(bv) | ((uint64_t)(uint32_t)bi << 32);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + (size_t)m * nchunk + c, pk, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(counters + m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == nchunk - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!last || threadIdx.x >= 64) return;
   bv = -INFINITY;
   bi = 0x7fffffff;
   for (int k = threadIdx.x; k < nchunk; k += 64) {
-    const float2 pv = part[(size_t)m * nchunk + k];
-    if (am_better(pv.x, __float_as_int(pv.y), bv, bi)) { bv = pv.x; bi = __float_as_int(pv.y); }
+    const uint64_t pk = __hip_atomic_load(reinterpret_cast<uint64_t*>(part) + (size_t)m * nchunk + k, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const float v = __uint_as_float((uint32_t)pk);
+    const int i = (int)(uint32_t)(pk >> 32);
+    if (am_better(v, i, bv, bi)) { bv = v; bi = i; }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -269,6 +272,25 @@ __global__ __launch_bounds__(256) void argmax2_kernel(const float* logits, int l
     tok[m] = bi == 0x7fffffff ? 0 : bi;
     __hip_atomic_store(counters + m, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// deterministic reductions: a fixed summation order per element, no atomics
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t ss, int ldp,
+                                                            int n, float* __restrict__ Y, int ldy) {
+  const int m = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  float acc = Y[(size_t)m * ldy + j];
+  for (int s = 0; s < nsplit; ++s) acc += part[(size_t)s * ss + (size_t)m * ldp + j];
+  Y[(size_t)m * ldy + j] = acc;
+}
+
+__global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ ys, int lds, int k, int n,
+                                                          float* __restrict__ Y, int ldy) {
+  const int t = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  float acc = Y[(size_t)t * ldy + j];
+  for (int e = 0; e < k; ++e) acc += ys[((size_t)t * k + e) * lds + j];
+  Y[(size_t)t * ldy + j] = acc;
 }
 
 __global__ void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
@@ -362,6 +384,16 @@ void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, h
   nchunk = (n + chunk - 1) / chunk;
   hipLaunchKernelGGL(mpk::argmax2_kernel, dim3(nchunk, M), dim3(256), 0, st, logits, ld, n, chunk,
                      reinterpret_cast<float2*>(sc->part), sc->counters, tokens);
+}
+
+void launch_splitk_reduce(const float* part, int nsplit, int64_t split_stride, int ldp, int M, int n, float* Y, int ldy,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(mpk::splitk_reduce_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, part, nsplit, split_stride,
+                     ldp, n, Y, ldy);
+}
+
+void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, float* Y, int ldy, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::moe_combine_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, Yslot, ld_slot, k, n, Y, ldy);
 }
 
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {

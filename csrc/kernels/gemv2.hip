@@ -137,12 +137,13 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   const f16* xrow0 = &xs[0][r * G2_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
   const f16* xrow1 = &xs[1][r * G2_LDX + (t16_xoff(g, 0) ^ x_qswap(r))];
   // one super-block; all loads unconditional (clamped to the range): path-independent vmcnt
+  const Consts kc = make_consts();   // nibble masks / exponent magics, once per kernel
   auto step = [&](const int sl, const int cur) {
     const int buf = (cur - sbA) & 1;
     const f16* xr = buf ? xrow1 : xrow0;
     half8_t b[TW][4];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) D::template dequant<0>(ring[sl][t], b[t], lane);
+    for (int t = 0; t < TW; ++t) D::template dequant<0>(ring[sl][t], b[t], lane, kc);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
         for (int t = 0; t < TW; ++t) acc[t][mt] = mfma16x16x32(a, b[t][s], acc[t][mt]);
       }
 #pragma unroll
-    for (int t = 0; t < TW; ++t) D::template dequant<1>(ring[sl][t], b[t], lane);
+    for (int t = 0; t < TW; ++t) D::template dequant<1>(ring[sl][t], b[t], lane, kc);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           for (int i = 0; i < 4; ++i) {
             const int m = 16 * mt + 4 * g + i;
             if (m < M) {
-              float* dst = p.Y + (size_t)m * p.ldy + n;
+              float* dst = p.Y + (size_t)blockIdx.y * p.split_stride + (size_t)m * p.ldy + n;
               if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[t][mt][i] + bias);
               else *dst = acc[t][mt][i] + bias;
             }

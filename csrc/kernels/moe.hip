@@ -103,7 +103,10 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
       } else if (m < rows) {
         const int n = tile * 16 + r;
         const int slot = list[r0 + m];
-        if (n < p.n_valid) unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[i]);
+        if (n < p.n_valid) {
+          if (p.Yslot) p.Yslot[(size_t)slot * p.ldy + n] = p.weights[slot] * acc[i];   // deterministic mode
+          else unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[i]);
+        }
       }
     }
   }
@@ -222,7 +225,8 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
         const int n = tile * 16 + r;
         if (m < rows && n < p.n_valid) {
           const int slot = list[m];
-          unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[mt][i]);
+          if (p.Yslot) p.Yslot[(size_t)slot * p.ldy + n] = p.weights[slot] * acc[mt][i];   // deterministic mode
+          else unsafeAtomicAdd(p.Y + (size_t)(slot / p.k) * p.ldy + n, p.weights[slot] * acc[mt][i]);
         }
       }
     }
@@ -269,7 +273,7 @@ static void moe_launch_pt(int epi, const MoeGemvParams& p, int nsplit, hipStream
 }
 
 void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st) {
-  if (nsplit < 1 || epi == EPI_SWIGLU) nsplit = 1;
+  if (nsplit < 1 || epi == EPI_SWIGLU || p.Yslot) nsplit = 1;
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
   switch (ptype) {

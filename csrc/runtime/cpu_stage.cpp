@@ -208,7 +208,11 @@ void CpuStage::alloc_runtime() {
   const int B = opt_.mb_size, NM = opt_.n_mb, d = cfg_.d_model;
   const int rows = std::max(B, opt_.prefill_chunk);
   const int n_slots = NM * B;
-  const size_t per = (size_t)n_slots * opt_.max_ctx * cfg_.kv_dim();
+  // paged KV (kvpager.h): kv_pages pages of [64][kv_dim] f32 + the TRASH page, per layer
+  max_pages_ = opt_.max_ctx / 64;
+  n_pages_ = opt_.kv_pages > 0 ? opt_.kv_pages : n_slots * max_pages_;
+  bt_.assign((size_t)n_slots * max_pages_, n_pages_);
+  const size_t per = (size_t)(n_pages_ + 1) * 64 * cfg_.kv_dim();
   for (size_t i = 0; i < layers_.size(); ++i) {
     kc_.emplace_back(per, 0.f);
     vc_.emplace_back(per, 0.f);
@@ -228,9 +232,9 @@ void CpuStage::alloc_runtime() {
   att_.resize((size_t)rows * cfg_.q_dim());
   h_.resize((size_t)rows * cfg_.d_ff);
   gu_.resize((size_t)rows * 2 * cfg_.d_ff);
-  MP_LOGI("stage %d: layers %d-%d on CPU (%d threads), weights %.2f GiB, KV %.2f GiB (%d slots x %d ctx)",
-          spec_.stage, spec_.layer_begin, spec_.layer_end - 1, pool_->size(), weight_bytes_ / 1073741824.0,
-          kv_bytes_ / 1073741824.0, n_slots, opt_.max_ctx);
+  MP_LOGI("stage %d: layers %d-%d on CPU (%d threads), weights %.2f GiB, KV %.2f GiB (%d pages of 64 tokens; "
+          "%d slots x <= %d ctx)", spec_.stage, spec_.layer_begin, spec_.layer_end - 1, pool_->size(),
+          weight_bytes_ / 1073741824.0, kv_bytes_ / 1073741824.0, n_pages_, n_slots, opt_.max_ctx);
 }
 
 void CpuStage::set_positions(int mb, const std::vector<int32_t>& pos) {
@@ -302,7 +306,7 @@ void CpuStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
         *e1 = x0 * s + x1 * c;
       }
     }
-    const size_t kv_off = ((size_t)slot[m] * ctx + p) * kvd;
+    const size_t kv_off = kv_row(slot[m], p) * kvd;
     std::memcpy(&kc_[li][kv_off], row + qd, (size_t)kvd * 4);
     std::memcpy(&vc_[li][kv_off], row + qd + kvd, (size_t)kvd * 4);
   }
@@ -314,11 +318,11 @@ void CpuStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       const int m = (int)(i / Hq), h = (int)(i % Hq), kh = h / G;
       const float* q = qkv_.data() + (size_t)m * ldq + (size_t)h * hd;
       const int n = pos[m] + 1;
-      const float* kb = &kc_[li][(size_t)slot[m] * ctx * kvd + (size_t)kh * hd];
-      const float* vb = &vc_[li][(size_t)slot[m] * ctx * kvd + (size_t)kh * hd];
+      const float* kb = &kc_[li][(size_t)kh * hd];
+      const float* vb = &vc_[li][(size_t)kh * hd];
       float mx = -INFINITY;
       for (int t = 0; t < n; ++t) {
-        const float* k = kb + (size_t)t * kvd;
+        const float* k = kb + kv_row(slot[m], t) * kvd;
         float s = 0;
         for (int j = 0; j < hd; ++j) s += q[j] * k[j];
         sc[t] = s * scale;
@@ -330,7 +334,7 @@ void CpuStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       std::fill(o, o + hd, 0.f);
       for (int t = 0; t < n; ++t) {
         const float p = sc[t] / sum;
-        const float* v = vb + (size_t)t * kvd;
+        const float* v = vb + kv_row(slot[m], t) * kvd;
         for (int j = 0; j < hd; ++j) o[j] += p * v[j];
       }
     }
@@ -414,30 +418,44 @@ int CpuStage::sample_row(const float* lg, uint64_t salt, int row) {
   return v[keep - 1].second;
 }
 
-// KV of one slot: per layer, K rows then V rows [n_tok][kv_dim] f32 (contiguous in kc_/vc_)
+// KV of one slot: per layer, K rows then V rows [n_tok][kv_dim] f32 (gathered through the slot's
+// block-table row)
 size_t CpuStage::kv_state_bytes(int n_tok) const {
   return kc_.size() * 2 * (size_t)n_tok * cfg_.kv_dim() * 4;
 }
 
+size_t CpuStage::kv_row(int slot, int pos) const {
+  return (size_t)bt_[(size_t)slot * max_pages_ + pos / 64] * 64 + pos % 64;
+}
+
+void CpuStage::set_block_table(const std::vector<int32_t>& t) {
+  if (t.size() != bt_.size()) throw std::runtime_error("set_block_table: size mismatch");
+  for (int32_t e : t)
+    if (e < 0 || e > n_pages_) throw std::runtime_error("set_block_table: page id out of range");
+  bt_ = t;
+}
+
 void CpuStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
-  const size_t row = (size_t)cfg_.kv_dim(), n = (size_t)n_tok * row * 4;
-  const size_t off = (size_t)slot * opt_.max_ctx * row;
+  const size_t row = (size_t)cfg_.kv_dim();
   for (size_t li = 0; li < kc_.size(); ++li)
-    for (const auto* c : {&kc_[li], &vc_[li]}) {
-      const uint8_t* p = reinterpret_cast<const uint8_t*>(c->data() + off);
-      out.insert(out.end(), p, p + n);
-    }
+    for (const auto* c : {&kc_[li], &vc_[li]})
+      for (int t = 0; t < n_tok; ++t) {
+        if (bt_[(size_t)slot * max_pages_ + t / 64] >= n_pages_) throw std::runtime_error("kv_export: unmapped page");
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(c->data() + kv_row(slot, t) * row);
+        out.insert(out.end(), p, p + row * 4);
+      }
 }
 
 void CpuStage::kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) {
   if (bytes != kv_state_bytes(n_tok)) throw std::runtime_error("kv_import: size mismatch");
-  const size_t row = (size_t)cfg_.kv_dim(), n = (size_t)n_tok * row * 4;
-  const size_t off = (size_t)slot * opt_.max_ctx * row;
+  const size_t row = (size_t)cfg_.kv_dim();
   for (size_t li = 0; li < kc_.size(); ++li)
-    for (auto* c : {&kc_[li], &vc_[li]}) {
-      std::memcpy(c->data() + off, data, n);
-      data += n;
-    }
+    for (auto* c : {&kc_[li], &vc_[li]})
+      for (int t = 0; t < n_tok; ++t) {
+        if (bt_[(size_t)slot * max_pages_ + t / 64] >= n_pages_) throw std::runtime_error("kv_import: unmapped page");
+        std::memcpy(c->data() + kv_row(slot, t) * row, data, row * 4);
+        data += row * 4;
+      }
 }
 
 void CpuStage::set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) {

@@ -66,6 +66,7 @@ class CpuStage : public Stage {
   void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt);
   void set_history(int mb, const std::vector<std::vector<int32_t>>& seqs) override;
   void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) override;
+  void set_block_table(const std::vector<int32_t>& table) override;
   void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) override;
   size_t kv_state_bytes(int n_tok) const override;
   uint64_t sample_step() override { return step_; }
@@ -85,7 +86,10 @@ class CpuStage : public Stage {
   std::vector<float> out_norm_;
   std::vector<float> inv_freq_;
   // KV: [layer][slot][ctx][kv_dim]
-  std::vector<std::vector<float>> kc_, vc_;
+  std::vector<std::vector<float>> kc_, vc_;   // per layer: (kv_pages + 1) pages of [64][kv_dim]
+  std::vector<int32_t> bt_;                    // block table [n_slots][max_pages] (kvpager.h)
+  int max_pages_ = 0, n_pages_ = 0;
+  size_t kv_row(int slot, int pos) const;      // page row of (slot, position)
   // per micro-batch
   std::vector<std::vector<float>> act_;
   std::vector<std::vector<int32_t>> tok_, pos_;

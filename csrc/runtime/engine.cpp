@@ -180,15 +180,23 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       const double reserve =
           dev_n[e.first] * (4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4);
       const double budget = frac * cap_bytes - e.second - reserve;
-      const long c = budget > 0 ? (long)(budget / (pt * M_ * B_)) : 0;
+      // paged KV: the pool holds the LIVE tokens of all slots (not n_slots x max_ctx)
+      const long c = budget > 0 ? (long)(budget / pt) : 0;
       if (c < ctx) { ctx = c; per_tok = pt; lmax = layers; }
     }
-    const long train = cfg_.n_ctx_train > 0 ? cfg_.n_ctx_train : 131072;
-    ctx = std::min(ctx, std::min(train, (long)j.get_int("max_ctx_cap", 1 << 20)));
     if (ctx < 64) throw std::runtime_error("max_ctx auto: no HBM left for the KV cache");
-    max_ctx_ = (int)(ctx / 64 * 64);
-    MP_LOGI("max_ctx auto: %d tokens per sequence (%d slots, %.1f GiB KV on the GPU holding %d layers; device %.0f GiB)",
-            max_ctx_, M_ * B_, per_tok * max_ctx_ * M_ * B_ / 1073741824.0, lmax, cap_bytes / 1073741824.0);
+    kv_pages_ = (int)std::min<long>(ctx / 64, std::numeric_limits<int>::max() / 64);
+    const long train = cfg_.n_ctx_train > 0 ? cfg_.n_ctx_train : 131072;
+    const long per_seq = std::min((long)kv_pages_ * 64, std::min(train, (long)j.get_int("max_ctx_cap", 1 << 20)));
+    max_ctx_ = (int)(per_seq / 64 * 64);
+    MP_LOGI("max_ctx auto: KV pool of %d pages (%ld tokens, %.1f GiB on the GPU holding %d layers; device %.0f GiB) "
+            "shared by %d slots, up to %d tokens per sequence",
+            kv_pages_, (long)kv_pages_ * 64, per_tok * kv_pages_ * 64 / 1073741824.0, lmax, cap_bytes / 1073741824.0,
+            M_ * B_, max_ctx_);
+  } else {
+    // explicit pool (kv_pool_tokens; e.g. oversubscribed slots), else every slot can hold max_ctx
+    const long pool = j.get_int("kv_pool_tokens", 0);
+    kv_pages_ = pool > 0 ? (int)((pool + 63) / 64) : M_ * B_ * (max_ctx_ / 64);
   }
   for (auto& sp : specs_)
     MP_LOGI("partition: stage %d <- layers [%d, %d) (%d layers)%s%s", sp.stage, sp.layer_begin, sp.layer_end,
@@ -207,7 +215,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       if (sp.first()) w += embd_b;
       if (sp.last()) w += head_cost;
       const double kv = (double)(sp.layer_end - sp.layer_begin) * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() *
-                        (cpu_ ? 4.0 : 2.0) * max_ctx_ * M_ * B_;
+                        (cpu_ ? 4.0 : 2.0) * ((double)kv_pages_ + 1) * 64;
       auto& e = need[devices[sp.stage]];
       e.first += w;
       e.second += kv;
@@ -250,13 +258,15 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.n_mb = M_;
   so.mb_size = B_;
   so.max_ctx = max_ctx_;
+  so.kv_pages = kv_pages_;
   so.prefill_chunk = chunk_;
   so.use_graphs = j.get_bool("graphs", true);
   so.attn_split_len = j.get_int("attn_split_len", 0);   // 0 = auto
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
-  so.fused_norm = j.get_bool("fused_norm", false);
+  so.deterministic = j.get_bool("deterministic", false);
+  so.fused_norm = j.get_bool("fused_norm", false) && !so.deterministic;   // its sums of squares are atomics
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);
 
@@ -326,6 +336,8 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       MP_LOGI("stage boundary: %s activations, %.1f KiB per token", act_dtype_ == ACT_F32 ? "f32" : act_dtype_ == ACT_F16 ? "f16" : "bf16",
               cfg_.d_model * (act_dtype_ == ACT_F32 ? 4 : 2) / 1024.0);
   }
+  pager_.init(M_ * B_, max_ctx_ / 64, kv_pages_);
+  kv_sync();
   rounds_cap_ = max_ctx_ + 2;
   if (cpu_) {
     out_vec_.resize((size_t)rounds_cap_ * M_ * B_);
@@ -813,6 +825,12 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   base_round_.assign((size_t)M_ * B_, 0);
   active_.assign((size_t)M_ * B_, 0);
   for (size_t i = 0; i < prompts.size(); ++i) active_[i] = 1;
+  // KV pages: each prompt + its first decode position; slots without a prompt give theirs back
+  // (a reused prefix keeps the pages it already owns)
+  for (size_t i = prompts.size(); i < (size_t)M_ * B_; ++i) pager_.release((int)i);
+  for (size_t i = 0; i < prompts.size(); ++i)
+    if (!prompts[i].empty() && (int)prompts[i].size() < max_ctx_) kv_grant(i, (int)prompts[i].size() + 1);
+  kv_sync();
   std::vector<Item> items;
   for (auto& w : workers_) {
     Stage& st = *w->stage;
@@ -1003,6 +1021,11 @@ Json Engine::load_state(const std::string& dir) {
       throw std::runtime_error("load_state: bad session (base_round)");
     if (active_[i] && slot_pos(i) >= max_ctx_) throw std::runtime_error("load_state: sequence longer than max_ctx");
   }
+  // KV pages for the restored sequences (their KV bytes are imported page by page below)
+  for (int i = 0; i < M_ * B_; ++i) pager_.release(i);
+  for (size_t i = 0; i < prompts_.size(); ++i)
+    if (active_[i]) kv_grant(i, slot_pos(i) + 1);
+  kv_sync();
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
     if (!cpu_) HIP_OK(hipSetDevice(wp->device));
@@ -1140,6 +1163,24 @@ void Engine::push_positions(int mb) {
 
 void Engine::release(int slot) {
   if (slot >= 0 && slot < (int)active_.size()) active_[slot] = 0;
+  if (slot >= 0 && slot < M_ * B_) pager_.release(slot);   // table pushed before the next engine call
+}
+
+void Engine::kv_grant(size_t slot, int n_tokens) {
+  if (pager_.ensure((int)slot, n_tokens)) return;
+  throw std::runtime_error("KV page pool exhausted: slot " + std::to_string(slot) + " needs " +
+                           std::to_string((n_tokens + 63) / 64) + " pages, owns " +
+                           std::to_string(pager_.owned((int)slot)) + ", " + std::to_string(pager_.free_pages()) +
+                           " of " + std::to_string(pager_.n_pages()) + " free (kv_pool_tokens / max_ctx auto)");
+}
+
+void Engine::kv_sync() {
+  if (!pager_.dirty()) return;
+  for (auto& w : workers_) {
+    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    w->stage->set_block_table(pager_.table());
+  }
+  pager_.clean();
 }
 
 void Engine::admit(const std::vector<int>& slots, const std::vector<std::vector<int32_t>>& prompts) {
@@ -1157,6 +1198,7 @@ void Engine::admit(const std::vector<int>& slots, const std::vector<std::vector<
     if (i < 0 || (size_t)i >= NS) throw std::runtime_error("admit: bad slot");
     if (active_[i]) throw std::runtime_error("admit: slot " + std::to_string(i) + " is busy");
     if (prompts[k].empty() || (int)prompts[k].size() >= max_ctx_) throw std::runtime_error("bad prompt length");
+    kv_grant((size_t)i, (int)prompts[k].size() + 1);
     prompts_[i] = prompts[k];
     gen_[i].clear();
     base_round_[i] = rounds_done_;
@@ -1164,6 +1206,7 @@ void Engine::admit(const std::vector<int>& slots, const std::vector<std::vector<
     seqs.push_back((size_t)i);
     mbs[i / B_] = 1;
   }
+  kv_sync();
   for (auto& w : workers_) {
     Stage& st = *w->stage;
     if (!cpu_) HIP_OK(hipSetDevice(w->device));
@@ -1213,6 +1256,10 @@ StepStats Engine::decode_steps(int k) {
     base_round_[i] = rounds_done_;
     push_positions((int)(i / B_));
   }
+  // KV pages for the k positions every running sequence is about to write
+  for (size_t i = 0; i < (size_t)M_ * B_; ++i)
+    if (i < active_.size() && active_[i]) kv_grant(i, slot_pos(i) + k + 1);
+  kv_sync();
   for (auto& w : workers_)
     if (w->stage->spec().last() && cpu_) {
       w->tok_t.clear();
@@ -1353,6 +1400,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
         if ((int)d.size() > room) d.resize(std::max(0, room));
         chunk[i].push_back(ctx[i].back());
         chunk[i].insert(chunk[i].end(), d.begin(), d.end());
+        kv_grant(i, pos + (int)chunk[i].size());
         drafted += (long)d.size();
         if (cpu_) std::memcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4);
         else {
@@ -1368,6 +1416,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
       if (it.T > 0) items.push_back(it);
     }
     if (items.empty()) break;
+    kv_sync();
     run_all(items);
     ++rounds;
     for (const Item& it : items) {
@@ -1462,6 +1511,8 @@ Json Engine::info() const {
   j["n_mb"] = M_;
   j["mb_size"] = B_;
   j["max_ctx"] = max_ctx_;
+  j["kv_pages"] = kv_pages_;
+  j["kv_free_pages"] = pager_.free_pages();
   j["mode"] = mode_;
   j["backend"] = cpu_ ? "cpu" : "hip";
   j["load_ms"] = load_ms_;

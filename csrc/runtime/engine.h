@@ -25,6 +25,7 @@
 
 #include "hip_stage.h"
 #include "json.h"
+#include "kvpager.h"
 #include "model.h"
 #include "transport.h"
 
@@ -57,6 +58,8 @@ class Engine {
   int n_mb() const { return M_; }
   int mb_size() const { return B_; }
   int max_ctx() const { return max_ctx_; }
+  int kv_pages() const { return kv_pages_; }
+  int kv_free_pages() const { return pager_.free_pages(); }
   double load_ms() const { return load_ms_; }
   bool owns_last() const;
   bool owns_first() const;
@@ -174,6 +177,10 @@ class Engine {
   // per slot: the round at which its sequence was admitted, and whether one is running
   std::vector<int> base_round_;
   std::vector<char> active_;
+  KvPager pager_;            // paged KV: one logical table, installed on every stage
+  int kv_pages_ = 0;         // pool pages per stage
+  void kv_grant(size_t slot, int n_tokens);   // throws when the pool is exhausted
+  void kv_sync();            // push a changed table to the stages (between engine calls)
   int slot_pos(size_t i) const {
     return (i < prompts_.size() ? (int)prompts_[i].size() : 0) + rounds_done_ - (i < base_round_.size() ? base_round_[i] : 0);
   }

@@ -353,6 +353,7 @@ void HipStage::alloc_runtime() {
     moe_lists_ = (int32_t*)zalloc((size_t)cfg_.n_expert * scratch_rows_ * k * 4);
     moe_w_ = (float*)zalloc((size_t)scratch_rows_ * k * 4);
     moe_h_ = (f16*)zalloc((size_t)scratch_rows_ * k * Kff_ * 2);
+    if (opt_.deterministic) moe_yslot_ = (float*)zalloc((size_t)std::min(scratch_rows_, 64) * k * cfg_.d_model * 4);
   }
   if (spec_.last()) {
     logits_ld_ = (int)round_up(cfg_.vocab, 16);
@@ -380,20 +381,40 @@ void HipStage::alloc_runtime() {
     ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
   }
   attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
-  // KV cache: static paging, every slot owns max_ctx/64 pages
+  if (opt_.deterministic) {
+    // fixed-order split-K: the largest nsplit x rows x N of any ATOMIC GEMV call (<= 64 rows each)
+    size_t need = 0;
+    auto acc = [&](const PackedMat& m) {
+      if (!m.d) return;
+      for (int M : {1, 16, 32, 64}) {
+        const int ns = det_splits((int)m.dims.ntiles, (int)m.dims.nsb, M, EPI_ATOMIC);
+        if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
+      }
+    };
+    for (const LayerW& L : layers_) {
+      for (const MatSeg& sg : L.qkv) acc(sg.m);
+      acc(L.wo);
+      acc(L.down);
+      if (L.moe) acc(L.ex.router);
+    }
+    if (need) det_part_ = (float*)zalloc(need * 4);
+    det_part_n_ = need;
+  }
+  // KV cache: a pool of kv_pages 64-token pages per layer + one TRASH page (id kv_pages) that
+  // unmapped block-table entries point at (idle rows of a micro-batch still append K/V); the engine's
+  // KvPager installs the table (set_block_table)
   const int n_slots = NM * B;
   max_pages_ = opt_.max_ctx / 64;
-  const int64_t n_pages = (int64_t)n_slots * max_pages_;
-  const size_t per = (size_t)n_pages * Hkv * 64 * Dp_ * 2;
+  n_pages_ = opt_.kv_pages > 0 ? opt_.kv_pages : n_slots * max_pages_;
+  const size_t per = (size_t)(n_pages_ + 1) * Hkv * 64 * Dp_ * 2;
   for (size_t i = 0; i < layers_.size(); ++i) {
     kc_.push_back((f16*)zalloc(per));
     vc_.push_back((f16*)zalloc(per));
     kv_bytes_ += 2 * per;
   }
-  std::vector<int32_t> bt((size_t)n_slots * max_pages_);
-  for (size_t i = 0; i < bt.size(); ++i) bt[i] = (int32_t)i;
-  block_table_ = (int32_t*)dmalloc(bt.size() * 4);
-  HIP_OK(hipMemcpy(block_table_, bt.data(), bt.size() * 4, hipMemcpyHostToDevice));
+  host_bt_.assign((size_t)n_slots * max_pages_, n_pages_);
+  block_table_ = (int32_t*)dmalloc(host_bt_.size() * 4);
+  HIP_OK(hipMemcpy(block_table_, host_bt_.data(), host_bt_.size() * 4, hipMemcpyHostToDevice));
   // RoPE table (NORM mode), Llama-3.1 frequency factors if present
   const int hd2 = cfg_.head_dim / 2;
   std::vector<float2> cs((size_t)opt_.max_ctx * hd2);
@@ -427,10 +448,11 @@ void HipStage::alloc_runtime() {
   if (spec_.last())
     for (int mb = 0; mb < NM; ++mb) last_h_.push_back((float*)zalloc((size_t)B * d * 4));
   HIP_OK(hipDeviceSynchronize());
-  MP_LOGI("stage %d: layers %d-%d offloaded to GPU %d (%s), weights %.2f GiB, KV %.2f GiB (%d slots x %d ctx)",
+  MP_LOGI("stage %d: layers %d-%d offloaded to GPU %d (%s), weights %.2f GiB, KV %.2f GiB (%d pages of 64 tokens; "
+          "%d slots x <= %d ctx)",
           spec_.stage, spec_.layer_begin, spec_.layer_end - 1, spec_.device,
           spec_.first() && spec_.last() ? "embd+head" : spec_.first() ? "embd" : spec_.last() ? "head" : "mid",
-          weight_bytes_ / 1073741824.0, kv_bytes_ / 1073741824.0, n_slots, opt_.max_ctx);
+          weight_bytes_ / 1073741824.0, kv_bytes_ / 1073741824.0, n_pages_, n_slots, opt_.max_ctx);
 }
 
 void HipStage::set_positions(int mb, const std::vector<int32_t>& pos) {
@@ -442,9 +464,18 @@ void HipStage::set_positions(int mb, const std::vector<int32_t>& pos) {
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
-// KV of one slot: its pages are contiguous (identity block table: slot s owns pages
-// [s * max_pages, (s + 1) * max_pages)), page = [Hkv][64][Dp] f16; per layer the first
-// ceil(n_tok / 64) pages of K, then of V
+void HipStage::set_block_table(const std::vector<int32_t>& t) {
+  if (t.size() != host_bt_.size()) throw std::runtime_error("set_block_table: size mismatch");
+  for (int32_t e : t)
+    if (e < 0 || e > n_pages_) throw std::runtime_error("set_block_table: page id out of range");
+  HIP_OK(hipSetDevice(spec_.device));
+  HIP_OK(hipStreamSynchronize(stream_));   // no launch may still read the old table
+  host_bt_ = t;
+  HIP_OK(hipMemcpy(block_table_, host_bt_.data(), host_bt_.size() * 4, hipMemcpyHostToDevice));
+}
+
+// KV of one slot: per layer the first ceil(n_tok / 64) pages of K, then of V, each page
+// [Hkv][64][Dp] (K) / [Hkv][Dp][64] (V) f16, located through the slot's block-table row
 size_t HipStage::kv_state_bytes(int n_tok) const {
   const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
   return kc_.size() * 2 * (size_t)((n_tok + 63) / 64) * page;
@@ -452,30 +483,36 @@ size_t HipStage::kv_state_bytes(int n_tok) const {
 
 void HipStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
   HIP_OK(hipSetDevice(spec_.device));
-  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2, n = (size_t)((n_tok + 63) / 64) * page;
-  const size_t off = (size_t)slot * max_pages_ * page;
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  const int np = (n_tok + 63) / 64;
   const size_t base = out.size();
   out.resize(base + kv_state_bytes(n_tok));
   uint8_t* dst = out.data() + base;
   HIP_OK(hipStreamSynchronize(stream_));
   for (size_t li = 0; li < kc_.size(); ++li)
-    for (f16* c : {kc_[li], vc_[li]}) {
-      HIP_OK(hipMemcpy(dst, reinterpret_cast<const uint8_t*>(c) + off, n, hipMemcpyDeviceToHost));
-      dst += n;
-    }
+    for (f16* c : {kc_[li], vc_[li]})
+      for (int k = 0; k < np; ++k) {
+        const int32_t pg = host_bt_[(size_t)slot * max_pages_ + k];
+        if (pg >= n_pages_) throw std::runtime_error("kv_export: slot has no page for its tokens");
+        HIP_OK(hipMemcpy(dst, reinterpret_cast<const uint8_t*>(c) + (size_t)pg * page, page, hipMemcpyDeviceToHost));
+        dst += page;
+      }
 }
 
 void HipStage::kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) {
   if (bytes != kv_state_bytes(n_tok)) throw std::runtime_error("kv_import: size mismatch");
   HIP_OK(hipSetDevice(spec_.device));
-  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2, n = (size_t)((n_tok + 63) / 64) * page;
-  const size_t off = (size_t)slot * max_pages_ * page;
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  const int np = (n_tok + 63) / 64;
   HIP_OK(hipStreamSynchronize(stream_));
   for (size_t li = 0; li < kc_.size(); ++li)
-    for (f16* c : {kc_[li], vc_[li]}) {
-      HIP_OK(hipMemcpy(reinterpret_cast<uint8_t*>(c) + off, data, n, hipMemcpyHostToDevice));
-      data += n;
-    }
+    for (f16* c : {kc_[li], vc_[li]})
+      for (int k = 0; k < np; ++k) {
+        const int32_t pg = host_bt_[(size_t)slot * max_pages_ + k];
+        if (pg >= n_pages_) throw std::runtime_error("kv_import: slot has no page for its tokens");
+        HIP_OK(hipMemcpy(reinterpret_cast<uint8_t*>(c) + (size_t)pg * page, data, page, hipMemcpyHostToDevice));
+        data += page;
+      }
 }
 
 uint64_t HipStage::sample_step() {
@@ -566,6 +603,17 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     p.nsb = (int)m.dims.nsb;
     p.n_valid = n_valid;
     const int nsplit = allow_split ? gemv_auto_split(p.ntiles, p.nsb, p.M, epi) : 1;
+    const int ns = det_splits(p.ntiles, p.nsb, p.M, epi, allow_split);
+    if (opt_.deterministic && epi == EPI_ATOMIC && ns > 1) {
+      // split s stores its partial to det_part_[s]; then one fixed-order reduction adds them into Y
+      const int ldp = p.ntiles * 16;
+      if ((size_t)ns * p.M * ldp > det_part_n_) throw std::runtime_error("deterministic split-K scratch too small");
+      GemvParams q = p;
+      q.Y = det_part_; q.ldy = ldp; q.split_stride = (int64_t)p.M * ldp;
+      launch_gemv(m.ptype, EPI_STORE, q, ns, st);
+      launch_splitk_reduce(det_part_, ns, (int64_t)p.M * ldp, ldp, p.M, n_valid, p.Y, ldy, st);
+      continue;
+    }
     launch_gemv(m.ptype, epi, p, nsplit, st);
   }
 }
@@ -601,6 +649,7 @@ void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, floa
   dp.ntiles = (int)L.ex.down.dims.ntiles; dp.nsb = (int)L.ex.down.dims.nsb;
   dp.X = moe_h_; dp.ldx = Kff_; dp.x_per_slot = 1; dp.H = nullptr; dp.ldh = 0;
   dp.Y = x + (size_t)r0 * d; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
+  if (opt_.deterministic) dp.Yslot = moe_yslot_;   // per-slot outputs, combined in expert-rank order below
   // only ~k/E of the expert grid is busy: size the split for the active experts
   const int active = std::min(E, M * k);
   // v1 (M > 64): one tile per 1-wave workgroup, ~4096 of them; v2: 8-tile workgroups, ~1024 of
@@ -608,6 +657,15 @@ void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, floa
   const int nsplit = M <= 64 ? std::max(1, std::min(dp.nsb / 4, 1024 / std::max(1, (dp.ntiles + 7) / 8 * active)))
                              : std::max(1, std::min(dp.nsb / 4, 4096 / std::max(1, dp.ntiles * active)));
   launch_moe_gemv(L.ex.down.ptype, EPI_ATOMIC, dp, nsplit, st);
+  if (opt_.deterministic) launch_moe_combine(moe_yslot_, d, k, M, d, x + (size_t)r0 * d, d, st);
+}
+
+// split count launch_gemv will actually use (deterministic mode reproduces its rounding)
+int HipStage::det_splits(int ntiles, int nsb, int M, int epi, bool allow_split) const {
+  if (!allow_split) return 1;
+  int ns = std::max(1, gemv_auto_split(ntiles, nsb, M, epi));
+  const int per = (nsb + ns - 1) / ns;
+  return (nsb + per - 1) / per;
 }
 
 void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* kvlen,

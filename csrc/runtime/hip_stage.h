@@ -108,6 +108,7 @@ class HipStage : public Stage {
   size_t weight_bytes() const override { return weight_bytes_; }
   size_t kv_bytes() const override { return kv_bytes_; }
   void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) override;
+  void set_block_table(const std::vector<int32_t>& table) override;
   void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) override;
   size_t kv_state_bytes(int n_tok) const override;
   uint64_t sample_step() override;
@@ -124,7 +125,8 @@ class HipStage : public Stage {
                      bool decode, hipStream_t st);
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
-  bool fuse_norm(int M) const;   // RMSNorm folded into the consuming GEMVs at this row count
+  bool fuse_norm(int M) const;
+  int det_splits(int ntiles, int nsb, int M, int epi, bool allow_split = true) const;   // RMSNorm folded into the consuming GEMVs at this row count
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
             int n_valid, bool allow_split, hipStream_t st,
             const GemvParams* extras = nullptr);
@@ -156,6 +158,8 @@ class HipStage : public Stage {
   int act_rows_ = 0, scratch_rows_ = 0;
 
   // scratch (shared by micro-batches: compute is serial on the stage's stream)
+  float* det_part_ = nullptr; size_t det_part_n_ = 0;   // deterministic split-K partials
+  float* moe_yslot_ = nullptr;                           // deterministic MoE per-slot down outputs
   float* ssq_ = nullptr;   // [64] deferred-norm sums of squares, immediately followed by qkv_
   f16* xn_ = nullptr; float* qkv_ = nullptr; f16* q_ = nullptr; f16* attn_ = nullptr; f16* h_ = nullptr;
   float* gu_ = nullptr;   // unfused gate|up f32
@@ -168,7 +172,8 @@ class HipStage : public Stage {
   float* moe_w_ = nullptr; f16* moe_h_ = nullptr;
   // KV
   std::vector<f16*> kc_, vc_;
-  int32_t* block_table_ = nullptr; int max_pages_ = 0;
+  int32_t* block_table_ = nullptr; int max_pages_ = 0; int n_pages_ = 0;   // paged KV (kvpager.h)
+  std::vector<int32_t> host_bt_;                                            // host copy of the table
   float2* rope_cs_ = nullptr;
   std::vector<float> rope_ff_;
   // per-mb I/O

@@ -33,6 +33,7 @@ struct GemvParams {
   float eps = 0.f;
   int d_norm = 0;                // row length of the norm (d_model; multiple of 8)
   float* ssq = nullptr;          // ATOMIC + Xf: [M] sum of squares accumulator (zeroed by the caller)
+  int64_t split_stride = 0;      // STORE: split s writes Y + s * split_stride (deterministic split-K partials)
   const float* bias = nullptr;   // [n] added once (split 0) to STORE / ATOMIC outputs
   float* zero = nullptr;         // side job after the GEMV: zero_n floats cleared
   int64_t zero_n = 0;
@@ -61,6 +62,11 @@ void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, i
 
 // Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.
 void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
+
+// Y[m][n] += sum_{s < nsplit} part[s][m][n], s ascending: the fixed-order split-K reduction of the
+// deterministic mode (part rows of ldp floats, splits split_stride floats apart)
+void launch_splitk_reduce(const float* part, int nsplit, int64_t split_stride, int ldp, int M, int n, float* Y, int ldy,
+                          hipStream_t st);
 
 // x f32 [M][ldx] -> out f16 [M][ldo] = rmsnorm(x) * w ; also zero `zero_n` floats at `zero`
 // `zero` is filled with 0, or with `bias` repeated every `bias_n` floats when bias != nullptr (the
@@ -197,7 +203,11 @@ struct MoeGemvParams {
   int n_valid;
   int sb_per_split;      // set by the launcher
   int M = 0;             // tokens of the call (bound on rows per expert); 1..64 -> workgroup-shared x kernel
+  float* Yslot = nullptr;  // deterministic mode: down out stored per slot [M*k][ldy] (weight applied,
+                           // no split-K); launch_moe_combine then adds the k slots in order
 };
+// Y[t][n] += sum_{j < k} Yslot[t*k + j][n], j ascending (deterministic MoE combine)
+void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, float* Y, int ldy, hipStream_t st);
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
 void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st);
 

@@ -25,6 +25,9 @@ struct StageOptions {
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
+  int kv_pages = 0;          // KV pool pages per stage (64 tokens each; 0: n_slots x max_ctx / 64)
+  bool deterministic = false;  // split-K and MoE partials reduced in a fixed order (no float atomics
+                               // on shared outputs): bitwise-reproducible logits, PP=1 == PP=S
   bool fused_norm = false;  // M <= 4 rows: deferred RMSNorm folded into the qkv / gate-up GEMVs (gemv2.hip);
                             // off by default: 8B mb1 470.7 vs 473.7 tok/s, 70B mb1 92.5 vs 104.8 (r2i)
 };
@@ -94,6 +97,9 @@ class Stage {
   // f32 rows), appended to `out`; kv_import writes the same bytes back.  Called with the stage
   // idle (between decode_steps calls).
   virtual void kv_export(int slot, int n_tok, std::vector<uint8_t>& out) = 0;
+  // paged KV (kvpager.h): the block table [n_slots][max_ctx / 64] of page ids (kv_pages = TRASH),
+  // installed between engine calls (the stage's stream is idle or synchronised first)
+  virtual void set_block_table(const std::vector<int32_t>& table) = 0;
   virtual void kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) = 0;
   virtual size_t kv_state_bytes(int n_tok) const = 0;   // bytes kv_export appends for n_tok
   // sampling step counter (seeds the per-row RNG streams of the sampler)

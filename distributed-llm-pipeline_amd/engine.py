@@ -84,6 +84,11 @@ class Engine:
                 "admit")
         self._n_seq = self.n_seq_cap
 
+    def kv_stats(self):
+        """Live paged-KV numbers: pool pages, free pages (the `info` dict is a load-time snapshot)."""
+        j = N.jcall(N.lib().mp_engine_info, self._h, what="engine info")
+        return {"kv_pages": j["kv_pages"], "kv_free_pages": j["kv_free_pages"]}
+
     def release(self, slot: int):
         """Mark a slot idle (its sequence is finished); it can be admitted again."""
         N.check(N.lib().mp_engine_release(self._h, int(slot)), "release")
