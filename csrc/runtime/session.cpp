@@ -1,6 +1,7 @@
 #include "session.h"
 
 #include <algorithm>
+#include <deque>
 #include <chrono>
 #include <cstdio>
 
@@ -158,9 +159,21 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     GenResult res;
     Utf8Acc acc;
     int step = 0;
+    int pages = 0;   // KV pages reserved for prompt + n_predict (paged KV admission control)
     double t0 = 0, t1 = 0;
   };
+  struct Pending {
+    Served s;
+    std::vector<int32_t> prompt;
+    int pages = 0;
+  };
   const int cap = capacity(), max_ctx = eng_.max_ctx();
+  // paged KV (kvpager.h): a request is admitted only when the pool can hold its prompt plus every
+  // token it may generate on top of what the running requests may still grow into, so a decode
+  // round never runs out of pages; requests that do not fit wait (FIFO) for pages to come back
+  const int pool = eng_.kv_pages();
+  int reserved = 0;
+  std::deque<Pending> waiting;
   std::vector<std::unique_ptr<Live>> live(cap);
   auto consume = [&](int slot, int32_t t) -> bool {   // false: the request is finished
     Live& L = *live[slot];
@@ -174,7 +187,8 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     ++L.step;
     if (!p.empty() && L.s.req.on_piece && !L.s.req.on_piece(p)) { r.stop = "cancelled"; return false; }
     if (L.step >= L.s.req.n_predict) { r.stop = "length"; return false; }
-    if (eng_.slot_position(slot) + 1 >= max_ctx) { r.stop = "context"; return false; }
+    // the context or the request's share of the KV pool is full
+    if (eng_.slot_position(slot) + 1 >= std::min(max_ctx, L.pages * 64)) { r.stop = "context"; return false; }
     return true;
   };
   auto finish = [&](int slot) {
@@ -186,30 +200,42 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     L.res.decode_ms = now_ms() - L.t1;
     if (L.s.done) L.s.done(L.res);
     eng_.release(slot);
+    reserved -= L.pages;
     live[slot].reset();
   };
   for (;;) {
     int free = 0;
     for (auto& l : live) free += l ? 0 : 1;
-    std::vector<Served> fresh = free ? next(free) : std::vector<Served>{};
-    if (!fresh.empty()) {
-      if ((int)fresh.size() > free) throw std::runtime_error("serve: more requests than free slots");
-      std::vector<int> slots;
-      std::vector<std::vector<int32_t>> prompts;
-      const bool idle = free == cap;
-      for (auto& f : fresh) {
-        int sl = 0;
-        while (live[sl] || std::find(slots.begin(), slots.end(), sl) != slots.end()) ++sl;
-        std::vector<int32_t> pr = encode(f.req.prompt);
-        if ((int)pr.size() >= max_ctx) pr.erase(pr.begin(), pr.end() - (max_ctx / 2));
-        auto L = std::make_unique<Live>();
-        L->s = std::move(f);
-        L->res.n_prompt = (int)pr.size();
-        L->t0 = now_ms();
-        live[sl] = std::move(L);
-        slots.push_back(sl);
-        prompts.push_back(std::move(pr));
+    // new requests only when nobody is waiting for pages (FIFO)
+    if (free > (int)waiting.size() && waiting.empty())
+      for (auto& f : next(free)) {
+        Pending pd;
+        pd.prompt = encode(f.req.prompt);
+        if ((int)pd.prompt.size() >= max_ctx) pd.prompt.erase(pd.prompt.begin(), pd.prompt.end() - (max_ctx / 2));
+        const long want = (long)pd.prompt.size() + std::max(0, f.req.n_predict) + 1;
+        pd.pages = (int)std::min<long>({(want + 63) / 64, (long)max_ctx / 64, (long)pool});
+        pd.s = std::move(f);
+        waiting.push_back(std::move(pd));
       }
+    std::vector<int> slots;
+    std::vector<std::vector<int32_t>> prompts;
+    const bool idle = free == cap;
+    while (!waiting.empty() && (int)slots.size() < free && reserved + waiting.front().pages <= pool) {
+      Pending pd = std::move(waiting.front());
+      waiting.pop_front();
+      int sl = 0;
+      while (live[sl] || std::find(slots.begin(), slots.end(), sl) != slots.end()) ++sl;
+      auto L = std::make_unique<Live>();
+      L->res.n_prompt = (int)pd.prompt.size();
+      L->pages = pd.pages;
+      L->s = std::move(pd.s);
+      L->t0 = now_ms();
+      reserved += L->pages;
+      live[sl] = std::move(L);
+      slots.push_back(sl);
+      prompts.push_back(std::move(pd.prompt));
+    }
+    if (!slots.empty()) {
       // nothing running: a plain start() of slots 0..n-1 (resets the engine's rounds)
       if (idle && slots.back() == (int)slots.size() - 1) eng_.start(prompts);
       else eng_.admit(slots, prompts);
@@ -224,7 +250,7 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     bool any = false;
     for (auto& l : live) any = any || (bool)l;
     if (!any) {
-      if (fresh.empty()) return;
+      if (waiting.empty() && slots.empty()) return;
       continue;
     }
     eng_.decode_steps(1);

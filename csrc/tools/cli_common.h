@@ -149,6 +149,7 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--master") master = val();
     else if (a == "--prefetch") e["prefetch"] = true;
     else if (a == "--gpu-mem") e["gpu_mem_gib"] = std::atof(val().c_str());
+    else if (a == "--kv-pool") e["kv_pool_tokens"] = std::atoi(val().c_str());   // paged KV pool (tokens per stage)
     else if (a == "--force") e["force"] = true;
     else if (a == "--base-port") e["base_port"] = std::atoi(val().c_str());
     else if (a == "--rpc") rpc = val();

@@ -390,6 +390,36 @@ def test_continuous_batching_admits_mid_generation(native_bins, tiny_gguf):
         s.close()
 
 
+def test_kv_pool_admission_waits_for_pages(native_bins, tiny_gguf):
+    """Paged KV: with a pool that holds ONE request's prompt + n_predict, a second concurrent
+    request waits for the first one's pages instead of failing mid-decode; both texts equal the CLI's."""
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-c", "512", "-ngl", "0", "--no-display-prompt"]
+    p1, p2 = "The pipeline sends activations", "Once upon a time"
+    def cli(p, n):
+        out = subprocess.run(base + ["-p", p, "-n", str(n)], capture_output=True, timeout=120).stdout
+        return out.decode("utf-8", errors="replace").rstrip("\n")
+    ref1, ref2 = cli(p1, 100), cli(p2, 100)
+    s = Orchestrator("-m", tiny_gguf, "-ngl", "0", "-c", "512", "--mb-size", "2", "--kv-pool", "192",
+                     "--threads", "2")
+    try:
+        done = {}
+
+        def go(name, prompt):
+            r = httpx.post(s.url + "/completion", json={"prompt": prompt, "n_predict": 100}, timeout=120).json()
+            done[name] = (time.time(), r["content"])
+
+        ts = [threading.Thread(target=go, args=(n, p)) for n, p in (("a", p1), ("b", p2))]
+        ts[0].start()
+        time.sleep(0.2)
+        ts[1].start()
+        for t in ts:
+            t.join()
+        assert done["a"][1] == ref1 and done["b"][1] == ref2
+        assert done["a"][0] < done["b"][0]     # b ran after a returned its pages
+    finally:
+        s.close()
+
+
 def test_cli_gpu_mem_force_prefetch(native_bins, tiny_gguf):
     """prima.cpp launch flags: --gpu-mem budget check, --force, --prefetch."""
     base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-p", "abc", "-n", "4", "-c", "128", "-ngl", "0",
