@@ -455,6 +455,12 @@ void launch_attention(const AttnParams& p, hipStream_t st) {
   }
 }
 
+// LSE merge of n_split partials (o_part / ml_part, [z][m * Hq + h]) into out
+void launch_attn_combine(const AttnParams& p, hipStream_t st) {
+  if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_combine_kernel<128>, dim3(p.M * p.Hq), dim3(128), 0, st, p);
+  else hipLaunchKernelGGL(mpk::attn_combine_kernel<64>, dim3(p.M * p.Hq), dim3(64), 0, st, p);
+}
+
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
   dim3 grid(p.M, p.Hkv, p.n_split);
   if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_decode_kernel<128>, grid, dim3(256), 0, st, p);

@@ -1,0 +1,227 @@
+// Prefill flash attention on MFMA (K7, prompt chunks): many query rows per workgroup, K/V tiles
+// staged once per workgroup in LDS, causal tile skipping, one launch per packed chunk.
+//
+// The decode-shaped attn_kernel (attention.hip) gave every row group of 16 MFMA rows (2-4 tokens x
+// the G heads of one kv head) its own pass over the whole K/V of the sequence: at a 32K prompt each
+// layer-chunk re-streamed ~16 GB of K/V and attention was 64 % of prefill time
+// (profiles/r1g_prof_8b_ctx32k_mb1.txt).  Here one 512-thread workgroup owns 128 MFMA rows
+// rho = t * G + g (BT = 128 / G consecutive tokens of ONE sequence x the G query heads of kv head
+// `kvh`), 16 rows per wave, and walks the 64-key pages up to its last token's position:
+//   * the page's K [64][Dp] and V^T [Dp][64] are loaded once per workgroup (register prefetch of
+//     page j+1 while page j is consumed) into padded, double-buffered LDS tiles shared by 8 waves;
+//   * per 32-key chunk a wave computes S^T = K Q^T (A = K rows in the permuted order
+//     pi(c, R) = 8(R>>2) + 4c + (R&3), B = Q^T in registers) so the exponentiated scores already
+//     form the B operand of O^T += V^T P^T (A = V^T rows from LDS) -- as in the decode kernel;
+//   * online softmax in f32 registers; keys past a row's own position are masked; pages past the
+//     workgroup's last token are never touched (causal tile skip).
+// Work list: the host splits every prefill segment (rows of one sequence, consecutive positions)
+// into tiles of <= BT rows and passes them as kernel arguments (m0 | n << 16), so a chunk packing
+// many sequences is one launch.
+#include "kcommon.h"
+#include "../runtime/kernels_api.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace mpk {
+using namespace mp;
+
+template <int DP>
+__global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnParams p) {
+  constexpr int NW = 8;
+  constexpr int KK = DP / 32;    // k-steps of S^T over d
+  constexpr int DT = DP / 16;    // 16-row d tiles of O^T
+  constexpr int KLD = DP + 8;    // K tile row stride (f16): 16 key rows of a fragment hit distinct banks
+  constexpr int VLD = 64 + 8;    // V^T tile row stride (f16)
+  constexpr int KCH = 64 * DP / 8 / (NW * 64);   // 16 B K chunks per thread per page (= V chunks)
+  __shared__ __attribute__((aligned(16))) f16 ks[2][64 * KLD];
+  __shared__ __attribute__((aligned(16))) f16 vs[2][DP * VLD];
+
+  const int tile = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
+  if (tile >= p.n_tiles) return;
+  const int m0 = (int)(p.tiles[tile] & 0xFFFFu), n = (int)(p.tiles[tile] >> 16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q4 = lane >> 4, col = lane & 15;
+  const int G = p.Hq / p.Hkv;
+  const int R = 16 * wave + col;            // MFMA row of this lane's column
+  const int t = R / G, g = R - t * G;
+  const bool rvalid = t < n && R < (128 / G) * G;
+  const int m = m0 + (rvalid ? t : 0);
+  const int h = kvh * G + g;
+  const int my_pos = rvalid ? p.pos[m] : -1;
+  const int pmax = p.pos[m0 + n - 1];       // rows of a tile: consecutive positions of one slot
+  const int32_t* bt = p.block_table + (size_t)p.slot[m0] * p.max_pages;
+  const int n_kt_all = pmax / 64 + 1;       // causal: pages past the last row are skipped
+  // KV split z (grid.z) takes pages [kt0, kt1); its (m, l, O) partials are merged by attn_combine
+  const int sp = p.n_split > 1 ? p.split_pages : n_kt_all;
+  const int kt0 = min(z * sp, n_kt_all), kt1 = min(kt0 + sp, n_kt_all);
+  const int n_kt = kt1 - kt0;
+
+  // Q^T fragments: lane holds q[m][h][d = 32kk + 8q4 + j] (q_scale already applied)
+  half8_t qf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk)
+    qf[kk] = rvalid ? *reinterpret_cast<const half8_t*>(p.q + ((size_t)m * p.Hq + h) * DP + 32 * kk + 8 * q4)
+                    : half8_t{};
+
+  // page staging: thread owns K chunks (key = c / (DP/8), d8 = c % (DP/8)) and V^T chunks
+  // (d = c / 8, k8 = c % 8), c = tid + 512 j
+  u32x4 kr[KCH], vr[KCH];
+  auto load_page = [&](int kt) {
+    const int page = bt[kt];
+    const f16* kb = p.k_cache + ((size_t)page * p.Hkv + kvh) * 64 * DP;
+    const f16* vb = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) {
+      const int c = tid + NW * 64 * j;
+      kr[j] = *reinterpret_cast<const u32x4*>(kb + (size_t)c * 8);
+      vr[j] = *reinterpret_cast<const u32x4*>(vb + (size_t)c * 8);
+    }
+  };
+  auto store_page = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) {
+      const int c = tid + NW * 64 * j;
+      *reinterpret_cast<u32x4*>(&ks[buf][(c / (DP / 8)) * KLD + (c % (DP / 8)) * 8]) = kr[j];
+      *reinterpret_cast<u32x4*>(&vs[buf][(c / 8) * VLD + (c % 8) * 8]) = vr[j];
+    }
+  };
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int krow0 = 8 * (col >> 2) + (col & 3);   // pi(c, R) - 4c
+
+  if (n_kt > 0) {
+    load_page(kt0);
+    store_page(0);
+    __syncthreads();
+    if (n_kt > 1) load_page(kt0 + 1);
+  }
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int buf = kt & 1;
+    const f16* kt_s = ks[buf];
+    const f16* vt_s = vs[buf];
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const int P0 = (kt0 + kt) * 64 + kc * 32;
+      f32x4 s[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const half8_t kf = *reinterpret_cast<const half8_t*>(kt_s + (32 * kc + krow0 + 4 * c) * KLD + 32 * kk + 8 * q4);
+          a = mfma16x16x32(kf, qf[kk], a);
+        }
+        s[c] = a;
+      }
+      // lane holds scores of row `col` for keys P0 + 8 q4 + 4c + i
+      float mx = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = P0 + 8 * q4 + 4 * c + i <= my_pos ? s[c][i] : -INFINITY;
+          s[c][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = m_new == -INFINITY ? 1.f : __expf(m_run - m_new);
+      float psum = 0.f;
+      half8_t pf;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = m_new == -INFINITY ? 0.f : __expf(s[c][i] - m_new);
+          psum += e;
+          pf[4 * c + i] = (f16)e;
+        }
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const half8_t vf = *reinterpret_cast<const half8_t*>(vt_s + (16 * dt + col) * VLD + 32 * kc + 8 * q4);
+        o[dt] = mfma16x16x32(vf, pf, o[dt] * alpha);
+      }
+    }
+    if (kt + 1 < n_kt) {
+      store_page(buf ^ 1);        // page kt+1 (loaded one page ago); buf^1 was released by the last barrier
+      __syncthreads();
+      if (kt + 2 < n_kt) load_page(kt0 + kt + 2);
+    }
+  }
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+  if (!rvalid) return;
+  if (p.n_split > 1) {   // unnormalised partials, the attn_combine layout [z][m * Hq + h][Dp]
+    const size_t rid = (size_t)m * p.Hq + h, stride = (size_t)p.M * p.Hq;
+    float* op = p.o_part + ((size_t)z * stride + rid) * DP;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      *reinterpret_cast<float4*>(op + 16 * dt + 4 * q4) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+    if (q4 == 0) {
+      float* ml = p.ml_part + ((size_t)z * stride + rid) * 2;
+      ml[0] = n_kt > 0 ? m_run : -INFINITY;
+      ml[1] = n_kt > 0 ? l_run : 0.f;
+    }
+    return;
+  }
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  f16* orow = p.out + (size_t)m * p.ldo + (size_t)h * p.hd;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int d0 = 16 * dt + 4 * q4;   // lane holds O^T[d0 + i][row]
+    if (d0 + 4 <= p.hd) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<h4*>(orow + d0) = h4{(f16)(o[dt][0] * inv), (f16)(o[dt][1] * inv), (f16)(o[dt][2] * inv),
+                                             (f16)(o[dt][3] * inv)};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (d0 + i < p.hd) orow[d0 + i] = (f16)(o[dt][i] * inv);
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+int prefill_attn_rows_per_tile(int G) { return 128 / G; }
+
+void launch_attn_combine(const AttnParams& p, hipStream_t st);
+
+void launch_attn_prefill(const PrefillAttnParams& p, hipStream_t st) {
+  if (p.n_tiles <= 0) return;
+  if (p.n_tiles > kPrefillAttnMaxTiles) throw std::runtime_error("launch_attn_prefill: too many tiles");
+  if (p.Hq % p.Hkv || p.Hq / p.Hkv > 128) throw std::runtime_error("launch_attn_prefill: bad GQA group");
+  if (p.n_split > 1 && (!p.o_part || !p.ml_part || p.split_pages < 1))
+    throw std::runtime_error("launch_attn_prefill: split without partial buffers");
+  const dim3 grid(p.n_tiles, p.Hkv, std::max(1, p.n_split)), block(512);
+  if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_prefill_kernel<128>, grid, block, 0, st, p);
+  else if (p.Dp == 64) hipLaunchKernelGGL(mpk::attn_prefill_kernel<64>, grid, block, 0, st, p);
+  else throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
+  if (p.n_split > 1) {   // LSE merge of the splits into out (attention.hip)
+    AttnParams a{};
+    a.M = p.M; a.Hq = p.Hq; a.hd = p.hd; a.Dp = p.Dp; a.n_split = p.n_split;
+    a.o_part = p.o_part; a.ml_part = p.ml_part; a.out = p.out; a.ldo = p.ldo;
+    launch_attn_combine(a, st);
+  }
+}
+
+// KV splits for a chunk: enough (tile, kv head, split) workgroups to cover the CUs twice, >= 4 pages
+// per split, at most max_split (the partial buffers)
+int prefill_attn_splits(int n_tiles, int Hkv, int max_pages_needed, int max_split, int* split_pages) {
+  const int wgs = std::max(1, n_tiles * Hkv);
+  int ns = std::min(max_split, std::max(1, (512 + wgs - 1) / wgs));
+  ns = std::max(1, std::min(ns, max_pages_needed / 4));
+  *split_pages = (max_pages_needed + ns - 1) / ns;
+  return (max_pages_needed + *split_pages - 1) / *split_pages;
+}
+
+}  // namespace mp

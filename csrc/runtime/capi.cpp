@@ -263,6 +263,31 @@ int mp_op_attention(const void* q, const void* kvlen, const void* slot, const vo
   API_CATCH(-1)
 }
 
+// prefill flash attention over a packed chunk: segs = (row0, T) pairs of consecutive rows of one
+// sequence each; the tiles are cut here exactly as the engine cuts them
+int mp_op_attn_prefill(const void* q, const void* pos, const void* slot, const void* block_table, int max_pages,
+                       const void* k_cache, const void* v_cache, int Hq, int Hkv, int hd, int Dp, const int32_t* segs,
+                       int n_segs, void* out, int ldo, int n_split, int split_pages, void* o_part, void* ml_part,
+                       int M, void* stream) {
+  API_TRY
+  PrefillAttnParams p{};
+  p.q = (const f16*)q; p.pos = (const int32_t*)pos; p.slot = (const int32_t*)slot;
+  p.block_table = (const int32_t*)block_table; p.max_pages = max_pages;
+  p.k_cache = (const f16*)k_cache; p.v_cache = (const f16*)v_cache;
+  p.Hq = Hq; p.Hkv = Hkv; p.hd = hd; p.Dp = Dp; p.out = (f16*)out; p.ldo = ldo;
+  p.M = M; p.n_split = n_split; p.split_pages = split_pages; p.o_part = (float*)o_part; p.ml_part = (float*)ml_part;
+  const int bt = prefill_attn_rows_per_tile(Hq / Hkv);
+  for (int s = 0; s < n_segs; ++s)
+    for (int r = 0; r < segs[2 * s + 1]; r += bt) {
+      if (p.n_tiles == kPrefillAttnMaxTiles) { launch_attn_prefill(p, (hipStream_t)stream); p.n_tiles = 0; }
+      p.tiles[p.n_tiles++] = (uint32_t)(segs[2 * s] + r) | ((uint32_t)std::min(bt, segs[2 * s + 1] - r) << 16);
+    }
+  launch_attn_prefill(p, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_argmax(const void* logits, int ld, int n, int M, void* tokens, void* part, void* counters, void* stream) {
   API_TRY
   // part [M][kArgmaxChunks][2] f32 + counters [M] zeroed int32 select the two-level kernel

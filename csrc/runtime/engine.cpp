@@ -266,6 +266,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
   so.deterministic = j.get_bool("deterministic", false);
+  so.prefill_flash = j.get_bool("prefill_flash", true);
   so.fused_norm = j.get_bool("fused_norm", false) && !so.deterministic;   // its sums of squares are atomics
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);

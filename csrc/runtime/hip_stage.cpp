@@ -381,6 +381,10 @@ void HipStage::alloc_runtime() {
     ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
   }
   attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
+  if (opt_.prefill_flash && opt_.max_ctx > 256) {   // prefill KV-split partials (attn_prefill.hip)
+    pf_opart_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * Dp_ * 4);
+    pf_ml_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * 2 * 4);
+  }
   if (opt_.deterministic) {
     // fixed-order split-K: the largest nsplit x rows x N of any ATOMIC GEMV call (<= 64 rows each)
     size_t need = 0;
@@ -709,6 +713,40 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     rp.max_pages = max_pages_; rp.rope_cs = rope_cs_; rp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
     rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li];
     launch_rope_kv(rp, st);
+    if (!decode && opt_.prefill_flash) {
+      PrefillAttnParams pa{};
+      pa.q = q_; pa.pos = pos; pa.slot = slot; pa.block_table = block_table_; pa.max_pages = max_pages_;
+      pa.k_cache = kc_[li]; pa.v_cache = vc_[li]; pa.Hq = cfg_.n_head; pa.Hkv = cfg_.n_head_kv;
+      pa.hd = cfg_.head_dim; pa.Dp = Dp_; pa.out = attn_; pa.ldo = Ko_;
+      const int bt = prefill_attn_rows_per_tile(cfg_.n_head / cfg_.n_head_kv);
+      auto add_rows = [&](int row0, int T) {
+        for (int r = 0; r < T; r += bt) {
+          if (pa.n_tiles == kPrefillAttnMaxTiles) { launch_attn_prefill(pa, st); pa.n_tiles = 0; }
+          pa.tiles[pa.n_tiles++] = (uint32_t)(row0 + r) | ((uint32_t)std::min(bt, T - r) << 16);
+        }
+      };
+      int pages_needed = 0, n_tiles = 0;
+      if (segs_ && !segs_->empty()) {
+        for (const PrefillSeg& sg : *segs_) {
+          pages_needed = std::max(pages_needed, (sg.p0 + sg.T - 1) / 64 + 1);
+          n_tiles += (sg.T + bt - 1) / bt;
+        }
+      }
+      // long contexts: split every tile's pages over grid.z so the chunk fills the CUs; the LSE
+      // merge runs in the same launcher (one workgroup list per launch, so only when it fits one)
+      pa.M = M;
+      if (pf_opart_ && n_tiles > 0 && n_tiles <= kPrefillAttnMaxTiles) {
+        pa.n_split = prefill_attn_splits(n_tiles, cfg_.n_head_kv, pages_needed, kPrefillMaxSplit, &pa.split_pages);
+        pa.o_part = pf_opart_; pa.ml_part = pf_ml_;
+      }
+      if (segs_ && !segs_->empty()) {
+        int row = 0;
+        for (const PrefillSeg& sg : *segs_) { add_rows(row, sg.T); row += sg.T; }
+      } else {
+        add_rows(0, M);
+      }
+      launch_attn_prefill(pa, st);
+    } else {
     AttnParams ap{};
     ap.q = q_; ap.kvlen = kvlen; ap.slot = slot; ap.block_table = block_table_; ap.max_pages = max_pages_;
     ap.k_cache = kc_[li]; ap.v_cache = vc_[li]; ap.M = M; ap.Hq = cfg_.n_head; ap.Hkv = cfg_.n_head_kv;
@@ -737,6 +775,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       }
     } else {
       launch_attention(ap, st);
+    }
     }
   }
   if (small) {

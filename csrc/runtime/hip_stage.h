@@ -158,6 +158,8 @@ class HipStage : public Stage {
   int act_rows_ = 0, scratch_rows_ = 0;
 
   // scratch (shared by micro-batches: compute is serial on the stage's stream)
+  static constexpr int kPrefillMaxSplit = 8;
+  float* pf_opart_ = nullptr; float* pf_ml_ = nullptr;   // prefill attention KV-split partials
   float* det_part_ = nullptr; size_t det_part_n_ = 0;   // deterministic split-K partials
   float* moe_yslot_ = nullptr;                           // deterministic MoE per-slot down outputs
   float* ssq_ = nullptr;   // [64] deferred-norm sums of squares, immediately followed by qkv_

@@ -115,6 +115,29 @@ struct AttnParams {
 };
 void launch_attention(const AttnParams& p, hipStream_t st);
 
+// prefill flash attention (attn_prefill.hip): 128 MFMA rows (tokens x GQA heads) per workgroup,
+// K/V pages staged once per workgroup in LDS, causal page skipping.  One launch per chunk: the
+// tiles are (m0 | n << 16) runs of n <= 128 / G consecutive rows of ONE sequence (consecutive
+// positions), q [M][Hq][Dp] with q_scale applied, out [M][ldo] (head h at columns h * hd).
+constexpr int kPrefillAttnMaxTiles = 256;
+struct PrefillAttnParams {
+  const f16* q;
+  const int32_t* pos; const int32_t* slot;
+  const int32_t* block_table; int max_pages;
+  const f16* k_cache; const f16* v_cache;
+  int Hq, Hkv, hd, Dp;
+  f16* out; int ldo;
+  int M = 0;                     // rows of the chunk (partial-buffer layout)
+  int n_split = 1, split_pages = 1;   // KV splits (grid.z), pages per split
+  float* o_part = nullptr; float* ml_part = nullptr;   // [n_split][M*Hq][Dp], [n_split][M*Hq][2]
+  int n_tiles;
+  uint32_t tiles[kPrefillAttnMaxTiles];
+};
+void launch_attn_prefill(const PrefillAttnParams& p, hipStream_t st);
+// KV split count for a chunk (sets *split_pages); max_pages_needed = last row's position / 64 + 1
+int prefill_attn_splits(int n_tiles, int Hkv, int max_pages_needed, int max_split, int* split_pages);
+int prefill_attn_rows_per_tile(int G);   // tokens per tile: 128 / G
+
 // fused decode step of attention: RoPE(q, k) + KV append + split-K flash-decoding + last-arriver
 // merge (replaces rope_kv + attention + combine for tq = 1)
 struct DecodeAttnParams {

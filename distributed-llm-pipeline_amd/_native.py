@@ -53,6 +53,9 @@ _SIGS = {
     "mp_op_attention": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p], c_int),
     "mp_op_argmax": ([c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p], c_int),
+    "mp_op_attn_prefill": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                            c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                            c_void_p], c_int),
     "mp_op_gemv_fused": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                           c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_float, c_int, c_void_p, c_void_p,
                           c_void_p, c_int64, c_void_p], c_int),

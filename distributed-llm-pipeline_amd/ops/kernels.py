@@ -115,6 +115,25 @@ def embed(raw_table: torch.Tensor, ggml_type: int, d: int, tokens: torch.Tensor)
     return x
 
 
+def attn_prefill(q, pos, slot, block_table, k_cache, v_cache, Hkv, hd, segs=None, n_split=1, split_pages=1):
+    """Prefill flash attention (attn_prefill.hip): q [M][Hq][Dp] f16 (q_scale applied), rows in
+    `segs` = [(row0, T), ...] runs of consecutive positions of one sequence each (default: one run);
+    n_split > 1 splits every tile's pages (split_pages each) over workgroups, merged by attn_combine."""
+    M, Hq, Dp = q.shape
+    segs = segs or [(0, M)]
+    sa = np.asarray(segs, np.int32).reshape(-1)
+    out = torch.zeros(M, Hq * hd, dtype=torch.float16, device=q.device)
+    op = ml = None
+    if n_split > 1:
+        op = torch.full((n_split, M * Hq, Dp), float("nan"), dtype=torch.float32, device=q.device)
+        ml = torch.full((n_split, M * Hq, 2), float("nan"), dtype=torch.float32, device=q.device)
+    N.check(N.lib().mp_op_attn_prefill(_ptr(q), _ptr(pos), _ptr(slot), _ptr(block_table), block_table.shape[1],
+                                       _ptr(k_cache), _ptr(v_cache), Hq, Hkv, hd, Dp,
+                                       sa.ctypes.data, len(segs), _ptr(out), out.stride(0), n_split, split_pages,
+                                       _ptr(op), _ptr(ml), M, _stream()), "attn_prefill")
+    return out
+
+
 ARGMAX_CHUNKS = 64
 
 
