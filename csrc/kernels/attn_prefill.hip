@@ -21,19 +21,24 @@
 #include "../runtime/kernels_api.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace mpk {
 using namespace mp;
 
-template <int DP>
-__global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnParams p) {
-  constexpr int NW = 8;
+// NW waves x RG row groups of 16 MFMA rows = 128 rows per workgroup.  RG = 2: every K / V^T
+// fragment read from LDS feeds two MFMAs (one per row group): with one row group per wave the
+// 16 ds_read_b128 per 32-key chunk kept the CU's LDS as busy as its matrix pipes.
+template <int DP, int NW, int RG>
+__global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttnParams p) {
   constexpr int KK = DP / 32;    // k-steps of S^T over d
   constexpr int DT = DP / 16;    // 16-row d tiles of O^T
   constexpr int KLD = DP + 8;    // K tile row stride (f16): 16 key rows of a fragment hit distinct banks
   constexpr int VLD = 64 + 8;    // V^T tile row stride (f16)
-  constexpr int KCH = 64 * DP / 8 / (NW * 64);   // 16 B K chunks per thread per page (= V chunks)
+  constexpr int NT = NW * 64;
+  constexpr int KCH = 64 * DP / 8 / NT;   // 16 B K chunks per thread per page (= V chunks)
+  static_assert(NW * RG * 16 == 128, "128 MFMA rows per workgroup");
   __shared__ __attribute__((aligned(16))) f16 ks[2][64 * KLD];
   __shared__ __attribute__((aligned(16))) f16 vs[2][DP * VLD];
 
@@ -43,12 +48,17 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q4 = lane >> 4, col = lane & 15;
   const int G = p.Hq / p.Hkv;
-  const int R = 16 * wave + col;            // MFMA row of this lane's column
-  const int t = R / G, g = R - t * G;
-  const bool rvalid = t < n && R < (128 / G) * G;
-  const int m = m0 + (rvalid ? t : 0);
-  const int h = kvh * G + g;
-  const int my_pos = rvalid ? p.pos[m] : -1;
+  bool rvalid[RG];
+  int m[RG], h[RG], my_pos[RG];
+#pragma unroll
+  for (int rg = 0; rg < RG; ++rg) {
+    const int R = 16 * (RG * wave + rg) + col;   // MFMA row of this lane's column
+    const int t = R / G, g = R - t * G;
+    rvalid[rg] = t < n && R < (128 / G) * G;
+    m[rg] = m0 + (rvalid[rg] ? t : 0);
+    h[rg] = kvh * G + g;
+    my_pos[rg] = rvalid[rg] ? p.pos[m[rg]] : -1;
+  }
   const int pmax = p.pos[m0 + n - 1];       // rows of a tile: consecutive positions of one slot
   const int32_t* bt = p.block_table + (size_t)p.slot[m0] * p.max_pages;
   const int n_kt_all = pmax / 64 + 1;       // causal: pages past the last row are skipped
@@ -57,15 +67,22 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
   const int kt0 = min(z * sp, n_kt_all), kt1 = min(kt0 + sp, n_kt_all);
   const int n_kt = kt1 - kt0;
 
-  // Q^T fragments: lane holds q[m][h][d = 32kk + 8q4 + j] (q_scale already applied)
-  half8_t qf[KK];
+  // Q^T fragments: lane holds q[m][h][d = 32kk + 8q4 + j] (q_scale already applied), times log2(e)
+  // so the softmax runs on v_exp_f32 (2^x) directly; m is kept in that base-2 domain
+  half8_t qf[RG][KK];
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk)
-    qf[kk] = rvalid ? *reinterpret_cast<const half8_t*>(p.q + ((size_t)m * p.Hq + h) * DP + 32 * kk + 8 * q4)
-                    : half8_t{};
+  for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      half8_t v = rvalid[rg] ? *reinterpret_cast<const half8_t*>(p.q + ((size_t)m[rg] * p.Hq + h[rg]) * DP + 32 * kk + 8 * q4)
+                             : half8_t{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (f16)((float)v[j] * 1.4426950408889634f);
+      qf[rg][kk] = v;
+    }
 
   // page staging: thread owns K chunks (key = c / (DP/8), d8 = c % (DP/8)) and V^T chunks
-  // (d = c / 8, k8 = c % 8), c = tid + 512 j
+  // (d = c / 8, k8 = c % 8), c = tid + NT j
   u32x4 kr[KCH], vr[KCH];
   auto load_page = [&](int kt) {
     const int page = bt[kt];
@@ -73,7 +90,7 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
     const f16* vb = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
 #pragma unroll
     for (int j = 0; j < KCH; ++j) {
-      const int c = tid + NW * 64 * j;
+      const int c = tid + NT * j;
       kr[j] = *reinterpret_cast<const u32x4*>(kb + (size_t)c * 8);
       vr[j] = *reinterpret_cast<const u32x4*>(vb + (size_t)c * 8);
     }
@@ -81,16 +98,21 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
   auto store_page = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < KCH; ++j) {
-      const int c = tid + NW * 64 * j;
+      const int c = tid + NT * j;
       *reinterpret_cast<u32x4*>(&ks[buf][(c / (DP / 8)) * KLD + (c % (DP / 8)) * 8]) = kr[j];
       *reinterpret_cast<u32x4*>(&vs[buf][(c / 8) * VLD + (c % 8) * 8]) = vr[j];
     }
   };
 
-  f32x4 o[DT];
+  f32x4 o[RG][DT];
+  float m_run[RG], l_run[RG];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  for (int rg = 0; rg < RG; ++rg) {
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[rg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run[rg] = -INFINITY;
+    l_run[rg] = 0.f;
+  }
   const int krow0 = 8 * (col >> 2) + (col & 3);   // pi(c, R) - 4c
 
   if (n_kt > 0) {
@@ -106,47 +128,60 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       const int P0 = (kt0 + kt) * 64 + kc * 32;
-      f32x4 s[2];
+      f32x4 s[RG][2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) s[rg][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) {
           const half8_t kf = *reinterpret_cast<const half8_t*>(kt_s + (32 * kc + krow0 + 4 * c) * KLD + 32 * kk + 8 * q4);
-          a = mfma16x16x32(kf, qf[kk], a);
+#pragma unroll
+          for (int rg = 0; rg < RG; ++rg) s[rg][c] = mfma16x16x32(kf, qf[rg][kk], s[rg][c]);
         }
-        s[c] = a;
       }
-      // lane holds scores of row `col` for keys P0 + 8 q4 + 4c + i
-      float mx = -INFINITY;
+      half8_t pf[RG];
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int rg = 0; rg < RG; ++rg) {
+        // lane holds scores of row `col` (row group rg) for keys P0 + 8 q4 + 4c + i
+        float mx = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float v = P0 + 8 * q4 + 4 * c + i <= my_pos ? s[c][i] : -INFINITY;
-          s[c][i] = v;
-          mx = fmaxf(mx, v);
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = P0 + 8 * q4 + 4 * c + i <= my_pos[rg] ? s[rg][c][i] : -INFINITY;
+            s[rg][c][i] = v;
+            mx = fmaxf(mx, v);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        // lazy rescale: the running max only moves when a score exceeds it by > 8 (2^8: P stays
+        // far inside f16 range), so the O^T rescale (DT x 4 multiplies) is skipped on most chunks
+        const bool resc = mx > m_run[rg] + 8.f;
+        if (__any(resc)) {
+          const float m_new = resc ? mx : m_run[rg];
+          const float alpha = m_run[rg] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run[rg] - m_new);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[rg][dt] *= alpha;
+          l_run[rg] *= alpha;
+          m_run[rg] = m_new;
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = m_new == -INFINITY ? 1.f : __expf(m_run - m_new);
-      float psum = 0.f;
-      half8_t pf;
+        float psum = 0.f;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = m_new == -INFINITY ? 0.f : __expf(s[c][i] - m_new);
-          psum += e;
-          pf[4 * c + i] = (f16)e;
-        }
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
+          for (int i = 0; i < 4; ++i) {
+            const float e = m_run[rg] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[rg][c][i] - m_run[rg]);
+            psum += e;
+            pf[rg][4 * c + i] = (f16)e;
+          }
+        l_run[rg] += psum;
+      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const half8_t vf = *reinterpret_cast<const half8_t*>(vt_s + (16 * dt + col) * VLD + 32 * kc + 8 * q4);
-        o[dt] = mfma16x16x32(vf, pf, o[dt] * alpha);
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) o[rg][dt] = mfma16x16x32(vf, pf[rg], o[rg][dt]);
       }
     }
     if (kt + 1 < n_kt) {
@@ -155,35 +190,40 @@ __global__ __launch_bounds__(512) void attn_prefill_kernel(const PrefillAttnPara
       if (kt + 2 < n_kt) load_page(kt0 + kt + 2);
     }
   }
-  l_run += __shfl_xor(l_run, 16);
-  l_run += __shfl_xor(l_run, 32);
-  if (!rvalid) return;
-  if (p.n_split > 1) {   // unnormalised partials, the attn_combine layout [z][m * Hq + h][Dp]
-    const size_t rid = (size_t)m * p.Hq + h, stride = (size_t)p.M * p.Hq;
-    float* op = p.o_part + ((size_t)z * stride + rid) * DP;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-      *reinterpret_cast<float4*>(op + 16 * dt + 4 * q4) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
-    if (q4 == 0) {
-      float* ml = p.ml_part + ((size_t)z * stride + rid) * 2;
-      ml[0] = n_kt > 0 ? m_run : -INFINITY;
-      ml[1] = n_kt > 0 ? l_run : 0.f;
+  for (int rg = 0; rg < RG; ++rg) {
+    float l = l_run[rg];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
+    if (!rvalid[rg]) continue;
+    if (p.n_split > 1) {   // unnormalised partials, the attn_combine layout [z][m * Hq + h][Dp]
+      const size_t rid = (size_t)m[rg] * p.Hq + h[rg], stride = (size_t)p.M * p.Hq;
+      float* op = p.o_part + ((size_t)z * stride + rid) * DP;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+        *reinterpret_cast<float4*>(op + 16 * dt + 4 * q4) =
+            make_float4(o[rg][dt][0], o[rg][dt][1], o[rg][dt][2], o[rg][dt][3]);
+      if (q4 == 0) {
+        float* ml = p.ml_part + ((size_t)z * stride + rid) * 2;
+        ml[0] = n_kt > 0 && m_run[rg] != -INFINITY ? m_run[rg] * 0.6931471805599453f : -INFINITY;   // natural log
+        ml[1] = n_kt > 0 ? l : 0.f;
+      }
+      continue;
     }
-    return;
-  }
-  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  f16* orow = p.out + (size_t)m * p.ldo + (size_t)h * p.hd;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    f16* orow = p.out + (size_t)m[rg] * p.ldo + (size_t)h[rg] * p.hd;
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    const int d0 = 16 * dt + 4 * q4;   // lane holds O^T[d0 + i][row]
-    if (d0 + 4 <= p.hd) {
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<h4*>(orow + d0) = h4{(f16)(o[dt][0] * inv), (f16)(o[dt][1] * inv), (f16)(o[dt][2] * inv),
-                                             (f16)(o[dt][3] * inv)};
-    } else {
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d0 = 16 * dt + 4 * q4;   // lane holds O^T[d0 + i][row]
+      if (d0 + 4 <= p.hd) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<h4*>(orow + d0) = h4{(f16)(o[rg][dt][0] * inv), (f16)(o[rg][dt][1] * inv),
+                                               (f16)(o[rg][dt][2] * inv), (f16)(o[rg][dt][3] * inv)};
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (d0 + i < p.hd) orow[d0 + i] = (f16)(o[dt][i] * inv);
+        for (int i = 0; i < 4; ++i)
+          if (d0 + i < p.hd) orow[d0 + i] = (f16)(o[rg][dt][i] * inv);
+      }
     }
   }
 }
@@ -202,10 +242,17 @@ void launch_attn_prefill(const PrefillAttnParams& p, hipStream_t st) {
   if (p.Hq % p.Hkv || p.Hq / p.Hkv > 128) throw std::runtime_error("launch_attn_prefill: bad GQA group");
   if (p.n_split > 1 && (!p.o_part || !p.ml_part || p.split_pages < 1))
     throw std::runtime_error("launch_attn_prefill: split without partial buffers");
-  const dim3 grid(p.n_tiles, p.Hkv, std::max(1, p.n_split)), block(512);
-  if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_prefill_kernel<128>, grid, block, 0, st, p);
-  else if (p.Dp == 64) hipLaunchKernelGGL(mpk::attn_prefill_kernel<64>, grid, block, 0, st, p);
-  else throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
+  // MIPIPE_PF_RG=1: one row group per wave (8 waves), the A/B reference of the default RG = 2
+  static const int rg = [] { const char* e = getenv("MIPIPE_PF_RG"); return e && atoi(e) == 1 ? 1 : 2; }();
+  const dim3 grid(p.n_tiles, p.Hkv, std::max(1, p.n_split));
+  if (p.Dp != 128 && p.Dp != 64) throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
+  if (rg == 1) {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1>), grid, dim3(512), 0, st, p);
+  } else {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 4, 2>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 4, 2>), grid, dim3(256), 0, st, p);
+  }
   if (p.n_split > 1) {   // LSE merge of the splits into out (attention.hip)
     AttnParams a{};
     a.M = p.M; a.Hq = p.Hq; a.hd = p.hd; a.Dp = p.Dp; a.n_split = p.n_split;
