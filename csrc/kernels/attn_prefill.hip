@@ -21,15 +21,15 @@
 #include "../runtime/kernels_api.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <stdexcept>
 
 namespace mpk {
 using namespace mp;
 
-// NW waves x RG row groups of 16 MFMA rows = 128 rows per workgroup.  RG = 2: every K / V^T
-// fragment read from LDS feeds two MFMAs (one per row group): with one row group per wave the
-// 16 ds_read_b128 per 32-key chunk kept the CU's LDS as busy as its matrix pipes.
+// NW waves x RG row groups of 16 MFMA rows = 128 rows per workgroup.  RG = 2 (every K / V^T
+// fragment read from LDS feeding two MFMAs, 4 waves) took 260 us per 8B 32K-prompt layer chunk
+// against 184 us for RG = 1 with 8 waves (190 vs 119 VGPRs: half the waves per SIMD;
+// profiles/r2n_prof_8b_32k_rg*.txt), so the launcher instantiates RG = 1.
 template <int DP, int NW, int RG>
 __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttnParams p) {
   constexpr int KK = DP / 32;    // k-steps of S^T over d
@@ -121,10 +121,12 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttn
     __syncthreads();
     if (n_kt > 1) load_page(kt0 + 1);
   }
+  const int pmin = p.pos[m0];               // the tile's first (smallest) position
   for (int kt = 0; kt < n_kt; ++kt) {
     const int buf = kt & 1;
     const f16* kt_s = ks[buf];
     const f16* vt_s = vs[buf];
+    const bool full = (kt0 + kt) * 64 + 63 <= pmin;   // every key of the page is visible to every row
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       const int P0 = (kt0 + kt) * 64 + kc * 32;
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttn
         for (int c = 0; c < 2; ++c)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float v = P0 + 8 * q4 + 4 * c + i <= my_pos[rg] ? s[rg][c][i] : -INFINITY;
+            const float v = full || P0 + 8 * q4 + 4 * c + i <= my_pos[rg] ? s[rg][c][i] : -INFINITY;
             s[rg][c][i] = v;
             mx = fmaxf(mx, v);
           }
@@ -167,11 +169,12 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttn
           m_run[rg] = m_new;
         }
         float psum = 0.f;
+        const float mb = m_run[rg] == -INFINITY ? 0.f : m_run[rg];   // all scores -inf then: 2^-inf = 0
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float e = m_run[rg] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[rg][c][i] - m_run[rg]);
+            const float e = __builtin_amdgcn_exp2f(s[rg][c][i] - mb);
             psum += e;
             pf[rg][4 * c + i] = (f16)e;
           }
@@ -242,17 +245,10 @@ void launch_attn_prefill(const PrefillAttnParams& p, hipStream_t st) {
   if (p.Hq % p.Hkv || p.Hq / p.Hkv > 128) throw std::runtime_error("launch_attn_prefill: bad GQA group");
   if (p.n_split > 1 && (!p.o_part || !p.ml_part || p.split_pages < 1))
     throw std::runtime_error("launch_attn_prefill: split without partial buffers");
-  // MIPIPE_PF_RG=1: one row group per wave (8 waves), the A/B reference of the default RG = 2
-  static const int rg = [] { const char* e = getenv("MIPIPE_PF_RG"); return e && atoi(e) == 1 ? 1 : 2; }();
   const dim3 grid(p.n_tiles, p.Hkv, std::max(1, p.n_split));
-  if (p.Dp != 128 && p.Dp != 64) throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
-  if (rg == 1) {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1>), grid, dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1>), grid, dim3(512), 0, st, p);
-  } else {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 4, 2>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 4, 2>), grid, dim3(256), 0, st, p);
-  }
+  if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1>), grid, dim3(512), 0, st, p);
+  else if (p.Dp == 64) hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1>), grid, dim3(512), 0, st, p);
+  else throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
   if (p.n_split > 1) {   // LSE merge of the splits into out (attention.hip)
     AttnParams a{};
     a.M = p.M; a.Hq = p.Hq; a.hd = p.hd; a.Dp = p.Dp; a.n_split = p.n_split;

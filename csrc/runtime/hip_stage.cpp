@@ -1,5 +1,8 @@
 #include "hip_stage.h"
 
+#include <chrono>
+#include <cstring>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
@@ -72,15 +75,70 @@ float* HipStage::upload_f32(const float* h, size_t n) {
   return d;
 }
 
+// ---- weight upload (load_gguf): T16 packing on host threads into pinned double-buffered staging,
+// hipMemcpyAsync on a dedicated stream, so packing piece i+1 overlaps the DMA of piece i (v1
+// packed into pageable memory and then blocked in a synchronous hipMemcpy per tensor)
+void HipStage::stage_begin() {
+  if (stg_.buf[0]) return;
+  stg_.cap = (size_t)256 << 20;
+  for (int b = 0; b < 2; ++b) {
+    HIP_OK(hipHostMalloc((void**)&stg_.buf[b], stg_.cap, hipHostMallocDefault));
+    HIP_OK(hipEventCreateWithFlags(&stg_.ev[b], hipEventDisableTiming));
+    stg_.busy[b] = false;
+  }
+  HIP_OK(hipStreamCreateWithFlags(&stg_.st, hipStreamNonBlocking));
+  stg_.cur = 0;
+  stg_.bytes = 0;
+  stg_.t0 = std::chrono::steady_clock::now();
+}
+
+void HipStage::stage_end() {
+  if (!stg_.buf[0]) return;
+  HIP_OK(hipStreamSynchronize(stg_.st));
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - stg_.t0).count();
+  upload_gbps_ = s > 0 ? stg_.bytes / s / 1e9 : 0.0;
+  MP_LOGI("stage %d: uploaded %.2f GiB of packed weights in %.2f s (%.2f GB/s incl. packing)", spec_.stage,
+          stg_.bytes / 1073741824.0, s, upload_gbps_);
+  for (int b = 0; b < 2; ++b) {
+    HIP_OK(hipEventDestroy(stg_.ev[b]));
+    HIP_OK(hipHostFree(stg_.buf[b]));
+    stg_.buf[b] = nullptr;
+  }
+  HIP_OK(hipStreamDestroy(stg_.st));
+  stg_.st = nullptr;
+}
+
+// dst[0, bytes) <- fill(host, off, n) piece by piece through the staging buffers
+void HipStage::stage_put(uint8_t* dst, size_t bytes, size_t granule,
+                         const std::function<void(uint8_t*, size_t, size_t)>& fill) {
+  const bool own = !stg_.buf[0];
+  if (own) stage_begin();
+  const size_t piece = std::max(granule, stg_.cap / granule * granule);
+  if (piece > stg_.cap) throw std::runtime_error("stage_put: granule larger than the staging buffer");
+  for (size_t off = 0; off < bytes; off += piece) {
+    const size_t n = std::min(piece, bytes - off);
+    const int b = stg_.cur;
+    if (stg_.busy[b]) HIP_OK(hipEventSynchronize(stg_.ev[b]));   // its previous DMA has drained
+    fill(stg_.buf[b], off, n);
+    HIP_OK(hipMemcpyAsync(dst + off, stg_.buf[b], n, hipMemcpyHostToDevice, stg_.st));
+    HIP_OK(hipEventRecord(stg_.ev[b], stg_.st));
+    stg_.busy[b] = true;
+    stg_.cur ^= 1;
+    stg_.bytes += n;
+  }
+  if (own) stage_end();
+}
+
 PackedMat HipStage::upload_packed(int t, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row) {
   PackedMat m;
   m.ptype = pack_type_of(t);
   if (m.ptype < 0) throw std::runtime_error(std::string("unsupported weight type ") + type_name(t));
   m.dims = packed_dims(m.ptype, N, K);
-  std::vector<uint8_t> host(m.dims.bytes);
-  pack_t16(t, N, K, row, host.data());
   m.d = (uint8_t*)dmalloc(m.dims.bytes);
-  HIP_OK(hipMemcpy(m.d, host.data(), m.dims.bytes, hipMemcpyHostToDevice));
+  const size_t tile_b = (size_t)m.dims.nsb * chunk_bytes(m.ptype);
+  stage_put(m.d, m.dims.bytes, tile_b, [&](uint8_t* h, size_t off, size_t n) {
+    pack_t16_tiles(t, N, K, row, h, (int64_t)(off / tile_b), (int64_t)((off + n) / tile_b));
+  });
   weight_bytes_ += m.dims.bytes;
   return m;
 }
@@ -92,12 +150,13 @@ PackedMat HipStage::upload_packed_experts(int t, int E, int64_t N, int64_t K, si
   if (m.ptype < 0) throw std::runtime_error(std::string("unsupported expert type ") + type_name(t));
   m.dims = packed_dims(m.ptype, N, K);
   *stride = m.dims.bytes;
-  std::vector<uint8_t> host(m.dims.bytes);
   m.d = (uint8_t*)dmalloc(m.dims.bytes * E);
-  for (int e = 0; e < E; ++e) {
-    pack_t16(t, N, K, [&](int64_t n) { return row(e, n); }, host.data());
-    HIP_OK(hipMemcpy(m.d + (size_t)e * m.dims.bytes, host.data(), m.dims.bytes, hipMemcpyHostToDevice));
-  }
+  const size_t tile_b = (size_t)m.dims.nsb * chunk_bytes(m.ptype);
+  for (int e = 0; e < E; ++e)
+    stage_put(m.d + (size_t)e * m.dims.bytes, m.dims.bytes, tile_b, [&](uint8_t* h, size_t off, size_t n) {
+      pack_t16_tiles(t, N, K, [&](int64_t r) { return row(e, r); }, h, (int64_t)(off / tile_b),
+                     (int64_t)((off + n) / tile_b));
+    });
   weight_bytes_ += m.dims.bytes * E;
   return m;
 }
@@ -122,6 +181,7 @@ static std::vector<float> tensor_f32(const GgufTensor& t) {
 
 void HipStage::load_gguf(const GgufFile& f) {
   HIP_OK(hipSetDevice(spec_.device));
+  stage_begin();
   auto need = [&](const std::string& n) -> const GgufTensor& {
     const GgufTensor* t = f.tensor(n);
     if (!t) throw std::runtime_error("missing tensor " + n);
@@ -248,7 +308,7 @@ void HipStage::load_gguf(const GgufFile& f) {
     embd_type_ = te.type;
     embd_row_bytes_ = row_bytes(te.type, te.ne[0]);
     embd_raw_ = (uint8_t*)dmalloc(te.nbytes);
-    HIP_OK(hipMemcpy(embd_raw_, te.data, te.nbytes, hipMemcpyHostToDevice));
+    stage_put(embd_raw_, te.nbytes, 1, [&](uint8_t* h, size_t off, size_t n) { std::memcpy(h, te.data + off, n); });
     weight_bytes_ += te.nbytes;
   }
   if (spec_.last()) {
@@ -259,6 +319,7 @@ void HipStage::load_gguf(const GgufFile& f) {
   }
   rope_ff_.clear();
   if (const GgufTensor* rf = f.tensor("rope_freqs.weight")) rope_ff_ = tensor_f32(*rf);
+  stage_end();
   HIP_OK(hipDeviceSynchronize());
 }
 

@@ -8,6 +8,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "kernels_api.h"
@@ -132,6 +133,20 @@ class HipStage : public Stage {
             const GemvParams* extras = nullptr);
   void head(int mb, int M, const float* x, int32_t* tok_out, uint64_t salt, hipStream_t st);
   void ensure_hist();
+  // pinned double-buffered weight staging (load_gguf)
+  struct Staging {
+    uint8_t* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    size_t cap = 0, bytes = 0;
+    int cur = 0;
+    hipStream_t st = nullptr;
+    std::chrono::steady_clock::time_point t0;
+  } stg_;
+  double upload_gbps_ = 0;
+  void stage_begin();
+  void stage_end();
+  void stage_put(uint8_t* dst, size_t bytes, size_t granule, const std::function<void(uint8_t*, size_t, size_t)>& fill);
   PackedMat upload_packed(int ggml_type, int64_t N, int64_t K, const std::function<const uint8_t*(int64_t)>& row);
   // E matrices of N x K packed back to back (MoE experts); row(e, n)
   PackedMat upload_packed_experts(int ggml_type, int E, int64_t N, int64_t K, size_t* stride,

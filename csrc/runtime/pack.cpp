@@ -165,11 +165,21 @@ static void pack_chunk(int t, int pt, const uint8_t* src, int64_t K, int64_t k0,
 int pack_t16(int t, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, int n_threads) {
   const int pt = pack_type_of(t);
   if (pt < 0) throw std::runtime_error(std::string("pack: unsupported ggml type ") + type_name(t));
+  return pack_t16_tiles(t, N, K, row, dst, 0, packed_dims(pt, N, K).ntiles, n_threads);
+}
+
+// tiles [tile0, tile1) of the T16 image (tile-major, so the range is one contiguous byte run
+// starting at tile0 * nsb * chunk_bytes) into dst
+int pack_t16_tiles(int t, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, int64_t tile0, int64_t tile1,
+                   int n_threads) {
+  const int pt = pack_type_of(t);
+  if (pt < 0) throw std::runtime_error(std::string("pack: unsupported ggml type ") + type_name(t));
   const PackedDims d = packed_dims(pt, N, K);
   const int cb = chunk_bytes(pt);
   const int be = block_elems(t), bb = block_bytes(t);
   if (K % be) throw std::runtime_error("pack: K not a block multiple");
-  std::memset(dst, 0, d.bytes);
+  if (tile0 < 0 || tile1 > d.ntiles || tile0 > tile1) throw std::runtime_error("pack: bad tile range");
+  std::memset(dst, 0, (size_t)(tile1 - tile0) * d.nsb * cb);
   auto work = [&](int64_t t0, int64_t t1) {
     for (int64_t tile = t0; tile < t1; ++tile) {
       for (int r = 0; r < 16; ++r) {
@@ -179,21 +189,22 @@ int pack_t16(int t, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, int n_
         if (!src) continue;
         for (int64_t sb = 0; sb < d.nsb; ++sb) {
           const int64_t k0 = sb * 256;
-          uint8_t* chunk = dst + (size_t)(tile * d.nsb + sb) * cb;
+          uint8_t* chunk = dst + (size_t)((tile - tile0) * d.nsb + sb) * cb;
           const uint8_t* s = src + (size_t)(k0 / be) * bb;
           pack_chunk(t, pt, s, K, k0, chunk, r);
         }
       }
     }
   };
+  const int64_t nt = tile1 - tile0;
   if (n_threads <= 0) n_threads = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-  if (d.ntiles < 64 || n_threads == 1) {
-    work(0, d.ntiles);
+  if (nt < 64 || n_threads == 1) {
+    work(tile0, tile1);
   } else {
     std::vector<std::thread> th;
-    const int64_t per = (d.ntiles + n_threads - 1) / n_threads;
+    const int64_t per = (nt + n_threads - 1) / n_threads;
     for (int i = 0; i < n_threads; ++i) {
-      const int64_t a = i * per, b = std::min<int64_t>(d.ntiles, a + per);
+      const int64_t a = tile0 + i * per, b = std::min<int64_t>(tile1, a + per);
       if (a < b) th.emplace_back(work, a, b);
     }
     for (auto& x : th) x.join();

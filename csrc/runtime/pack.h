@@ -14,6 +14,9 @@ using RowFn = std::function<const uint8_t*(int64_t n)>;
 // Pack N x K (ggml row-major, row = output feature) into dst (packed_dims(...).bytes bytes).
 // Multi-threaded over tiles.  Returns the packed type (PackType).
 int pack_t16(int ggml_type, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, int n_threads = 0);
+// tiles [tile0, tile1) only (a contiguous byte range of the tile-major image), into dst
+int pack_t16_tiles(int ggml_type, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, int64_t tile0, int64_t tile1,
+                   int n_threads = 0);
 
 // Row n of the gate/up interleaved matrix (2F rows): tile t rows 0-7 = gate rows 8t..8t+7,
 // rows 8-15 = up rows 8t..8t+7.
