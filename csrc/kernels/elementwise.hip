@@ -293,6 +293,16 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restric
   Y[(size_t)t * ldy + j] = acc;
 }
 
+// device probe (probe.cpp): stream a buffer with 16 B loads, one partial sum per workgroup
+__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restrict__ buf, size_t n16, float* out) {
+  uint32_t acc = 0;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+    const u32x4 v = __builtin_nontemporal_load(buf + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) out[blockIdx.x] = (float)acc;   // keeps the loads; practically never stores
+}
+
 __global__ void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
   const int i = threadIdx.x;
   if (i < M) { const int p = pos[i] + 1; pos[i] = p; kvlen[i] = p + 1; }
@@ -394,6 +404,11 @@ void launch_splitk_reduce(const float* part, int nsplit, int64_t split_stride, i
 
 void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, float* Y, int ldy, hipStream_t st) {
   hipLaunchKernelGGL(mpk::moe_combine_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, Yslot, ld_slot, k, n, Y, ldy);
+}
+
+void launch_stream_read(const void* buf, size_t bytes, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::stream_read_kernel, dim3(4096), dim3(256), 0, st, reinterpret_cast<const u32x4*>(buf),
+                     bytes / 16, out);
 }
 
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {

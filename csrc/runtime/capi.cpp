@@ -10,6 +10,7 @@
 #include <string>
 
 #include "engine.h"
+#include "probe.h"
 #include "model.h"
 #include "gguf.h"
 #include "hip_stage.h"
@@ -552,6 +553,17 @@ const char* mp_plan_partition(const char* cfg) {
   API_CATCH(nullptr)
 }
 // multi-process rendezvous helpers: unique id bytes for RCCL
+// Halda-style device profile (probe.h): out[0] HBM read GB/s, out[1] Q4_K decode GEMV GB/s;
+// device < 0: the host (CPU backend)
+int mp_device_probe(int device, double* out2) {
+  API_TRY
+  const DeviceProfile d = device < 0 ? probe_host() : probe_device(device);
+  out2[0] = d.hbm_read_gbps;
+  out2[1] = d.gemv_gbps;
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_rccl_unique_id(uint8_t* out128) {
   API_TRY
   return rccl_unique_id(out128);

@@ -1,4 +1,5 @@
 #include "engine.h"
+#include "probe.h"
 
 #include <algorithm>
 #include <chrono>
@@ -125,10 +126,6 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   } else {
     S_ = std::max(1, j.get_int("stages", 1));
   }
-  std::vector<double> speed(S_, 1.0);
-  if (j.has("device_speed"))
-    for (int s = 0; s < S_ && s < (int)j["device_speed"].arr().size(); ++s) speed[s] = j["device_speed"].arr()[s].num();
-  specs_ = partition_layers(layer_cost, embd_cost, head_cost, speed, parse_split_mode(j.get_str("split", "cost")));
   std::vector<int> devices(S_);
   for (int s = 0; s < S_; ++s) devices[s] = s;
   if (j.has("devices")) {
@@ -136,6 +133,27 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     for (int s = 0; s < S_; ++s) devices[s] = (int)a[s % a.size()].num();
   }
   if (mode_ == "mp") devices[rank_] = j.get_int("device", devices[rank_]);
+  // per-stage speed for the cost partitioner: given (device_speed: [..]), or measured
+  // (device_speed: "probe", Halda-style; mp mode: every rank must pass the same list, which
+  // mipipe.parallel.init_from_torchrun(device_speed="probe") gathers over torch.distributed)
+  std::vector<double> speed(S_, 1.0);
+  if (j.has("device_speed") && j["device_speed"].is_str()) {
+    if (j["device_speed"].str() != "probe") throw std::runtime_error("device_speed: a list or \"probe\"");
+    if (mode_ == "mp") throw std::runtime_error("device_speed probe in mp mode: gather the list across ranks first");
+    std::map<int, DeviceProfile> seen;
+    for (int s = 0; s < S_; ++s) {
+      if (!seen.count(devices[s])) seen[devices[s]] = cpu_ ? probe_host() : probe_device(devices[s]);
+      speed[s] = seen[devices[s]].speed();
+    }
+    // stages sharing one device (single-GPU emulation) split its speed
+    std::map<int, int> share;
+    for (int s = 0; s < S_; ++s) share[devices[s]]++;
+    for (int s = 0; s < S_; ++s) speed[s] /= share[devices[s]];
+  } else if (j.has("device_speed")) {
+    for (int s = 0; s < S_ && s < (int)j["device_speed"].arr().size(); ++s) speed[s] = j["device_speed"].arr()[s].num();
+  }
+  device_speed_ = speed;
+  specs_ = partition_layers(layer_cost, embd_cost, head_cost, speed, parse_split_mode(j.get_str("split", "cost")));
   for (int s = 0; s < S_; ++s) specs_[s].device = devices[s];
   // --gpu-mem (prima.cpp): per-GPU memory budget in GiB; caps the auto KV sizing and
   // is checked against every stage's weights + KV below (--force downgrades the failure to a warning)
@@ -682,6 +700,7 @@ void Engine::run_all(const std::vector<Item>& items) {
       run_items(*workers_[0], items);
     } catch (...) {
       failed_ = true;
+      failed_stage_ = workers_[0]->stage->spec().stage;
       for (auto& l : links_) l->abort();
       throw;
     }
@@ -703,6 +722,7 @@ void Engine::run_all(const std::vector<Item>& items) {
     for (auto& t : th) t.join();
     if (first_err >= 0) {
       failed_ = true;
+      failed_stage_ = workers_[first_err]->stage->spec().stage;
       std::rethrow_exception(errs[first_err]);
     }
   }
@@ -774,6 +794,10 @@ Json Engine::health() const {
   Json j = Json::object();
   j["ok"] = !failed_;
   j["prefix_reused_tokens"] = (int64_t)reused_tokens_;
+  if (failed_stage_ >= 0) {
+    j["failed_stage"] = failed_stage_;
+    j["failed_device"] = specs_[failed_stage_].device;
+  }
   Json st = Json::array();
   for (auto& w : workers_) {
     Json o = Json::object();
@@ -794,6 +818,38 @@ Json Engine::health() const {
 // message) would otherwise hang hipStreamSynchronize on a posted receive forever.  After
 // `watchdog_s` without completion the links are aborted (ncclCommAbort for RCCL) and the
 // engine reports the stall.
+// Failover (the reference design's auto-healing workers, PDF pp.6-7 §5.2-5.3):
+// the config of an engine rebuilt WITHOUT the failed stage's device -- one stage fewer, the layers
+// re-partitioned over the survivors by the same cost model; a single-stage engine is rebuilt in place.
+Json Engine::failover_config(const Json& cfg, const Json& health) {
+  Json c = cfg;
+  c["fault"] = Json::object();   // an injected fault does not follow the engine across a rebuild
+  const int S = cfg.get_int("stages", 1);
+  if (!health.has("failed_stage") || S <= 1 || cfg.get_str("mode", "local") == "mp") return c;
+  const int bad = health.get_int("failed_stage", 0);
+  Json devs = Json::array();
+  if (cfg.has("devices") && cfg["devices"].is_arr() && !cfg["devices"].arr().empty()) {
+    const auto& a = cfg["devices"].arr();
+    for (int s = 0; s < S; ++s)
+      if (s != bad) devs.push(a[s % a.size()]);
+  } else {
+    for (int s = 0; s < S; ++s)
+      if (s != bad) devs.push(Json((double)s));
+  }
+  c["stages"] = S - 1;
+  c["devices"] = devs;
+  if (cfg.has("device_speed") && cfg["device_speed"].is_arr()) {
+    Json sp = Json::array();
+    const auto& a = cfg["device_speed"].arr();
+    for (int s = 0; s < S && s < (int)a.size(); ++s)
+      if (s != bad) sp.push(a[s]);
+    c["device_speed"] = sp;
+  }
+  MP_LOGW("failover: stage %d (device %d) lost; re-partitioning over %d stage(s)", bad,
+          health.get_int("failed_device", -1), S - 1);
+  return c;
+}
+
 void Engine::sync_all() {
   if (cpu_) return;
   const double deadline = now_ms() + watchdog_s_ * 1e3;
@@ -806,6 +862,7 @@ void Engine::sync_all() {
         if (e != hipErrorNotReady) HIP_OK(e);
         if (now_ms() > deadline) {
           failed_ = true;
+          failed_stage_ = w->stage->spec().stage;
           for (auto& l : links_) l->abort();
           throw std::runtime_error("pipeline watchdog: stage " + std::to_string(w->stage->spec().stage) +
                                    " made no progress for " + std::to_string((int)watchdog_s_) +
@@ -1513,6 +1570,11 @@ Json Engine::info() const {
   j["mb_size"] = B_;
   j["max_ctx"] = max_ctx_;
   j["kv_pages"] = kv_pages_;
+  {
+    Json ds = Json::array();
+    for (double v : device_speed_) ds.push(v);
+    j["device_speed"] = ds;
+  }
   j["kv_free_pages"] = pager_.free_pages();
   j["mode"] = mode_;
   j["backend"] = cpu_ ? "cpu" : "hip";

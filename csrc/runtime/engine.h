@@ -59,6 +59,9 @@ class Engine {
   int mb_size() const { return B_; }
   int max_ctx() const { return max_ctx_; }
   int kv_pages() const { return kv_pages_; }
+  // config of a replacement engine after a fault: the failed stage's device dropped, layers
+  // re-partitioned over the survivors (see engine.cpp)
+  static Json failover_config(const Json& cfg, const Json& health);
   int kv_free_pages() const { return pager_.free_pages(); }
   double load_ms() const { return load_ms_; }
   bool owns_last() const;
@@ -179,6 +182,8 @@ class Engine {
   std::vector<char> active_;
   KvPager pager_;            // paged KV: one logical table, installed on every stage
   int kv_pages_ = 0;         // pool pages per stage
+  std::vector<double> device_speed_;
+  int failed_stage_ = -1;    // stage whose worker raised the fault (health()["failed_stage"])   // partitioner weights per stage (given or probed)
   void kv_grant(size_t slot, int n_tokens);   // throws when the pool is exhausted
   void kv_sync();            // push a changed table to the stages (between engine calls)
   int slot_pos(size_t i) const {

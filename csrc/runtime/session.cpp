@@ -32,7 +32,7 @@ std::string Utf8Acc::push(const std::string& b) {
   return o;
 }
 
-Session::Session(Engine& eng, const std::string& gguf_path) : eng_(eng) {
+Session::Session(Engine& eng, const std::string& gguf_path) : eng_(&eng) {
   if (!gguf_path.empty()) {
     gguf_.reset(new GgufFile(gguf_path));
     if (gguf_->get("tokenizer.ggml.tokens")) tok_.reset(new Tokenizer(Tokenizer::from_gguf(*gguf_)));
@@ -45,7 +45,7 @@ Session::~Session() = default;
 std::vector<int32_t> Session::encode(const std::string& text) const {
   if (tok_) return tok_->encode(text, tok_->add_bos_default(), true);
   std::vector<int32_t> o{1};
-  const int V = eng_.model().vocab;
+  const int V = eng_->model().vocab;
   for (unsigned char c : text) o.push_back((int32_t)((c + 3) % V));
   return o;
 }
@@ -61,7 +61,7 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
   if ((int)reqs.size() > capacity()) throw std::runtime_error("more requests than sequence slots");
   std::vector<GenResult> res(reqs.size());
   std::vector<std::vector<int32_t>> prompts(reqs.size());
-  const int max_ctx = eng_.max_ctx();
+  const int max_ctx = eng_->max_ctx();
   int max_prompt = 0;
   for (size_t i = 0; i < reqs.size(); ++i) {
     prompts[i] = encode(reqs[i].prompt);
@@ -77,8 +77,8 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
   n_max = std::max(0, std::min(n_max, max_ctx - max_prompt - 1));
   // all ranks of a multi-process pipeline must run the same number of rounds: early stop only
   // when this process owns the whole pipeline
-  const bool early_stop = eng_.owns_first() && eng_.owns_last();
-  const bool emit = eng_.owns_last();
+  const bool early_stop = eng_->owns_first() && eng_->owns_last();
+  const bool emit = eng_->owns_last();
   std::vector<Utf8Acc> acc(reqs.size());
   std::vector<bool> active(reqs.size(), true);
   auto consume = [&](size_t i, int32_t t, int step) {
@@ -93,18 +93,18 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
     if (emit && !p.empty() && reqs[i].on_piece && !reqs[i].on_piece(p)) { active[i] = false; r.stop = "cancelled"; }
   };
   const double t0 = now_ms();
-  const int draft_max = eng_.config().get_int("draft_max", 0);
+  const int draft_max = eng_->config().get_int("draft_max", 0);
   if (draft_max > 0 && early_stop) {
     // speculative decoding by prompt lookup (greedy): tokens arrive in accepted runs per round
     std::vector<int> steps(reqs.size(), 0);
     double t_first = 0;
-    eng_.on_token = [&](int i, int32_t t) { consume((size_t)i, t, steps[i]++); };
-    eng_.keep_going = [&](int i) { return (bool)active[i]; };
-    auto cleanup = [&] { eng_.on_token = nullptr; eng_.keep_going = nullptr; };
+    eng_->on_token = [&](int i, int32_t t) { consume((size_t)i, t, steps[i]++); };
+    eng_->keep_going = [&](int i) { return (bool)active[i]; };
+    auto cleanup = [&] { eng_->on_token = nullptr; eng_->keep_going = nullptr; };
     try {
       std::vector<std::vector<int32_t>> gen;
-      const Json st = eng_.spec_generate(prompts, std::max(1, n_max), draft_max,
-                                         eng_.config().get_int("lookup_ngram", 3), &gen);
+      const Json st = eng_->spec_generate(prompts, std::max(1, n_max), draft_max,
+                                         eng_->config().get_int("lookup_ngram", 3), &gen);
       t_first = t0 + st.get_num("prefill_ms", 0.0);
       MP_LOGI("speculative lookup: %ld verify rounds, %ld/%ld drafted tokens accepted",
               (long)st.get_num("verify_rounds", 0), (long)st.get_num("accepted", 0), (long)st.get_num("drafted", 0));
@@ -126,15 +126,15 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
     }
     return res;
   }
-  eng_.start(prompts);
+  eng_->start(prompts);
   const double t1 = now_ms();
   if (n_max > 0)
-    for (size_t i = 0; i < reqs.size(); ++i) consume(i, eng_.tokens()[i].back(), 0);
+    for (size_t i = 0; i < reqs.size(); ++i) consume(i, eng_->tokens()[i].back(), 0);
   int step = 1;
   auto any_active = [&] { return std::any_of(active.begin(), active.end(), [](bool b) { return b; }); };
   while (step < n_max && (!early_stop || any_active())) {
-    eng_.decode_steps(1);
-    const auto toks = eng_.tokens();
+    eng_->decode_steps(1);
+    const auto toks = eng_->tokens();
     for (size_t i = 0; i < reqs.size(); ++i) consume(i, toks[i].back(), step);
     ++step;
   }
@@ -153,13 +153,14 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
 }
 
 void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
-  if (!eng_.owns_first() || !eng_.owns_last()) throw std::runtime_error("serve: needs every stage in this process");
+  if (!eng_->owns_first() || !eng_->owns_last()) throw std::runtime_error("serve: needs every stage in this process");
   struct Live {
     Served s;
     GenResult res;
     Utf8Acc acc;
     int step = 0;
     int pages = 0;   // KV pages reserved for prompt + n_predict (paged KV admission control)
+    std::vector<int32_t> prompt;   // for re-admission into a replacement engine after a fault
     double t0 = 0, t1 = 0;
   };
   struct Pending {
@@ -167,11 +168,11 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     std::vector<int32_t> prompt;
     int pages = 0;
   };
-  const int cap = capacity(), max_ctx = eng_.max_ctx();
+  const int cap = capacity(), max_ctx = eng_->max_ctx();
   // paged KV (kvpager.h): a request is admitted only when the pool can hold its prompt plus every
   // token it may generate on top of what the running requests may still grow into, so a decode
   // round never runs out of pages; requests that do not fit wait (FIFO) for pages to come back
-  const int pool = eng_.kv_pages();
+  const int pool = eng_->kv_pages();
   int reserved = 0;
   std::deque<Pending> waiting;
   std::vector<std::unique_ptr<Live>> live(cap);
@@ -188,7 +189,7 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     if (!p.empty() && L.s.req.on_piece && !L.s.req.on_piece(p)) { r.stop = "cancelled"; return false; }
     if (L.step >= L.s.req.n_predict) { r.stop = "length"; return false; }
     // the context or the request's share of the KV pool is full
-    if (eng_.slot_position(slot) + 1 >= std::min(max_ctx, L.pages * 64)) { r.stop = "context"; return false; }
+    if (eng_->slot_position(slot) + 1 >= std::min(max_ctx, L.pages * 64)) { r.stop = "context"; return false; }
     return true;
   };
   auto finish = [&](int slot) {
@@ -199,9 +200,41 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     }
     L.res.decode_ms = now_ms() - L.t1;
     if (L.s.done) L.s.done(L.res);
-    eng_.release(slot);
+    eng_->release(slot);
     reserved -= L.pages;
     live[slot].reset();
+  };
+  // runs an engine call; on a pipeline fault with a handler installed, swaps in the replacement
+  // engine and re-admits every live request as prompt + the tokens it has produced (slots 0..n-1),
+  // consuming the re-prefill's token like a normal admission.  false: failed over (skip the rest
+  // of this round); rethrows when there is no handler, the handler gives up or the budget is spent.
+  std::function<bool(const std::function<void()>&)> guarded = [&](const std::function<void()>& call) -> bool {
+    try {
+      call();
+      return true;
+    } catch (const std::exception& e) {
+      if (!on_fault_ || failovers_ >= max_failovers_) throw;
+      Engine* ne = on_fault_(e.what());
+      if (!ne) throw;
+      eng_ = ne;
+      ++failovers_;
+      MP_LOGW("serve: failed over after \"%s\" (%d); re-admitting the running requests", e.what(), failovers_);
+    }
+    std::vector<std::unique_ptr<Live>> moved;
+    for (auto& l : live)
+      if (l) moved.push_back(std::move(l));
+    if (moved.empty()) return false;
+    std::vector<std::vector<int32_t>> prompts;
+    for (size_t i = 0; i < moved.size(); ++i) {
+      std::vector<int32_t> pr = moved[i]->prompt;
+      pr.insert(pr.end(), moved[i]->res.tokens.begin(), moved[i]->res.tokens.end());
+      prompts.push_back(std::move(pr));
+      live[i] = std::move(moved[i]);
+    }
+    eng_->start(prompts);   // a replacement fault propagates (the handler already had its turn)
+    for (size_t i = 0; i < prompts.size(); ++i)
+      if (!consume((int)i, eng_->last_token((int)i))) finish((int)i);
+    return false;
   };
   for (;;) {
     int free = 0;
@@ -228,6 +261,7 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       auto L = std::make_unique<Live>();
       L->res.n_prompt = (int)pd.prompt.size();
       L->pages = pd.pages;
+      L->prompt = pd.prompt;
       L->s = std::move(pd.s);
       L->t0 = now_ms();
       reserved += L->pages;
@@ -237,14 +271,17 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     }
     if (!slots.empty()) {
       // nothing running: a plain start() of slots 0..n-1 (resets the engine's rounds)
-      if (idle && slots.back() == (int)slots.size() - 1) eng_.start(prompts);
-      else eng_.admit(slots, prompts);
+      const bool ok = guarded([&] {
+        if (idle && slots.back() == (int)slots.size() - 1) eng_->start(prompts);
+        else eng_->admit(slots, prompts);
+      });
+      if (!ok) continue;   // failed over: every live request (these included) was re-admitted
       const double t = now_ms();
       for (int sl : slots) {
         Live& L = *live[sl];
         L.t1 = t;
         L.res.prefill_ms = t - L.t0;
-        if (L.s.req.n_predict <= 0 || !consume(sl, eng_.last_token(sl))) finish(sl);
+        if (L.s.req.n_predict <= 0 || !consume(sl, eng_->last_token(sl))) finish(sl);
       }
     }
     bool any = false;
@@ -253,9 +290,9 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       if (waiting.empty() && slots.empty()) return;
       continue;
     }
-    eng_.decode_steps(1);
+    if (!guarded([&] { eng_->decode_steps(1); })) continue;
     for (int sl = 0; sl < cap; ++sl)
-      if (live[sl] && !consume(sl, eng_.last_token(sl))) finish(sl);
+      if (live[sl] && !consume(sl, eng_->last_token(sl))) finish(sl);
   }
 }
 

@@ -40,8 +40,17 @@ class Session {
   // gguf may be empty (synthetic model: byte-level stand-in tokenizer)
   Session(Engine& eng, const std::string& gguf_path);
   ~Session();
-  Engine& engine() { return eng_; }
-  int capacity() const { return eng_.n_mb() * eng_.mb_size(); }
+  Engine& engine() { return *eng_; }
+  int capacity() const { return eng_->n_mb() * eng_->mb_size(); }
+  // Failover for serve(): called with the error of a failed engine call; returns a replacement
+  // engine (e.g. re-partitioned without the failed stage's GPU, Engine::failover_config) or nullptr
+  // to give up.  The running requests are then re-admitted as prompt + tokens generated so far and
+  // keep streaming.  At most `max_failovers` per serve() call.
+  void set_fault_handler(std::function<Engine*(const std::string& error)> h, int max_failovers = 4) {
+    on_fault_ = std::move(h);
+    max_failovers_ = max_failovers;
+  }
+  int failovers() const { return failovers_; }
   std::vector<int32_t> encode(const std::string& text) const;
   std::string piece(int32_t id) const;
   bool is_eog(int32_t id) const;
@@ -62,7 +71,9 @@ class Session {
   static std::string perf_summary(const GenResult& r, double load_ms);
 
  private:
-  Engine& eng_;
+  Engine* eng_;
+  std::function<Engine*(const std::string&)> on_fault_;
+  int max_failovers_ = 0, failovers_ = 0;
   std::unique_ptr<GgufFile> gguf_;
   std::unique_ptr<Tokenizer> tok_;
 };

@@ -315,6 +315,21 @@ void serve_model(Server& S, ModelSlot* slot, const std::string& model) {
     }
     return out;
   };
+  // failover: a stage fault mid-generation rebuilds the engine without the failed stage's GPU
+  // (layers re-partitioned over the survivors) and the running requests continue on it
+  slot->sess->set_fault_handler([&S, slot](const std::string& err) -> Engine* {
+    if (!slot->eng) return nullptr;
+    const Json cfg2 = Engine::failover_config(slot->cfg, slot->eng->health());
+    MP_LOGW("orchestrator: engine of model %s faulted (%s); failing over", slot->name.c_str(), err.c_str());
+    std::unique_ptr<Engine> e(new Engine(cfg2));
+    std::lock_guard<std::mutex> l(S.eng_mu);
+    const bool dflt = S.eng == slot->eng.get();
+    slot->eng = std::move(e);
+    slot->cfg = cfg2;
+    slot->restarts++;
+    if (dflt) S.eng = slot->eng.get();
+    return slot->eng.get();
+  });
   try {
     slot->sess->serve(next);
   } catch (const std::exception& e) {

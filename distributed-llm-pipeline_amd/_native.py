@@ -56,6 +56,7 @@ _SIGS = {
     "mp_op_attn_prefill": ([c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                             c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                             c_void_p], c_int),
+    "mp_device_probe": ([c_int, c_void_p], c_int),
     "mp_op_gemv_fused": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                           c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_float, c_int, c_void_p, c_void_p,
                           c_void_p, c_int64, c_void_p], c_int),

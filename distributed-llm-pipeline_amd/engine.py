@@ -134,6 +134,14 @@ class Engine:
         return out
 
 
+def device_probe(device: int = 0) -> dict:
+    """Halda-style device profile (probe.h): measured HBM read and Q4_K decode-GEMV bandwidth of a
+    GPU (device < 0: host memcpy bandwidth, the CPU backend's speed)."""
+    out = (ctypes.c_double * 2)()
+    N.check(N.lib().mp_device_probe(int(device), out), "device probe")
+    return {"hbm_read_gbps": out[0], "gemv_gbps": out[1], "speed": out[1] if out[1] > 0 else out[0]}
+
+
 def rccl_unique_id_hex() -> str:
     buf = (ctypes.c_uint8 * 128)()
     N.check(N.lib().mp_rccl_unique_id(buf), "rccl unique id")

@@ -125,6 +125,17 @@ def init_from_torchrun(pp: int | None = None, **cfg):
         cfg.setdefault("stages", 1)
         cfg.setdefault("devices", [local_rank])
         return Engine(**cfg)
+    if cfg.get("device_speed") == "probe":
+        # Halda: every rank measures its own device, the list is gathered so all ranks of the
+        # replica derive the same cost-balanced partition
+        from ..engine import device_probe
+        mine = device_probe(-1 if cpu else local_rank)["speed"]
+        speeds = [None] * world
+        if world > 1:
+            dist.all_gather_object(speeds, mine)
+        else:
+            speeds = [mine]
+        cfg["device_speed"] = speeds[group * pp:(group + 1) * pp]
     cfg.update(mode="mp", world=pp, rank=stage, device=local_rank, link=link)
     if link == "rccl":
         ids = [None] * world

@@ -315,8 +315,9 @@ def test_other_model_not_starved_under_continuous_load(native_bins, model_dir, t
 
 
 def test_engine_restart_after_fault(native_bins, tiny_gguf):
-    """A stage fault fails the request in flight; the orchestrator rebuilds the engine and the next
-    request succeeds (design report worker auto-restart)."""
+    """A stage fault in a single-stage engine: the orchestrator rebuilds the engine in place, the
+    fault is reported on the log stream, the request in flight is re-admitted and the next request
+    succeeds (design report worker auto-restart)."""
     env_fault = json.dumps({"stage": 0, "fail_at": 2})
     port = free_port()
     proc = subprocess.Popen([os.path.join(BIN, "orchestrator"), "--host", "127.0.0.1", "--port", str(port),
@@ -339,6 +340,41 @@ def test_engine_restart_after_fault(native_bins, tiny_gguf):
         assert h["ok"] and h["engine_restarts"] == 1
         ok = httpx.post(url + "/completion", json={"prompt": "abc", "n_predict": 6}, timeout=120).json()
         assert ok["tokens_predicted"] >= 1 and ok["stop_reason"] in ("length", "eog")
+    finally:
+        proc.terminate()
+        proc.wait(timeout=30)
+
+
+def test_failover_repartitions_and_requests_survive(native_bins, tiny_gguf):
+    """A stage of a 2-stage pipeline faults mid-generation: the orchestrator rebuilds the engine on
+    the surviving stage (layers re-partitioned) and the request in flight completes with the text a
+    fault-free run produces (design report auto-healing, PDF pp.6-7)."""
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-c", "256", "-ngl", "0", "--no-display-prompt"]
+    prompt = "The pipeline sends activations"
+    ref = subprocess.run(base + ["-p", prompt, "-n", "40"], capture_output=True, timeout=120).stdout
+    ref = ref.decode("utf-8", errors="replace").rstrip("\n")
+    env_fault = json.dumps({"stage": 1, "fail_at": 25})
+    port = free_port()
+    proc = subprocess.Popen([os.path.join(BIN, "orchestrator"), "--host", "127.0.0.1", "--port", str(port),
+                             "-m", tiny_gguf, "-ngl", "0", "-c", "256", "--stages", "2", "--split", "even",
+                             "--threads", "2"],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                            env={**os.environ, "MIPIPE_FAULT": env_fault})
+    url = f"http://127.0.0.1:{port}"
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                httpx.get(url + "/health", timeout=1)
+                break
+            except Exception:
+                time.sleep(0.2)
+        assert len(httpx.get(url + "/health", timeout=30).json()["stages"]) == 2
+        r = httpx.post(url + "/completion", json={"prompt": prompt, "n_predict": 40}, timeout=120).json()
+        assert r["content"] == ref
+        h = httpx.get(url + "/health", timeout=30).json()
+        assert h["ok"] and h["engine_restarts"] == 1
+        assert len(h["stages"]) == 1          # re-partitioned onto the surviving stage
     finally:
         proc.terminate()
         proc.wait(timeout=30)

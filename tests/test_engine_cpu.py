@@ -450,3 +450,22 @@ def test_cpu_gpu_mem_sums_stages_sharing_a_device(native, model_dir):
     assert budget_mib < total
     assert need([0, 1], budget_mib / 1024) is None      # each GPU fits alone
     assert need([0, 0], budget_mib / 1024)[0] == "0,1"  # together they do not
+
+
+def test_cpu_device_speed_probe_partition(native, model_dir):
+    """Halda-style partitioning from MEASURED device speed (device_speed="probe"): every stage gets
+    a positive speed, the split stays contiguous and generation matches PP=1."""
+    from mipipe.engine import Engine, device_probe
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    host = device_probe(-1)
+    assert host["hbm_read_gbps"] > 0.1 and host["speed"] == host["hbm_read_gbps"]
+    prompts = [[5, 6, 7, 8], [9, 10]]
+    with Engine(gguf=path, backend="cpu", max_ctx=128, mb_size=2) as eng:
+        ref, _ = eng.generate(prompts, 6)
+    with Engine(gguf=path, backend="cpu", max_ctx=128, mb_size=2, stages=2, device_speed="probe") as eng:
+        sp = eng.info["device_speed"]
+        assert len(sp) == 2 and all(v > 0 for v in sp)
+        st = eng.info["stages"]
+        assert st[0]["layer_begin"] == 0 and st[0]["layer_end"] == st[1]["layer_begin"]
+        out, _ = eng.generate(prompts, 6)
+    assert out == ref

@@ -443,3 +443,13 @@ def test_continuous_batching(cuda, native, model_dir, stages):
         t = eng.tokens()
     assert t[1][:10] == alone[1][:10] and t[2][:10] == alone[2][:10] and t[3][:10] == alone[3][:10]
     assert t[0][:5] == alone[4][:5]
+
+
+def test_gpu_device_probe(cuda, native):
+    """Halda device profile of the MI355X: HBM streaming read and the Q4_K decode GEMV rate."""
+    from mipipe.engine import device_probe
+    d = device_probe(0)
+    print(d)
+    assert 2000 < d["hbm_read_gbps"] < 9000
+    assert 1000 < d["gemv_gbps"] < 9000
+    assert d["speed"] == d["gemv_gbps"]
