@@ -30,7 +30,9 @@
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <sys/socket.h>
+#include <poll.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -150,6 +152,11 @@ struct Server {
   // a request for another model that has waited this long stops admission into the model being
   // served; its live requests drain and the generation loop switches models (no starvation)
   double switch_after_ms = 2000;
+  // --spawn-cli: the reference's process model (main.rs:35-57) -- every request runs a CLI child
+  // (mi-cli with the model flags this server was started with); its stdout streams as "token"
+  // messages, its stderr lines as "log" messages; a client disconnect kills the child
+  std::string spawn_cli;
+  std::vector<std::string> cli_args;
 };
 
 Server* g_srv = nullptr;
@@ -655,6 +662,84 @@ bool known_model(Server& S, int fd, std::string* model) {
   return false;
 }
 
+// one request = one child process (spawn-cli mode)
+void spawn_job(Server& S, std::shared_ptr<Job> job) {
+  std::vector<std::string> av{S.spawn_cli};
+  av.insert(av.end(), S.cli_args.begin(), S.cli_args.end());
+  for (const char* a : {"-p", "", "-n", "", "--no-display-prompt"}) av.push_back(a);
+  av[av.size() - 4] = job->prompt;
+  av[av.size() - 2] = std::to_string(job->n_predict);
+  int out[2], err[2];
+  if (pipe(out) != 0 || pipe(err) != 0) {
+    job->push({"log", std::string("error: pipe: ") + strerror(errno) + "\n"});
+    job->finish();
+    return;
+  }
+  const double t0 = now_ms();
+  const pid_t pid = fork();
+  if (pid == 0) {   // child: exec before touching anything else (no GPU state in this process)
+    dup2(out[1], 1);
+    dup2(err[1], 2);
+    close(out[0]); close(out[1]); close(err[0]); close(err[1]);
+    std::vector<char*> cv;
+    for (auto& a : av) cv.push_back(const_cast<char*>(a.c_str()));
+    cv.push_back(nullptr);
+    execv(cv[0], cv.data());
+    fprintf(stderr, "exec %s: %s\n", cv[0], strerror(errno));
+    _exit(127);
+  }
+  close(out[1]);
+  close(err[1]);
+  if (pid < 0) {
+    close(out[0]); close(err[0]);
+    job->push({"log", std::string("error: fork: ") + strerror(errno) + "\n"});
+    job->finish();
+    return;
+  }
+  Utf8Acc acc;
+  std::string line, text;
+  pollfd fds[2] = {{out[0], POLLIN, 0}, {err[0], POLLIN, 0}};
+  int open_fds = 2;
+  bool killed = false;
+  char buf[4096];
+  while (open_fds > 0) {
+    if (job->cancelled && !killed) { kill(pid, SIGTERM); killed = true; }
+    if (poll(fds, 2, 100) < 0 && errno != EINTR) break;
+    for (int k = 0; k < 2; ++k) {
+      if (fds[k].fd < 0 || !(fds[k].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+      const ssize_t n = read(fds[k].fd, buf, sizeof(buf));
+      if (n <= 0) { close(fds[k].fd); fds[k].fd = -1; --open_fds; continue; }
+      if (k == 0) {   // token stream (UTF-8 safe pieces, like the reference's stdout pump)
+        const std::string p = acc.push(std::string(buf, (size_t)n));
+        if (!p.empty()) { text += p; job->push({"token", p}); }
+      } else {        // log lines (stderr), line by line
+        line.append(buf, (size_t)n);
+        size_t nl;
+        while ((nl = line.find('\n')) != std::string::npos) {
+          job->push({"log", line.substr(0, nl + 1)});
+          line.erase(0, nl + 1);
+        }
+      }
+    }
+  }
+  if (!acc.buf.empty()) { text += acc.buf; job->push({"token", acc.buf}); }
+  if (!line.empty()) job->push({"log", line + "\n"});
+  int status = 0;
+  waitpid(pid, &status, 0);
+  GenResult r;
+  r.text = text;
+  r.stop = killed ? "cancelled" : (WIFEXITED(status) && WEXITSTATUS(status) == 0 ? "length" : "error");
+  r.decode_ms = now_ms() - t0;
+  job->result = r;
+  {
+    std::lock_guard<std::mutex> l(S.metrics.mu);
+    if (r.stop == "length") S.metrics.completed++;
+    else if (killed) S.metrics.cancelled++;
+    else S.metrics.errors++;
+  }
+  job->finish();
+}
+
 std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n, const std::string& model = "") {
   auto job = std::make_shared<Job>();
   job->prompt = prompt;
@@ -666,6 +751,10 @@ std::shared_ptr<Job> submit(Server& S, const std::string& prompt, int n, const s
   }
   printf("request: %s\n", prompt.c_str());   // reference main.rs:32 request log
   fflush(stdout);
+  if (!S.spawn_cli.empty()) {   // a child process per request, no engine in this process
+    std::thread(spawn_job, std::ref(S), job).detach();
+    return job;
+  }
   {
     std::lock_guard<std::mutex> l(S.jobs_mu);
     job->enqueued_ms = now_ms();
@@ -830,7 +919,8 @@ void handle_conn(Server& S, int fd, std::string peer) {
         {
           std::lock_guard<std::mutex> l(S.eng_mu);
           h = S.eng ? S.eng->health() : Json::object();
-          if (!S.eng) h["ok"] = S.mock;
+          if (!S.eng) h["ok"] = S.mock || !S.spawn_cli.empty();
+          if (!S.spawn_cli.empty()) h["spawn_cli"] = S.spawn_cli;
           int restarts = 0;
           for (auto& mm : S.models) restarts += mm->restarts;
           h["engine_restarts"] = restarts;
@@ -871,7 +961,8 @@ void handle_conn(Server& S, int fd, std::string peer) {
 void usage() {
   fprintf(stderr, "usage: orchestrator (-m MODEL.gguf | --synthetic NAME | --mock) [--port 3005] [--host 0.0.0.0]\n"
                   "                    [--static DIR] [--api-key KEY] [--rate-limit N/min] [engine flags]\n"
-                  "                    [--alias NAME] [--model-alias NAME=PATH.gguf|synthetic:NAME ...] [--max-models N]\n");
+                  "                    [--alias NAME] [--model-alias NAME=PATH.gguf|synthetic:NAME ...] [--max-models N]\n"
+                  "                    [--spawn-cli mi-cli|PATH]  (a CLI child process per request, as the reference)\n");
   print_common_usage(stderr);
 }
 
@@ -906,6 +997,7 @@ int main(int argc, char** argv) {
       else if (a == "--max-models") S.max_models = std::max(1, std::atoi(val().c_str()));
       else if (a == "--no-continuous") S.continuous = false;
       else if (a == "--model-switch-ms") S.switch_after_ms = std::atof(val().c_str());
+      else if (a == "--spawn-cli") S.spawn_cli = val();
       else if (a == "-h" || a == "--help") { usage(); exit(0); }
       else return false;
       return true;
@@ -925,6 +1017,26 @@ int main(int argc, char** argv) {
   }
   S.mock = mock;
   S.default_n = o.n_predict;
+  if (!S.spawn_cli.empty()) {
+    // forward the model / engine flags to every child; the server's own flags stay here
+    static const char* own1[] = {"--port", "--host", "--static", "--api-key", "--rate-limit", "--mock-delay-ms",
+                                 "--alias", "--model-alias", "--max-models", "--model-switch-ms", "--spawn-cli",
+                                 "-p", "--prompt", "-n", "--n-predict"};
+    static const char* own0[] = {"--mock", "--no-continuous", "--daemon"};
+    for (int i = 1; i < argc; ++i) {
+      bool skip = false;
+      for (const char* f : own1)
+        if (!strcmp(argv[i], f)) { skip = true; ++i; break; }
+      for (const char* f : own0)
+        if (!strcmp(argv[i], f)) skip = true;
+      if (!skip) S.cli_args.push_back(argv[i]);
+    }
+    if (S.spawn_cli == "mi-cli" || S.spawn_cli == "default") {   // the mi-cli next to this binary
+      char exe[4096];
+      const ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+      if (n > 0) { exe[n] = 0; std::string d(exe); S.spawn_cli = d.substr(0, d.rfind('/')) + "/mi-cli"; }
+    }
+  }
   {
     struct stat stt;
     if (stat(S.static_dir.c_str(), &stt) != 0) {   // fall back to the package's static/ next to bin/
@@ -945,7 +1057,10 @@ int main(int argc, char** argv) {
     else broadcast_log(line);
   });
   try {
-    if (!mock) {
+    if (!S.spawn_cli.empty()) {
+      S.startup_logs.push_back("spawn-cli mode: every request runs " + S.spawn_cli + " (no engine in this process)\n");
+      S.capacity = 1 << 20;
+    } else if (!mock) {
       if (!o.eng.has("mb_size")) o.eng["mb_size"] = 4;
       std::unique_ptr<ModelSlot> d(new ModelSlot);
       d->cfg = o.eng;

@@ -380,6 +380,30 @@ def test_failover_repartitions_and_requests_survive(native_bins, tiny_gguf):
         proc.wait(timeout=30)
 
 
+def test_spawn_cli_mode_streams_child_process(native_bins, tiny_gguf):
+    """--spawn-cli: the reference's process model (main.rs:35-57): each request runs mi-cli as a
+    child; its stdout arrives as "token" messages (same text as running the CLI directly), its
+    stderr as "log" messages."""
+    base = [os.path.join(BIN, "mi-cli"), "-m", tiny_gguf, "-c", "256", "-ngl", "0", "--no-display-prompt"]
+    prompt = "Once upon a time"
+    ref = subprocess.run(base + ["-p", prompt, "-n", "12"], capture_output=True, timeout=120).stdout
+    ref = ref.decode("utf-8", errors="replace")
+    s = Orchestrator("-m", tiny_gguf, "-ngl", "0", "-c", "256", "--spawn-cli", "mi-cli")
+    try:
+        h = httpx.get(s.url + "/health", timeout=30).json()
+        assert h["ok"] and h["spawn_cli"].endswith("mi-cli")
+        with httpx.stream("POST", s.url + "/chat", json={"prompt": prompt, "n_predict": 12}, timeout=120) as r:
+            ev, _ = sse_events(r)
+        text = "".join(e["content"] for e in ev if e["msg_type"] == "token")
+        assert text == ref
+        logs = "".join(e["content"] for e in ev if e["msg_type"] == "log")
+        assert "layers" in logs                      # the child's placement line (stderr)
+        r2 = httpx.post(s.url + "/completion", json={"prompt": prompt, "n_predict": 12}, timeout=120).json()
+        assert r2["content"] == ref and r2["stop_reason"] == "length"
+    finally:
+        s.close()
+
+
 def test_cli_state_save_and_resume(native_bins, tiny_gguf, tmp_path):
     """mi-cli --state-save after 10 tokens, then --state-load -n 6 prints exactly the last 6 tokens
     of an uninterrupted 16-token run (checkpoint/resume)."""
