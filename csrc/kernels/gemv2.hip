@@ -17,6 +17,7 @@
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace mpk {
@@ -46,7 +47,13 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
-  const int tile0 = (blockIdx.x * NW + wave) * TW;
+  // prompt GEMM use (p.m_blocks > 1): blockIdx.x = tile group * m_blocks + row block, so the row
+  // blocks sharing a weight tile group are dispatched together (their weight reads after the first
+  // hit the memory-side cache)
+  const int mblk = p.m_blocks > 1 ? (int)blockIdx.x % p.m_blocks : 0;
+  const int bx = p.m_blocks > 1 ? (int)blockIdx.x / p.m_blocks : (int)blockIdx.x;
+  const int tile0 = (bx * NW + wave) * TW;
+  const size_t r_off = (size_t)mblk * 16 * MT;   // first row of this workgroup
   const int sbA = blockIdx.y * p.sb_per_split;
   const int sbB = min(sbA + p.sb_per_split, p.nsb);
   if (sbA >= sbB) return;   // uniform over the workgroup
@@ -60,7 +67,8 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     const int nb = tl < p.ntiles ? sbB - sbA : 0;
     wsrc[t] = make_rsrc(p.W + ((size_t)min(tl, p.ntiles - 1) * p.nsb + sbA) * CB, (uint32_t)(nb * CB));
   }
-  const int M = p.M;
+  const int M = min(p.M - (int)r_off, 16 * MT);
+  const f16* const Xg = p.X + r_off * p.ldx;
 
   // x staging: 16 MT rows x 256 k per super-block = 512 MT chunks of 16 B; thread t owns chunks t, t+NT..
   // The x chunks of super-block j are loaded TOGETHER with its weights (register rings of NSLOT),
@@ -95,7 +103,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           xv[sl][j][2] = in ? *reinterpret_cast<const u32x4*>(p.gamma + k) : u32x4{0u, 0u, 0u, 0u};
           xv[sl][j][3] = in ? *reinterpret_cast<const u32x4*>(p.gamma + k + 4) : u32x4{0u, 0u, 0u, 0u};
         } else {
-          xv[sl][j][0] = row < M ? *reinterpret_cast<const u32x4*>(p.X + (size_t)row * p.ldx + (size_t)sbx * 256 + col)
+          xv[sl][j][0] = row < M ? *reinterpret_cast<const u32x4*>(Xg + (size_t)row * p.ldx + (size_t)sbx * 256 + col)
                                  : u32x4{0u, 0u, 0u, 0u};
         }
       }
@@ -206,7 +214,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           const float other = __shfl_xor(acc[t][mt][i], 8);
           const int m = 16 * mt + 4 * g + i;
           const int o = tile * 8 + r;
-          if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[t][mt][i]) * other);
+          if (r < 8 && m < M && o < p.n_valid) p.H[(r_off + m) * p.ldh + o] = (f16)(silu(acc[t][mt][i]) * other);
         }
       } else {
         const int n = tile * 16 + r;
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           for (int i = 0; i < 4; ++i) {
             const int m = 16 * mt + 4 * g + i;
             if (m < M) {
-              float* dst = p.Y + (size_t)blockIdx.y * p.split_stride + (size_t)m * p.ldy + n;
+              float* dst = p.Y + (size_t)blockIdx.y * p.split_stride + (r_off + m) * p.ldy + n;
               if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[t][mt][i] + bias);
               else *dst = acc[t][mt][i] + bias;
             }
@@ -296,6 +304,43 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
     case P_Q8_0: gemv2_pt<P_Q8_0>(epi, p, nsplit, nw, tw, st); break;
     case P_Q4_0: gemv2_pt<P_Q4_0>(epi, p, nsplit, nw, tw, st); break;
     case P_F16: gemv2_pt<P_F16>(epi, p, nsplit, nw, tw, st); break;
+  }
+}
+
+template <int PT, int EPI>
+static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st) {
+  constexpr int NW = 8, TW = 2, MT = 8;
+  p.m_blocks = (p.M + 16 * MT - 1) / (16 * MT);
+  const int groups = (p.ntiles + NW * TW - 1) / (NW * TW);
+  // narrow outputs (8B down / qkv, 70B o / down: 16-32 tile groups) leave CUs idle: split K over
+  // workgroups when the epilogue accumulates anyway, as far as the grid still runs in ONE round of
+  // one workgroup per CU (135 KB of LDS each) and >= 4 super-blocks per split (M=512: 70B down
+  // 409 -> 261 us, o 136 -> 99, 8B down 206 -> 94; a second round cost 70B qkv 142 -> 170)
+  int nsplit = 1;
+  const int wgs = groups * p.m_blocks;
+  if (EPI == EPI_ATOMIC && allow_split && wgs < 256) nsplit = std::min(256 / wgs, std::max(1, p.nsb / 4));
+  p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
+  nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
+  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, MT, TW, false>), dim3(wgs, nsplit), dim3(NW * 64), 0, st, p);
+}
+
+template <int PT>
+static void gemm2_pt(int epi, const GemvParams& p, bool allow_split, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return gemm2_go<PT, EPI_STORE>(p, allow_split, st);
+    case EPI_ATOMIC: return gemm2_go<PT, EPI_ATOMIC>(p, allow_split, st);
+    case EPI_SWIGLU: return gemm2_go<PT, EPI_SWIGLU>(p, allow_split, st);
+  }
+}
+
+void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split) {
+  switch (ptype) {
+    case P_Q4_K: gemm2_pt<P_Q4_K>(epi, p, allow_split, st); break;
+    case P_Q5_K: gemm2_pt<P_Q5_K>(epi, p, allow_split, st); break;
+    case P_Q6_K: gemm2_pt<P_Q6_K>(epi, p, allow_split, st); break;
+    case P_Q8_0: gemm2_pt<P_Q8_0>(epi, p, allow_split, st); break;
+    case P_Q4_0: gemm2_pt<P_Q4_0>(epi, p, allow_split, st); break;
+    default: launch_gemm(ptype, epi, p, st); break;   // f16 weights: the 64 x 64 GEMM
   }
 }
 

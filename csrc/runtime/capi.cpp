@@ -156,6 +156,17 @@ int mp_op_gemm(int ptype, int epi, const void* W, int ntiles, int nsb, const voi
   API_CATCH(-1)
 }
 
+int mp_op_gemm2(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+                int ldy, void* H, int ldh, int n_valid, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  launch_gemm2(ptype, epi, p, (hipStream_t)stream);
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
                int ldy, void* H, int ldh, int n_valid, int nsplit, void* stream) {
   API_TRY

@@ -641,12 +641,16 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // exception: the large gate/up GEMVs that run two tiles per wave (>= 192 workgroups of 16
   // tiles) beat the 64x64-tile GEMM per 64 rows (70B: 4 x 73.6 us vs 410 us per 256-row chunk;
   // profiles/r1g_prefill_gemm_vs_gemv.txt)
+  // v2 GEMM (128 rows x 256 columns per workgroup, the decode GEMV's dequant + LDS-shared rows):
+  // every shape, f16 weights excepted (they take the 64 x 64 GEMM)
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
-  if (M > 64 && opt_.prefill_gemm && !wide_swiglu) {
+  const bool v2 = opt_.prefill_gemm_v == 2 && m.ptype != P_F16;
+  if (M > 64 && opt_.prefill_gemm && (v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
-    launch_gemm(m.ptype, epi, p, st);
+    if (v2) launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+    else launch_gemm(m.ptype, epi, p, st);
     return;
   }
   for (int r0 = 0; r0 < M; r0 += 64) {

@@ -37,6 +37,7 @@ struct GemvParams {
   const float* bias = nullptr;   // [n] added once (split 0) to STORE / ATOMIC outputs
   float* zero = nullptr;         // side job after the GEMV: zero_n floats cleared
   int64_t zero_n = 0;
+  int m_blocks = 1;              // prompt GEMM (launch_gemm2): row blocks of 128 per weight tile group
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
@@ -62,6 +63,11 @@ void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, i
 
 // Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.
 void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
+// Prefill GEMM v2: the decode GEMV design widened to 128 rows per workgroup (8 MFMA row groups per
+// dequantized weight fragment, two 16-column tiles per wave, 256 columns x 128 rows per 8-wave
+// workgroup, whole K per workgroup); EPI_ATOMIC adds into Y (single writer per element)
+// (EPI_ATOMIC: split-K over workgroups when there are few output tiles, unless allow_split is false)
+void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
 
 // Y[m][n] += sum_{s < nsplit} part[s][m][n], s ascending: the fixed-order split-K reduction of the
 // deterministic mode (part rows of ldp floats, splits split_stride floats apart)

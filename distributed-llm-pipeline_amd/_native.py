@@ -45,6 +45,8 @@ _SIGS = {
                     c_int, c_int, c_int, c_void_p], c_int),
     "mp_op_gemm": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                     c_int, c_int, c_void_p], c_int),
+    "mp_op_gemm2": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                    c_int, c_int, c_void_p], c_int),
     "mp_op_unpack": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_rmsnorm": ([c_void_p, c_int, c_void_p, c_int, c_float, c_void_p, c_int, c_int, c_void_p], c_int),
     "mp_op_embed": ([c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),

@@ -82,19 +82,21 @@ def gemv(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
 
 
 def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor | None = None,
-         n_valid: int | None = None) -> torch.Tensor:
-    """Prefill GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC = single-owner add)."""
+         n_valid: int | None = None, v: int = 2) -> torch.Tensor:
+    """Prefill GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC = single-owner add).
+    v=2: 128-row x 256-column workgroup tiles (launch_gemm2); v=1: the 64 x 64 tile GEMM."""
     assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
     M = x.shape[0]
+    fn = N.lib().mp_op_gemm2 if v == 2 else N.lib().mp_op_gemm
     if epi == EPI_SWIGLU:
         F = w.n // 2
         h = torch.zeros(M, F, dtype=torch.float16, device=x.device) if y is None else y
-        N.check(N.lib().mp_op_gemm(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, None, 0,
+        N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, None, 0,
                                    _ptr(h), h.stride(0), F if n_valid is None else n_valid, _stream()), "gemm")
         return h
     if y is None:
         y = torch.zeros(M, w.n, dtype=torch.float32, device=x.device)
-    N.check(N.lib().mp_op_gemm(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
+    N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
                                y.stride(0), None, 0, w.n if n_valid is None else n_valid, _stream()), "gemm")
     return y
 

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--iters", type=int, default=24)
     ap.add_argument("--target", type=int, default=2048)
     ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 store, 1 atomic): timing probes")
+    ap.add_argument("--copies", type=int, default=0, help="weight copies cycled (default: enough to defeat the 256 MiB MALL; 1 = hot)")
+    ap.add_argument("--gemm", type=int, default=0, help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256)")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -46,7 +48,7 @@ def main():
             pt = pack_type(qt)
             n_pad, k_pad, ntiles, nsb = packed_dims(qt, n, k)
             nbytes = L.mp_packed_bytes(qt, n, k)
-            copies = max(2, min(24, (1536 << 20) // nbytes + 1))
+            copies = a.copies or max(2, min(24, (1536 << 20) // nbytes + 1))
             Ws = []
             for c in range(copies):
                 W = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -59,7 +61,7 @@ def main():
                 for tpw in [int(t) for t in a.tpw.split(",")]:
                     L.mp_set_gemv_tpw(tpw)
                     waves = (ntiles + max(tpw, 1) - 1) // max(tpw, 1)
-                    if epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
+                    if a.gemm or epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
                         splits = [1]
                     elif a.splits == "auto":
                         splits = [max(1, min((a.target + waves - 1) // waves, max(1, nsb // 4)))]
@@ -67,6 +69,13 @@ def main():
                         splits = [int(s) for s in a.splits.split(",")]
                     for nsplit in splits:
                         def run(W):
+                            if a.gemm:
+                                fn = L.mp_op_gemm2 if a.gemm == 2 else L.mp_op_gemm
+                                N.check(fn(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
+                                           ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
+                                           n, ctypes.c_void_p(H.data_ptr()), n // 2,
+                                           n if epi != EPI_SWIGLU else n // 2, st()), "gemm")
+                                return
                             N.check(L.mp_op_gemv(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
                                                  ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
                                                  n, ctypes.c_void_p(H.data_ptr()), n // 2,
@@ -82,7 +91,8 @@ def main():
                         torch.cuda.synchronize()
                         us = e0.elapsed_time(e1) * 1e3 / a.iters
                         print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
-                                              GBps=round(nbytes / us / 1e3, 1))), flush=True)
+                                              GBps=round(nbytes / us / 1e3, 1),
+                                              TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm)), flush=True)
             del Ws
             torch.cuda.empty_cache()
 
