@@ -116,10 +116,20 @@ def init_from_torchrun(pp: int | None = None, **cfg):
     else:
         torch.cuda.set_device(local_rank)
     if world > 1 and not dist.is_initialized():
+        kw = {}
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart not in (None, "0") and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
+            # under torchrun the agent's store outlives a restart: key a restarted attempt's
+            # rendezvous by the restart count, or its ranks read the dead attempt's peer addresses
+            # (parallel/elastic.py)
+            from datetime import timedelta
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
+                                 timeout=timedelta(seconds=300))
+            kw = dict(store=dist.PrefixStore(f"mipipe/attempt_{restart}", base), rank=rank, world_size=world)
         if cpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **kw)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **kw)
     if pp == 1:
         cfg.setdefault("mode", "local")
         cfg.setdefault("stages", 1)

@@ -91,3 +91,40 @@ def test_init_from_torchrun_replicas(native, model_dir, tmp_path, world, pp):
         last = res[g * pp + pp - 1]
         assert len(last["stages"]) == pp
         assert last["out"] == ref   # the replica's last stage holds the generated tokens
+
+
+_ELASTIC = r"""
+import json, os, sys
+sys.path.insert(0, {repo!r})
+from mipipe.parallel import generate_elastic
+import torch.distributed as dist
+out = generate_elastic({prompts!r}, {n!r}, {ckpt!r}, every=3, pp=2, gguf={path!r}, backend="cpu", max_ctx=128,
+                       n_mb=2, mb_size=1, prefill_chunk=16, split="even", base_port={port})
+print("OUT " + json.dumps(dict(rank=int(os.environ["RANK"]), restart=os.environ.get("TORCHELASTIC_RESTART_COUNT"),
+                               out=out)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_elastic_rank_restart_resumes_from_checkpoint(native, model_dir, tmp_path):
+    """A 2-stage multi-process pipeline under `torchrun --max-restarts 1`: rank 1 dies after 7
+    decode rounds; torchrun restarts both ranks, they resume from the round-6 checkpoint and the
+    generation equals the uninterrupted single-process one."""
+    from mipipe.engine import Engine
+    from test_engine_cpu import free_port
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts, n = [[5, 6, 7, 8], [9, 10]], 12
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16) as eng:
+        ref, _ = eng.generate(prompts, n)
+    ckpt = tmp_path / "ckpt"
+    script = tmp_path / "run.py"
+    script.write_text(_ELASTIC.format(repo=REPO, path=path, prompts=prompts, n=n, ckpt=str(ckpt), port=free_port()))
+    env = dict(os.environ, OMP_NUM_THREADS="2", MIPIPE_ELASTIC_FAIL="1,7")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--max-restarts", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    outs = [json.loads(l[4:]) for l in p.stdout.splitlines() if l.startswith("OUT ")]
+    assert {o["restart"] for o in outs} == {"1"}, outs       # only the restarted attempt finished
+    assert all(o["out"] == ref for o in outs)
+    assert (ckpt / "replica0" / "round_00000009" / "COMPLETE").exists()   # last checkpoint before the end
