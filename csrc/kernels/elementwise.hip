@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const float* gu, int ld, in
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j < F) {
     const float g = gu[(size_t)m * ld + j], u = gu[(size_t)m * ld + F + j];
-    h[(size_t)m * ldh + j] = (f16)(silu(g) * u);
+    h[(size_t)m * ldh + j] = sat_f16(silu(g) * u);
   }
 }
 

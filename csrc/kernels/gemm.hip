@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
       if constexpr (EPI == EPI_SWIGLU) {
         const float other = __shfl_xor(acc[ms][i], 8);
         const int o = tile * 8 + r;
-        if (r < 8 && m < p.M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = (f16)(silu(acc[ms][i]) * other);
+        if (r < 8 && m < p.M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(acc[ms][i]) * other);
       } else {
         const int n = tile * 16 + r;
         if (m < p.M && n < p.n_valid) {

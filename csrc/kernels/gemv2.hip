@@ -214,7 +214,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           const float other = __shfl_xor(acc[t][mt][i], 8);
           const int m = 16 * mt + 4 * g + i;
           const int o = tile * 8 + r;
-          if (r < 8 && m < M && o < p.n_valid) p.H[(r_off + m) * p.ldh + o] = (f16)(silu(acc[t][mt][i]) * other);
+          if (r < 8 && m < M && o < p.n_valid) p.H[(r_off + m) * p.ldh + o] = sat_f16(silu(acc[t][mt][i]) * other);
         }
       } else {
         const int n = tile * 16 + r;

@@ -51,3 +51,6 @@ __device__ __forceinline__ void scale_min_k4(int j, const uint8_t* q, int& sc, i
 }
 
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// f16 with saturation: the SwiGLU intermediate of layers with massive activations can pass f16's
+// 65504; saturating keeps an inf (and the NaNs it breeds in the next GEMV) out of the pipeline
+__device__ __forceinline__ f16 sat_f16(float v) { return (f16)fminf(fmaxf(v, -65504.f), 65504.f); }

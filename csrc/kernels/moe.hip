@@ -98,7 +98,7 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
         if (r < 8 && m < rows) {
           const int o = tile * 8 + r;
           const int slot = list[r0 + m];
-          if (o < p.n_valid) p.H[(size_t)slot * p.ldh + o] = (f16)(silu(acc[i]) * other);
+          if (o < p.n_valid) p.H[(size_t)slot * p.ldh + o] = sat_f16(silu(acc[i]) * other);
         }
       } else if (m < rows) {
         const int n = tile * 16 + r;
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
       if constexpr (EPI == EPI_SWIGLU) {
         const float other = __shfl_xor(acc[mt][i], 8);
         const int o = tile * 8 + r;
-        if (r < 8 && m < rows && o < p.n_valid) p.H[(size_t)list[m] * p.ldh + o] = (f16)(silu(acc[mt][i]) * other);
+        if (r < 8 && m < rows && o < p.n_valid) p.H[(size_t)list[m] * p.ldh + o] = sat_f16(silu(acc[mt][i]) * other);
       } else {
         const int n = tile * 16 + r;
         if (m < rows && n < p.n_valid) {

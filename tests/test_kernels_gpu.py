@@ -85,6 +85,28 @@ def test_gemv_swiglu(cuda, native, qt, M):
     assert nmse(h.float().cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("M", [1, 64, 200])
+def test_swiglu_saturates_instead_of_inf(cuda, native, M):
+    """A gate/up pair whose SwiGLU product passes f16's 65504 (massive-activation channels):
+    the f16 intermediate saturates at +-65504 instead of becoming inf (decode GEMV for M <= 64,
+    prompt GEMM above); the in-range columns stay exact."""
+    from mipipe.ops.kernels import PackedWeight, gemv, gemm, EPI_SWIGLU
+    F, k = 16, 256
+    g = np.zeros((F, k), np.float32)
+    u = np.zeros((F, k), np.float32)
+    g[:8, 0], u[:8, 0] = 60.0, 60.0          # 8 saturating outputs: silu(60 x) * 60 x >> 65504 for x = 10
+    g[8:, 1], u[8:, 1] = 0.5, 0.25           # 8 ordinary outputs
+    raw = Q.quantize(np.concatenate([g, u]), Q.F16)
+    w = PackedWeight(raw, Q.F16, 2 * F, k, gateup=True)
+    xh = torch.zeros(M, k, dtype=torch.float16)
+    xh[:, 0], xh[:, 1] = 10.0, 2.0
+    h = (gemv(w, xh.cuda(), EPI_SWIGLU) if M <= 64 else gemm(w, xh.cuda(), EPI_SWIGLU)).float().cpu()
+    assert torch.isfinite(h).all()
+    assert (h[:, :8] == 65504.0).all()
+    ref = torch.nn.functional.silu(torch.tensor(1.0)) * 0.5
+    torch.testing.assert_close(h[:, 8:], ref.expand(M, 8), rtol=2e-3, atol=1e-4)
+
+
 def test_gemv_asymmetric_identity(cuda, native):
     """A = I style check with an asymmetric operand (catches transposed C writes)."""
     from mipipe.ops.kernels import PackedWeight, gemv
