@@ -9,6 +9,8 @@
 // (O^T = V^T P^T, A = V^T read from the transposed V page) -- no LDS round trip, no shuffles for P.
 // Online softmax in registers; 4 waves interleave chunks and are merged through LDS; splits are
 // merged by attn_combine (LSE merge).  KV pages hold 64 tokens: K [64][Dp], V^T [Dp][64].
+#include <type_traits>
+
 #include "kcommon.h"
 #include "../runtime/kernels_api.h"
 
@@ -203,8 +205,15 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
 
 constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
 
-template <int DP>
+// F8: the KV pages hold e4m3 bytes (kv_dtype "fp8"): half the KV bytes per step; fragments are
+// loaded raw (8 bytes per 8 keys / dims), kept raw through the prefetch, converted to f16 at use
+template <int DP, bool F8>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
+  using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
+  auto cvt = [](const KR& r) -> half8_t {
+    if constexpr (F8) return f8x8_to_h8(r);
+    else return r;
+  };
   constexpr int KK = DP / 32;
   constexpr int DT = DP / 16;
   __shared__ float sm_m[4][16], sm_l[4][16];
@@ -320,30 +329,31 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
   const int nch = (end - start + 31) / 32;
   const int krow0 = 8 * (col >> 2) + (col & 3);
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  auto load = [&](int ci, half8_t (&kf)[2][KK], half8_t (&vf)[DT]) {
+  constexpr int EB = F8 ? 1 : 2;   // bytes per cached element
+  auto load = [&](int ci, KR (&kf)[2][KK], KR (&vf)[DT]) {
     const int P0 = start + ci * 32;
     const int page = bt[P0 >> 6];
     const int in_page = P0 & 63;
-    const f16* kbase = p.k_cache + ((size_t)page * p.Hkv + kvh) * 64 * DP;
-    const f16* vbase = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
+    const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
+    const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
-        kf[c][kk] = *reinterpret_cast<const half8_t*>(kbase + (size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4);
+        kf[c][kk] = *reinterpret_cast<const KR*>(kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
-      vf[dt] = *reinterpret_cast<const half8_t*>(vbase + (size_t)(16 * dt + col) * 64 + in_page + 8 * q4);
+      vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
   };
-  half8_t kA[2][KK], vA[DT], kB[2][KK], vB[DT];
+  KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
   if (wv < nch) load(wv, kA, vA);
 
   if (owns) {
     const int page = bt[pos >> 6], idx = pos & 63;
     const int kr = p.Hq * p.hd + kvh * p.hd;
     const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
-    f16* kd = p.k_cache + (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
-    f16* vd = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
+    const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;     // element offsets
+    const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
     // one K pair and one V element per thread (DP <= 256 threads), all reads issued before any use
     const int j = threadIdx.x;
     float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
@@ -360,14 +370,29 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     }
     if (j < DP / 2) {
       const float x0 = fmaf(nrs, kx.x, kb.x), x1 = fmaf(nrs, kx.y, kb.y);
-      const half2_t o = kin ? half2_t{(f16)(x0 * c.x - x1 * c.y), (f16)(x0 * c.y + x1 * c.x)}
-                            : half2_t{(f16)0.f, (f16)0.f};
-      *reinterpret_cast<half2_t*>(kd + 2 * j) = o;
+      const float r0 = kin ? x0 * c.x - x1 * c.y : 0.f, r1 = kin ? x0 * c.y + x1 * c.x : 0.f;
+      half2_t o;
+      if constexpr (F8) {   // the patch sees exactly what later steps read back from the cache
+        const uint32_t q = f8x2_pack(r0, r1);
+        *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(p.k_cache) + koff + 2 * j) = (uint16_t)q;
+        o = f8x2_lo(q);
+      } else {
+        o = half2_t{(f16)r0, (f16)r1};
+        *reinterpret_cast<half2_t*>(p.k_cache + koff + 2 * j) = o;
+      }
       *reinterpret_cast<half2_t*>(sm_kn + 2 * j) = o;
     }
     if (j < DP) {
-      const f16 v = (f16)(vin ? fmaf(nrs, vx, vb) : 0.f);
-      vd[(size_t)j * 64] = v;
+      const float vv = vin ? fmaf(nrs, vx, vb) : 0.f;
+      f16 v;
+      if constexpr (F8) {
+        const uint32_t q = f8x2_pack(vv, 0.f);
+        reinterpret_cast<uint8_t*>(p.v_cache)[voff + (size_t)j * 64] = (uint8_t)q;
+        v = f8x2_lo(q).x;
+      } else {
+        v = (f16)vv;
+        p.v_cache[voff + (size_t)j * 64] = v;
+      }
       sm_vn[j] = v;
     }
     // LDS-only release/acquire around the barrier: the global append needs no wait here
@@ -383,7 +408,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
 
   // one 32-key chunk: patch the new token in (if this chunk holds it), S^T = K Q^T, online
   // softmax, O^T += V^T P^T
-  auto step = [&](int ci, half8_t (&kf)[2][KK], half8_t (&vf)[DT]) {
+  auto step_h = [&](int ci, half8_t (&kf)[2][KK], half8_t (&vf)[DT]) {
     const int P0 = start + ci * 32;
     if (owns && pos >= P0 && pos < P0 + 32) {   // wave-uniform
       const int r = pos - P0;
@@ -441,6 +466,20 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
                   (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+  };
+  auto step = [&](int ci, KR (&kraw)[2][KK], KR (&vraw)[DT]) {
+    if constexpr (F8) {   // convert the raw e4m3 fragments at use (the prefetch holds raw bytes)
+      half8_t kf[2][KK], vf[DT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) kf[c][kk] = cvt(kraw[c][kk]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) vf[dt] = cvt(vraw[dt]);
+      step_h(ci, kf, vf);
+    } else {
+      step_h(ci, kraw, vraw);
+    }
   };
   // waves take chunks wv, wv + 4, ...; the next chunk's loads are issued before this one's math
   for (int ci = wv; ci < nch;) {
@@ -572,8 +611,13 @@ void launch_attn_combine(const AttnParams& p, hipStream_t st) {
 
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
   dim3 grid(p.M, p.Hkv, p.n_split);
-  if (p.Dp == 128) hipLaunchKernelGGL(mpk::attn_decode_kernel<128>, grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL(mpk::attn_decode_kernel<64>, grid, dim3(256), 0, st, p);
+  if (p.kv_fp8) {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, true>), grid, dim3(256), 0, st, p);
+  } else {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, false>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, false>), grid, dim3(256), 0, st, p);
+  }
 }
 
 }  // namespace mp

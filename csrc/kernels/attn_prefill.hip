@@ -21,6 +21,7 @@
 #include "../runtime/kernels_api.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <stdexcept>
 
 namespace mpk {
@@ -30,8 +31,10 @@ using namespace mp;
 // fragment read from LDS feeding two MFMAs, 4 waves) took 260 us per 8B 32K-prompt layer chunk
 // against 184 us for RG = 1 with 8 waves (190 vs 119 VGPRs: half the waves per SIMD;
 // profiles/r2n_prof_8b_32k_rg*.txt), so the launcher instantiates RG = 1.
-template <int DP, int NW, int RG>
+// F8: e4m3 KV pages (kv_dtype "fp8"), converted to f16 while staging into LDS
+template <int DP, int NW, int RG, bool F8>
 __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttnParams p) {
+  using KR = std::conditional_t<F8, u32x2, u32x4>;   // raw 8-element chunk
   constexpr int KK = DP / 32;    // k-steps of S^T over d
   constexpr int DT = DP / 16;    // 16-row d tiles of O^T
   constexpr int KLD = DP + 8;    // K tile row stride (f16): 16 key rows of a fragment hit distinct banks
@@ -83,24 +86,29 @@ __global__ __launch_bounds__(NW * 64) void attn_prefill_kernel(const PrefillAttn
 
   // page staging: thread owns K chunks (key = c / (DP/8), d8 = c % (DP/8)) and V^T chunks
   // (d = c / 8, k8 = c % 8), c = tid + NT j
-  u32x4 kr[KCH], vr[KCH];
+  KR kr[KCH], vr[KCH];
+  constexpr int EB = F8 ? 1 : 2;   // bytes per cached element
   auto load_page = [&](int kt) {
     const int page = bt[kt];
-    const f16* kb = p.k_cache + ((size_t)page * p.Hkv + kvh) * 64 * DP;
-    const f16* vb = p.v_cache + ((size_t)page * p.Hkv + kvh) * DP * 64;
+    const uint8_t* kb = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
+    const uint8_t* vb = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
 #pragma unroll
     for (int j = 0; j < KCH; ++j) {
       const int c = tid + NT * j;
-      kr[j] = *reinterpret_cast<const u32x4*>(kb + (size_t)c * 8);
-      vr[j] = *reinterpret_cast<const u32x4*>(vb + (size_t)c * 8);
+      kr[j] = *reinterpret_cast<const KR*>(kb + (size_t)c * 8 * EB);
+      vr[j] = *reinterpret_cast<const KR*>(vb + (size_t)c * 8 * EB);
     }
+  };
+  auto as16 = [](const KR& r) -> u32x4 {
+    if constexpr (F8) return __builtin_bit_cast(u32x4, f8x8_to_h8(r));
+    else return r;
   };
   auto store_page = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < KCH; ++j) {
       const int c = tid + NT * j;
-      *reinterpret_cast<u32x4*>(&ks[buf][(c / (DP / 8)) * KLD + (c % (DP / 8)) * 8]) = kr[j];
-      *reinterpret_cast<u32x4*>(&vs[buf][(c / 8) * VLD + (c % 8) * 8]) = vr[j];
+      *reinterpret_cast<u32x4*>(&ks[buf][(c / (DP / 8)) * KLD + (c % (DP / 8)) * 8]) = as16(kr[j]);
+      *reinterpret_cast<u32x4*>(&vs[buf][(c / 8) * VLD + (c % 8) * 8]) = as16(vr[j]);
     }
   };
 
@@ -246,8 +254,11 @@ void launch_attn_prefill(const PrefillAttnParams& p, hipStream_t st) {
   if (p.n_split > 1 && (!p.o_part || !p.ml_part || p.split_pages < 1))
     throw std::runtime_error("launch_attn_prefill: split without partial buffers");
   const dim3 grid(p.n_tiles, p.Hkv, std::max(1, p.n_split));
-  if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1>), grid, dim3(512), 0, st, p);
-  else if (p.Dp == 64) hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1>), grid, dim3(512), 0, st, p);
+  if (p.kv_fp8) {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1, true>), grid, dim3(512), 0, st, p);
+    else if (p.Dp == 64) hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1, true>), grid, dim3(512), 0, st, p);
+  } else if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_prefill_kernel<128, 8, 1, false>), grid, dim3(512), 0, st, p);
+  else if (p.Dp == 64) hipLaunchKernelGGL((mpk::attn_prefill_kernel<64, 8, 1, false>), grid, dim3(512), 0, st, p);
   else throw std::runtime_error("launch_attn_prefill: Dp must be 64 or 128");
   if (p.n_split > 1) {   // LSE merge of the splits into out (attention.hip)
     AttnParams a{};

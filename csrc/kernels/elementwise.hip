@@ -151,23 +151,36 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const RopeKvParams p) {
     if (hg < p.Hq + p.Hkv) {                       // q or k head: rotate adjacent pair j
       const bool isq = hg < p.Hq;
       const int h = isq ? hg : hg - p.Hq;
-      half2_t o = {(f16)0.f, (f16)0.f};
+      float r0 = 0.f, r1 = 0.f;
       if (j < hd2) {
         const float* src = row + (isq ? 0 : p.Hq * p.hd) + h * p.hd + 2 * j;
         const float x0 = src[0], x1 = src[1];
         const float2 c = cs[j];
         const float sc = isq ? p.q_scale : 1.f;
-        o = half2_t{(f16)((x0 * c.x - x1 * c.y) * sc), (f16)((x0 * c.y + x1 * c.x) * sc)};
+        r0 = (x0 * c.x - x1 * c.y) * sc;
+        r1 = (x0 * c.y + x1 * c.x) * sc;
       }
+      const half2_t o = {(f16)r0, (f16)r1};
+      const size_t ko = (((size_t)page * p.Hkv + h) * 64 + idx) * p.Dp + 2 * j;
       if (isq) *reinterpret_cast<half2_t*>(p.q_out + ((size_t)m * p.Hq + h) * p.Dp + 2 * j) = o;
-      else *reinterpret_cast<half2_t*>(p.k_cache + (((size_t)page * p.Hkv + h) * 64 + idx) * p.Dp + 2 * j) = o;
+      else if (p.kv_fp8) *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(p.k_cache) + ko) = (uint16_t)f8x2_pack(r0, r1);
+      else *reinterpret_cast<half2_t*>(p.k_cache + ko) = o;
     } else {                                        // v head: transposed page layout [Dp][64]
       const int h = hg - p.Hq - p.Hkv;
       const float* vr = row + (p.Hq + p.Hkv) * p.hd + h * p.hd;
-      f16* vd = p.v_cache + (((size_t)page * p.Hkv + h) * p.Dp) * 64 + idx;
+      const size_t vo = (((size_t)page * p.Hkv + h) * p.Dp) * 64 + idx;
       const int d0 = 2 * j;
-      vd[(size_t)d0 * 64] = (f16)(d0 < p.hd ? vr[d0] : 0.f);
-      vd[(size_t)(d0 + 1) * 64] = (f16)(d0 + 1 < p.hd ? vr[d0 + 1] : 0.f);
+      const float v0 = d0 < p.hd ? vr[d0] : 0.f, v1 = d0 + 1 < p.hd ? vr[d0 + 1] : 0.f;
+      if (p.kv_fp8) {
+        uint8_t* vd = reinterpret_cast<uint8_t*>(p.v_cache) + vo;
+        const uint32_t q = f8x2_pack(v0, v1);
+        vd[(size_t)d0 * 64] = (uint8_t)q;
+        vd[(size_t)(d0 + 1) * 64] = (uint8_t)(q >> 8);
+      } else {
+        f16* vd = p.v_cache + vo;
+        vd[(size_t)d0 * 64] = (f16)v0;
+        vd[(size_t)(d0 + 1) * 64] = (f16)v1;
+      }
     }
   }
 }

@@ -54,3 +54,17 @@ __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcp
 // f16 with saturation: the SwiGLU intermediate of layers with massive activations can pass f16's
 // 65504; saturating keeps an inf (and the NaNs it breeds in the next GEMV) out of the pipeline
 __device__ __forceinline__ f16 sat_f16(float v) { return (f16)fminf(fmaxf(v, -65504.f), 65504.f); }
+
+// fp8 KV cache (kv_dtype "fp8"): OCP e4m3 bytes, converted with the gfx950 cvt instructions.
+// e4m3 has no inf: stored values are clamped to its +-448 range first.
+__device__ __forceinline__ uint32_t f8x2_pack(float a, float b) {   // -> bytes 0, 1 of the result
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
+}
+__device__ __forceinline__ half2_t f8x2_lo(uint32_t w) { return __builtin_amdgcn_cvt_scalef32_pk_f16_fp8((int)w, 1.0f, false); }
+__device__ __forceinline__ half2_t f8x2_hi(uint32_t w) { return __builtin_amdgcn_cvt_scalef32_pk_f16_fp8((int)w, 1.0f, true); }
+__device__ __forceinline__ half8_t f8x8_to_h8(u32x2 r) {   // 8 e4m3 bytes (element j = byte j) -> 8 f16
+  const half2_t a = f8x2_lo(r.x), b = f8x2_hi(r.x), c = f8x2_lo(r.y), d = f8x2_hi(r.y);
+  return half8_t{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+}

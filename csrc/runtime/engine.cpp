@@ -130,6 +130,13 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   // blocks per weight tile group: 8B 41.6k -> 59.0k, 70B 6.3k -> 6.9k prompt tok/s at 64 x 512
   // prompts), 512 when stages pipeline the chunks (finer chunks overlap the stages) or on CPU
   if (!j.has("prefill_chunk")) chunk_ = (S_ == 1 && j.get_str("backend", "hip") != "cpu") ? 2048 : 512;
+  // KV cache element type: "f16" (default) or "fp8" (OCP e4m3 bytes: half the KV bytes per decode
+  // step and twice the tokens per GiB; HIP backend, fused decode + flash prefill attention)
+  const std::string kv_dtype = j.get_str("kv_dtype", "f16");
+  if (kv_dtype != "f16" && kv_dtype != "fp8") throw std::runtime_error("kv_dtype must be f16 or fp8");
+  const bool kv_fp8 = kv_dtype == "fp8";
+  if (kv_fp8 && (j.get_str("backend", "hip") == "cpu" || !j.get_bool("fused_attn", true) || !j.get_bool("prefill_flash", true)))
+    throw std::runtime_error("kv_dtype fp8 needs the HIP backend with fused_attn and prefill_flash");
   std::vector<int> devices(S_);
   for (int s = 0; s < S_; ++s) devices[s] = s;
   if (j.has("devices")) {
@@ -198,7 +205,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     int lmax = 1;
     for (auto& e : dev_w) {
       const int layers = std::max(1, dev_l[e.first]);
-      const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : 2.0);
+      const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : kv_fp8 ? 1.0 : 2.0);
       const double reserve =
           dev_n[e.first] * (4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4);
       const double budget = frac * cap_bytes - e.second - reserve;
@@ -290,6 +297,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.prefill_gemm_v = j.get_int("prefill_gemm_v", 2);
   so.deterministic = j.get_bool("deterministic", false);
   so.prefill_flash = j.get_bool("prefill_flash", true);
+  so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";
   so.fused_norm = j.get_bool("fused_norm", false) && !so.deterministic;   // its sums of squares are atomics
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);

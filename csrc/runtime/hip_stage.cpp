@@ -471,7 +471,7 @@ void HipStage::alloc_runtime() {
   const int n_slots = NM * B;
   max_pages_ = opt_.max_ctx / 64;
   n_pages_ = opt_.kv_pages > 0 ? opt_.kv_pages : n_slots * max_pages_;
-  const size_t per = (size_t)(n_pages_ + 1) * Hkv * 64 * Dp_ * 2;
+  const size_t per = (size_t)(n_pages_ + 1) * Hkv * 64 * Dp_ * kv_eb();
   for (size_t i = 0; i < layers_.size(); ++i) {
     kc_.push_back((f16*)zalloc(per));
     vc_.push_back((f16*)zalloc(per));
@@ -540,15 +540,15 @@ void HipStage::set_block_table(const std::vector<int32_t>& t) {
 }
 
 // KV of one slot: per layer the first ceil(n_tok / 64) pages of K, then of V, each page
-// [Hkv][64][Dp] (K) / [Hkv][Dp][64] (V) f16, located through the slot's block-table row
+// [Hkv][64][Dp] (K) / [Hkv][Dp][64] (V) f16 (or e4m3 bytes), located through the slot's block-table row
 size_t HipStage::kv_state_bytes(int n_tok) const {
-  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * kv_eb();
   return kc_.size() * 2 * (size_t)((n_tok + 63) / 64) * page;
 }
 
 void HipStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
   HIP_OK(hipSetDevice(spec_.device));
-  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * kv_eb();
   const int np = (n_tok + 63) / 64;
   const size_t base = out.size();
   out.resize(base + kv_state_bytes(n_tok));
@@ -567,7 +567,7 @@ void HipStage::kv_export(int slot, int n_tok, std::vector<uint8_t>& out) {
 void HipStage::kv_import(int slot, int n_tok, const uint8_t* data, size_t bytes) {
   if (bytes != kv_state_bytes(n_tok)) throw std::runtime_error("kv_import: size mismatch");
   HIP_OK(hipSetDevice(spec_.device));
-  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * 2;
+  const size_t page = (size_t)cfg_.n_head_kv * 64 * Dp_ * kv_eb();
   const int np = (n_tok + 63) / 64;
   HIP_OK(hipStreamSynchronize(stream_));
   for (size_t li = 0; li < kc_.size(); ++li)
@@ -767,6 +767,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
     dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
     dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
+    dp.kv_fp8 = opt_.kv_fp8;
     dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
     dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
     if (qkv_deferred) { dp.ssq = ssq_; dp.eps = cfg_.eps; dp.d_model = d; dp.bias = L.qkv_bias; }
@@ -776,12 +777,13 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     rp.qkv = qkv_; rp.ldqkv = qkv_n_; rp.M = M; rp.Hq = cfg_.n_head; rp.Hkv = cfg_.n_head_kv;
     rp.hd = cfg_.head_dim; rp.Dp = Dp_; rp.pos = pos; rp.slot = slot; rp.block_table = block_table_;
     rp.max_pages = max_pages_; rp.rope_cs = rope_cs_; rp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
-    rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li];
+    rp.q_out = q_; rp.k_cache = kc_[li]; rp.v_cache = vc_[li]; rp.kv_fp8 = opt_.kv_fp8;
     launch_rope_kv(rp, st);
     if (!decode && opt_.prefill_flash) {
       PrefillAttnParams pa{};
       pa.q = q_; pa.pos = pos; pa.slot = slot; pa.block_table = block_table_; pa.max_pages = max_pages_;
       pa.k_cache = kc_[li]; pa.v_cache = vc_[li]; pa.Hq = cfg_.n_head; pa.Hkv = cfg_.n_head_kv;
+      pa.kv_fp8 = opt_.kv_fp8;
       pa.hd = cfg_.head_dim; pa.Dp = Dp_; pa.out = attn_; pa.ldo = Ko_;
       const int bt = prefill_attn_rows_per_tile(cfg_.n_head / cfg_.n_head_kv);
       auto add_rows = [&](int row0, int T) {
@@ -814,6 +816,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     } else {
     AttnParams ap{};
     ap.q = q_; ap.kvlen = kvlen; ap.slot = slot; ap.block_table = block_table_; ap.max_pages = max_pages_;
+    if (opt_.kv_fp8) throw std::runtime_error("kv_dtype fp8: the unfused attention path reads f16 pages");
     ap.k_cache = kc_[li]; ap.v_cache = vc_[li]; ap.M = M; ap.Hq = cfg_.n_head; ap.Hkv = cfg_.n_head_kv;
     ap.hd = cfg_.head_dim; ap.Dp = Dp_; ap.max_kv = opt_.max_ctx; ap.out = attn_; ap.ldo = Ko_;
     if (decode) {

@@ -98,6 +98,7 @@ struct RopeKvParams {
   f16* q_out;            // [M][Hq][Dp]
   f16* k_cache;          // pages: [n_pages][Hkv][64][Dp]
   f16* v_cache;          // pages: [n_pages][Hkv][Dp][64] (transposed)
+  int kv_fp8 = 0;        // caches hold e4m3 bytes (same element layout, 1 byte each)
 };
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st);
 
@@ -136,6 +137,7 @@ struct PrefillAttnParams {
   int M = 0;                     // rows of the chunk (partial-buffer layout)
   int n_split = 1, split_pages = 1;   // KV splits (grid.z), pages per split
   float* o_part = nullptr; float* ml_part = nullptr;   // [n_split][M*Hq][Dp], [n_split][M*Hq][2]
+  int kv_fp8 = 0;                // caches hold e4m3 bytes (kv_dtype "fp8")
   int n_tiles;
   uint32_t tiles[kPrefillAttnMaxTiles];
 };
@@ -162,6 +164,7 @@ struct DecodeAttnParams {
   // deferred RMSNorm of the qkv GEMV (nullptr: qkv already final): q|k|v = rsqrt(ssq[t] / d + eps)
   // * qkv + bias (bias optional, [q|k|v])
   const float* ssq = nullptr; float eps = 0.f; int d_model = 0; const float* bias = nullptr;
+  int kv_fp8 = 0;                  // caches hold e4m3 bytes (kv_dtype "fp8")
 };
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
 

@@ -27,6 +27,7 @@ struct StageOptions {
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
   int prefill_gemm_v = 2;    // 2: 128 x 256 workgroup tiles (launch_gemm2); 1: 64 x 64 tiles
   bool prefill_flash = true; // prompt chunks: the LDS-tiled prefill flash attention (attn_prefill.hip)
+  bool kv_fp8 = false;       // kv_dtype "fp8": KV pages hold OCP e4m3 bytes
   int kv_pages = 0;          // KV pool pages per stage (64 tokens each; 0: n_slots x max_ctx / 64)
   bool deterministic = false;  // split-K and MoE partials reduced in a fixed order (no float atomics
                                // on shared outputs): bitwise-reproducible logits, PP=1 == PP=S

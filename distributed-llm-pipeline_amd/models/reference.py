@@ -34,6 +34,7 @@ class RefLlama:
             self.t["output.weight"] = self.t["token_embd.weight"]
         self.cache_k = [None] * self.L
         self.cache_v = [None] * self.L
+        self.kv_round = None   # optional f(t) applied to new K (after RoPE) and V before caching
 
     @classmethod
     def from_gguf(cls, path: str, dtype=torch.float32, device="cpu"):
@@ -99,6 +100,8 @@ class RefLlama:
                 q, k, v = q + t[p + "attn_q.bias"], k + t[p + "attn_k.bias"], v + t[p + "attn_v.bias"]
             q, k, v = q.view(T, H, hd), k.view(T, Hk, hd), v.view(T, Hk, hd)
             q, k = self.rope(q, pos), self.rope(k, pos)
+            if self.kv_round is not None:   # e.g. the fp8 KV cache's rounding
+                k, v = self.kv_round(k), self.kv_round(v)
             if self.cache_k[i] is None or start_pos == 0:
                 self.cache_k[i], self.cache_v[i] = k, v
             else:

@@ -469,3 +469,12 @@ def test_cpu_device_speed_probe_partition(native, model_dir):
         assert st[0]["layer_begin"] == 0 and st[0]["layer_end"] == st[1]["layer_begin"]
         out, _ = eng.generate(prompts, 6)
     assert out == ref
+
+
+def test_fp8_kv_needs_hip_backend(native, model_dir):
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with pytest.raises(RuntimeError, match="kv_dtype fp8"):
+        Engine(gguf=path, backend="cpu", max_ctx=128, kv_dtype="fp8")
+    with pytest.raises(RuntimeError, match="kv_dtype must be"):
+        Engine(gguf=path, backend="cpu", max_ctx=128, kv_dtype="int4")

@@ -44,6 +44,64 @@ def test_engine_matches_reference(cuda, native, model_dir, name, ftype):
             assert nmse(lg, rl) < 2e-4, (step, nmse(lg, rl))
 
 
+def _fp8_round(t):
+    return t.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(t.dtype)
+
+
+@pytest.mark.parametrize("name,ftype", [("tiny-gqa", "Q8_0"), ("tiny-l3", "Q6_K"), ("tiny-qwen2", "Q4_K_M")])
+def test_fp8_kv_cache_matches_reference(cuda, native, model_dir, name, ftype):
+    """kv_dtype="fp8" (OCP e4m3 KV pages: prefill flash attention + fused decode attention, paged)
+    against the fp32 oracle whose cached K / V are rounded to e4m3 the same way, and close to the f16
+    cache's logits."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, name, ftype)
+    ref = RefLlama.from_gguf(path)
+    ref.kv_round = _fp8_round
+    prompt = [int(t) for t in np.random.default_rng(2).integers(3, cfg.vocab, 45)]
+    with Engine(gguf=path, max_ctx=256, prefill_chunk=16, kv_dtype="fp8") as eng, \
+            Engine(gguf=path, max_ctx=256, prefill_chunk=16) as e16:
+        assert eng.info["kv_bytes_local"] * 2 == e16.info["kv_bytes_local"]
+        eng.start([prompt])
+        e16.start([prompt])
+        ref.reset()
+        rl = ref.forward(prompt, 0)[-1].numpy()
+        assert nmse(eng.logits()[0], rl) < 5e-4, nmse(eng.logits()[0], rl)
+        assert nmse(eng.logits()[0], e16.logits()[0]) < 2e-2
+        pos = len(prompt)
+        for step in range(6):
+            tok = eng.tokens()[0][-1]
+            eng.decode(1)
+            rl = ref.forward([tok], pos)[-1].numpy()
+            pos += 1
+            assert nmse(eng.logits()[0], rl) < 5e-4, (step, nmse(eng.logits()[0], rl))
+
+
+def test_fp8_kv_cache_checkpoint_and_batch(cuda, native, model_dir, tmp_path):
+    """fp8 pages survive save_state / load_state byte for byte, and a micro-batch of 4 paged
+    sequences gives each sequence's single-stream tokens."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    rng = np.random.default_rng(4)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (70, 5, 33, 130)]
+    kw = dict(gguf=path, max_ctx=512, n_mb=1, mb_size=4, prefill_chunk=64, kv_dtype="fp8")
+    with Engine(**kw) as eng:
+        eng.start(prompts)
+        eng.decode(4)
+        eng.save_state(str(tmp_path / "st"))
+        eng.decode(5)
+        full = eng.tokens()
+    with Engine(**kw) as eng:
+        eng.load_state(str(tmp_path / "st"))
+        eng.decode(5)
+        assert eng.tokens() == full
+    alone = []
+    with Engine(gguf=path, max_ctx=512, prefill_chunk=64, kv_dtype="fp8") as eng:
+        for p in prompts:
+            alone.append(eng.generate([p], 10)[0][0])
+    assert full == alone
+
+
 @pytest.mark.parametrize("name,ftype", [("tiny-gqa", "Q4_K_M"), ("tiny-qwen2", "Q8_0"), ("tiny-moe", "Q8_0")])
 def test_fused_norm_matches_reference(cuda, native, model_dir, name, ftype):
     """fused_norm=true (deferred RMSNorm in the qkv / gate-up GEMVs, applied by the decode attention
