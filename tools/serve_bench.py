@@ -9,6 +9,7 @@ p50/p90 of time-to-first-token and of whole-request latency.
     python tools/serve_bench.py --synthetic llama3-8b --ftype Q4_K_M --clients 16 --requests 4
 """
 import argparse
+import asyncio
 import json
 import os
 import random
@@ -82,12 +83,37 @@ def run(args, continuous: bool):
                     lat.append((t_end - t_start) * 1e3)
                     ntok[0] += n
 
+        async def aclient(ci, ac):
+            rng = random.Random(1000 + ci)
+            for _ in range(args.requests):
+                prompt = " ".join(rng.choice(words) for _ in range(rng.randint(4, args.max_prompt_words)))
+                n = rng.randint(args.min_new, args.max_new)
+                t_start = time.time()
+                first = None
+                async with ac.stream("POST", url + "/chat", json={"prompt": prompt, "n_predict": n}, timeout=600) as r:
+                    async for line in r.aiter_lines():
+                        if first is None and line.startswith("data:") and '"token"' in line:
+                            first = time.time()
+                t_end = time.time()
+                ttft.append(((first or t_end) - t_start) * 1e3)
+                lat.append((t_end - t_start) * 1e3)
+                ntok[0] += n
+
+        async def amain():
+            limits = httpx.Limits(max_connections=args.clients + 4, max_keepalive_connections=args.clients + 4)
+            async with httpx.AsyncClient(limits=limits) as ac:
+                await asyncio.gather(*[aclient(i, ac) for i in range(args.clients)])
+
         t0 = time.time()
-        th = [threading.Thread(target=client, args=(i,)) for i in range(args.clients)]
-        [t.start() for t in th]
-        [t.join() for t in th]
+        if args.client == "async":   # one event loop: no GIL contention between 64 reader threads
+            asyncio.run(amain())
+        else:
+            th = [threading.Thread(target=client, args=(i,)) for i in range(args.clients)]
+            [t.start() for t in th]
+            [t.join() for t in th]
         wall = time.time() - t0
-        return dict(mode="continuous" if continuous else "batch-per-run", requests=len(lat),
+        return dict(mode="continuous" if continuous else "batch-per-run", client=args.client, slots=args.mb_size,
+                    clients=args.clients, requests=len(lat),
                     gen_tok_s=round(ntok[0] / wall, 1), wall_s=round(wall, 2),
                     ttft_p50_ms=round(pct(ttft, 0.5), 1), ttft_p90_ms=round(pct(ttft, 0.9), 1),
                     latency_p50_ms=round(pct(lat, 0.5), 1), latency_p90_ms=round(pct(lat, 0.9), 1))
@@ -113,6 +139,8 @@ def main():
     ap.add_argument("--min-new", type=int, default=16)
     ap.add_argument("--max-new", type=int, default=128)
     ap.add_argument("--modes", default="continuous,batch")
+    ap.add_argument("--client", default="async", choices=["async", "threads"],
+                    help="async: all streams on one asyncio loop (default); threads: one thread per client")
     args = ap.parse_args()
     for m in args.modes.split(","):
         print(json.dumps(run(args, m == "continuous")), flush=True)
