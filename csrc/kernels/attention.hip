@@ -207,8 +207,11 @@ constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
 
 // F8: the KV pages hold e4m3 bytes (kv_dtype "fp8"): half the KV bytes per step; fragments are
 // loaded raw (8 bytes per 8 keys / dims), kept raw through the prefetch, converted to f16 at use
-template <int DP, bool F8>
-__global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
+// PF: each wave loads its next chunk before the current chunk's math (short contexts: one split,
+// latency-bound); without it the kernel needs ~40 % fewer VGPRs (occupancy 3 instead of 2), which
+// the many-split long contexts need more (8B 32K mb8: 1019 vs 960 tok/s)
+template <int DP, bool F8, bool PF>
+__device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
   auto cvt = [](const KR& r) -> half8_t {
     if constexpr (F8) return f8x8_to_h8(r);
@@ -256,30 +259,36 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     const int hs = rvalid ? h : kvh * G;          // idle MFMA columns read a valid head, then zero
     // bias / no-bias as two straight-line bodies: a bias branch inside the loop split the loads
     // into per-kk groups, each waited for before the next was issued
+    // two k-slices per batch of loads: all KK at once peaked at ~180 VGPRs for DP=128 (occupancy 2)
+    constexpr int KH = KK < 2 ? KK : 2;
     auto build = [&](auto with_bias) {
       constexpr bool HB = decltype(with_bias)::value;
-      float4 xa[KK][2], ca[KK][2], ba[KK][2];
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
+      for (int k0 = 0; k0 < KK; k0 += KH) {
+      float4 xa[KH][2], ca[KH][2], ba[KH][2];
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        const int kk = k0 + kh;
         const int d0 = 32 * kk + 8 * q4;
         const int dl = d0 < p.hd ? d0 : 0;
         const float4* xs = reinterpret_cast<const float4*>(row + hs * p.hd + dl);
         const float4* cp = reinterpret_cast<const float4*>(cs + dl / 2);
-        xa[kk][0] = xs[0]; xa[kk][1] = xs[1];
-        ca[kk][0] = cp[0]; ca[kk][1] = cp[1];
+        xa[kh][0] = xs[0]; xa[kh][1] = xs[1];
+        ca[kh][0] = cp[0]; ca[kh][1] = cp[1];
         if constexpr (HB) {
           const float4* bs = reinterpret_cast<const float4*>(p.bias + hs * p.hd + dl);
-          ba[kk][0] = bs[0]; ba[kk][1] = bs[1];
+          ba[kh][0] = bs[0]; ba[kh][1] = bs[1];
         }
       }
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
+      for (int kh = 0; kh < KH; ++kh) {
+        const int kk = k0 + kh;
         const int d0 = 32 * kk + 8 * q4;
         const bool ok = rvalid && d0 < p.hd;
-        float x[8] = {xa[kk][0].x, xa[kk][0].y, xa[kk][0].z, xa[kk][0].w, xa[kk][1].x, xa[kk][1].y, xa[kk][1].z, xa[kk][1].w};
-        const float c[8] = {ca[kk][0].x, ca[kk][0].y, ca[kk][0].z, ca[kk][0].w, ca[kk][1].x, ca[kk][1].y, ca[kk][1].z, ca[kk][1].w};
+        float x[8] = {xa[kh][0].x, xa[kh][0].y, xa[kh][0].z, xa[kh][0].w, xa[kh][1].x, xa[kh][1].y, xa[kh][1].z, xa[kh][1].w};
+        const float c[8] = {ca[kh][0].x, ca[kh][0].y, ca[kh][0].z, ca[kh][0].w, ca[kh][1].x, ca[kh][1].y, ca[kh][1].z, ca[kh][1].w};
         if constexpr (HB) {
-          const float b[8] = {ba[kk][0].x, ba[kk][0].y, ba[kk][0].z, ba[kk][0].w, ba[kk][1].x, ba[kk][1].y, ba[kk][1].z, ba[kk][1].w};
+          const float b[8] = {ba[kh][0].x, ba[kh][0].y, ba[kh][0].z, ba[kh][0].w, ba[kh][1].x, ba[kh][1].y, ba[kh][1].z, ba[kh][1].w};
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = fmaf(nrs, x[j], b[j]);
         } else {
@@ -293,6 +302,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
           v[j + 1] = ok ? (f16)((x[j] * c[j + 1] + x[j + 1] * c[j]) * p.q_scale) : (f16)0.f;
         }
         qf[kk] = v;
+      }
       }
     };
     if (p.bias) build(std::true_type{});
@@ -346,7 +356,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
       vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
   };
   KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
-  if (wv < nch) load(wv, kA, vA);
+  if (PF && wv < nch) load(wv, kA, vA);   // in flight during the append
 
   if (owns) {
     const int page = bt[pos >> 6], idx = pos & 63;
@@ -482,14 +492,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     }
   };
   // waves take chunks wv, wv + 4, ...; the next chunk's loads are issued before this one's math
-  for (int ci = wv; ci < nch;) {
-    if (ci + 4 < nch) load(ci + 4, kB, vB);
-    step(ci, kA, vA);
-    ci += 4;
-    if (ci >= nch) break;
-    if (ci + 4 < nch) load(ci + 4, kA, vA);
-    step(ci, kB, vB);
-    ci += 4;
+  if constexpr (PF) {
+    for (int ci = wv; ci < nch;) {
+      if (ci + 4 < nch) load(ci + 4, kB, vB);
+      step(ci, kA, vA);
+      ci += 4;
+      if (ci >= nch) break;
+      if (ci + 4 < nch) load(ci + 4, kA, vA);
+      step(ci, kB, vB);
+      ci += 4;
+    }
+  } else {
+    for (int ci = wv; ci < nch; ci += 4) {
+      load(ci, kA, vA);
+      step(ci, kA, vA);
+    }
   }
   l_run += __shfl_xor(l_run, 16);
   l_run += __shfl_xor(l_run, 32);
@@ -587,6 +604,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams
     __hip_atomic_store(p.counters + (size_t)t * p.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int DP, bool F8>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) { attn_decode_body<DP, F8, true>(p); }
+// many-split long contexts: 3 workgroups per CU (occupancy, not per-wave latency, is what they need)
+template <int DP, bool F8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_decode_kernel_np(
+    const DecodeAttnParams p) {
+  attn_decode_body<DP, F8, false>(p);
+}
+
 }  // namespace mpk
 
 namespace mp {
@@ -609,15 +635,22 @@ void launch_attn_combine(const AttnParams& p, hipStream_t st) {
   else hipLaunchKernelGGL(mpk::attn_combine_kernel<64>, dim3(p.M * p.Hq), dim3(64), 0, st, p);
 }
 
-void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
+template <bool F8, bool PF>
+static void attn_decode_go(const DecodeAttnParams& p, hipStream_t st) {
   dim3 grid(p.M, p.Hkv, p.n_split);
-  if (p.kv_fp8) {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, true>), grid, dim3(256), 0, st, p);
+  if constexpr (PF) {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, F8>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, F8>), grid, dim3(256), 0, st, p);
   } else {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, false>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, false>), grid, dim3(256), 0, st, p);
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel_np<128, F8>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel_np<64, F8>), grid, dim3(256), 0, st, p);
   }
+}
+
+void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
+  const bool pf = p.n_split == 1;   // one split per (token, kv head): short contexts / wide batches
+  if (p.kv_fp8) pf ? attn_decode_go<true, true>(p, st) : attn_decode_go<true, false>(p, st);
+  else pf ? attn_decode_go<false, true>(p, st) : attn_decode_go<false, false>(p, st);
 }
 
 }  // namespace mp
