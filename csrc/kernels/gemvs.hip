@@ -1,0 +1,358 @@
+// Small-M decode GEMV ("gemvs", M <= 4: single-stream and tiny micro-batches).
+//
+// At M = 1 the v2 GEMV (gemv2.hip) is latency-bound, not bandwidth-bound: 7.3 us for a 9.4 MB
+// Llama-3-8B o-proj whose bytes need ~1.6 us, unchanged when the weights are MALL-resident
+// (profiles/r2u_prof_8b_mb1.txt, r2w_gemv_mall_hot_cold.txt).  Its per-super-block chain (x ring
+// -> LDS -> workgroup barrier -> dequant -> MFMA) and the split-K atomics cost round trips that a
+// batch of one cannot hide, and every projection needs a separate RMSNorm launch (4.6 us, 65 per
+// 8B token).  gemvs removes both:
+//
+//  * the workgroup stages ITS WHOLE k-range of x into LDS once (a prologue), so the weight loop
+//    has no barrier and no x loads: a wave issues its first NS super-blocks of weights before the
+//    prologue and then streams its k-slice through a register ring (MI355X guide: "GEMV / M <= 16
+//    decode weights ... load straight to VGPRs, deep unroll, late vmcnt");
+//  * the RMSNorm is fused into the prologue (NORM): every workgroup reduces sum(x^2) over the full
+//    f32 residual row (L2-resident, 16-32 KB) and stages f16(x * rsqrt(mean + eps) * gamma), the
+//    same rounding as the standalone rmsnorm kernel (elementwise.hip);
+//  * split-K runs INSIDE the workgroup (KSW waves per tile, partials reduced through LDS): the
+//    outputs are complete per workgroup, so STORE / SWIGLU need no zero-filled accumulator and
+//    ADD (the residual update of o / down) is a plain read-modify-write by the single owner --
+//    deterministic -- unless the host also splits K over grid.y (atomics).
+//
+//   grid (ceil(ntiles / G), nsplit)   block NW * 64 (NW = 8)
+//   wave w: tile blockIdx.x * G + w / KSW (KSW = NW / G), k-slice w % KSW of the workgroup's
+//   super-blocks [sbA, sbB) (split blockIdx.y)
+//
+// Layout: T16 chunks (csrc/runtime/qtypes.h, dequant.h): lane (g, r) holds weight column r;
+// MFMA i of a super-block covers k = 64 g + 8 i + j.  The A fragment of lane (g, r) is x[r][...]
+// for r < M, zero above (LDS holds M rows only).  C: lane (g, r) holds rows 4g + i: the M <= 4
+// valid rows are in lanes 0-15 (g = 0), acc[i] = row i, column r.
+#include "kcommon.h"
+#include "dequant.h"
+#include "../runtime/kernels_api.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+
+namespace mpk {
+using namespace mp;
+
+constexpr int GS_NW = 8;
+constexpr int GS_NT = GS_NW * 64;
+
+template <int PT, int EPI, int G, bool NORM>
+__global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const int nsplit) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB;
+  constexpr int KSW = GS_NW / G;
+  constexpr int NS = PT == P_F16 ? 2 : 4;
+  extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange]
+  __shared__ float red[GS_NW][64];
+  __shared__ float red_ss[GS_NW][4];
+  __shared__ float rs_s[4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int M = p.M;
+  const int sbA = blockIdx.y * p.sb_per_split;
+  const int sbB = min(sbA + p.sb_per_split, p.nsb);
+  if (sbA >= sbB) return;   // uniform over the workgroup
+  const int krange = (sbB - sbA) * 256;
+
+  // this wave's tile and contiguous k-slice [wA, wB) of the workgroup's super-blocks
+  const int gi = wave / KSW, ks = wave % KSW;
+  const int tile = blockIdx.x * G + gi;
+  const int per = (sbB - sbA + KSW - 1) / KSW;
+  const int wA = min(sbA + ks * per, sbB), wB = min(wA + per, sbB);
+  const bool live = tile < p.ntiles;
+  const __amdgpu_buffer_rsrc_t wsrc =
+      make_rsrc(p.W + ((size_t)min(tile, p.ntiles - 1) * p.nsb + wA) * CB, (uint32_t)(live ? (wB - wA) * CB : 0));
+  typename D::Raw ring[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) D::load(ring[s], BufSrc{wsrc, s * CB}, lane);   // past the range: zeros, no traffic
+
+  // ---- prologue: x of rows [0, M), k in [sbA*256, sbB*256) -> LDS as f16
+  if constexpr (NORM) {
+    const int d4 = p.d_norm >> 2;
+    const int k0 = sbA * 256, k1 = min(sbB * 256, p.d_norm);   // this workgroup's k-range (valid part)
+    if (M == 1 && d4 <= 4 * GS_NT) {
+      // one row of <= 8192: every float4 of the row loaded once, in one batch, and kept: the thread
+      // that reduced a chunk also stages it (no second pass over x)
+      float4 v[4], gm[4];
+      float ss = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = tid + u * GS_NT;
+        const bool in = c < d4, mine = in && 4 * c >= k0 && 4 * c < k1;
+        v[u] = in ? reinterpret_cast<const float4*>(p.Xf)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        gm[u] = mine ? reinterpret_cast<const float4*>(p.gamma)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+      ss = wave_sum(ss);
+      if (lane == 0) red_ss[wave][0] = ss;
+      // the k-range's zero tail (k >= d_norm, up to sbB * 256)
+      for (int c = k1 / 4 + tid; c < sbB * 64; c += GS_NT) *reinterpret_cast<u32x2*>(xs + 4 * c - k0) = u32x2{0u, 0u};
+      __syncthreads();
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < GS_NW; ++w) t += red_ss[w][0];
+      const float sc = rsqrtf(t / (float)p.d_norm + p.eps);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = tid + u * GS_NT;
+        if (c < d4 && 4 * c >= k0 && 4 * c < k1) {
+          const half2_t a = {(f16)(v[u].x * sc * gm[u].x), (f16)(v[u].y * sc * gm[u].y)};
+          const half2_t b = {(f16)(v[u].z * sc * gm[u].z), (f16)(v[u].w * sc * gm[u].w)};
+          *reinterpret_cast<u32x2*>(xs + 4 * c - k0) = u32x2{as_u32(a), as_u32(b)};
+        }
+      }
+    } else {
+      // pass 1: sum(x^2) over the full rows (d_norm f32, a multiple of 4), loads batched by 4
+      float ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (m < M) {
+          const float4* xr = reinterpret_cast<const float4*>(p.Xf + (size_t)m * p.ldxf);
+          for (int c0 = 0; c0 < d4; c0 += 4 * GS_NT) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int c = c0 + tid + u * GS_NT;
+              v[u] = c < d4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ss[m] += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        ss[m] = wave_sum(ss[m]);
+        if (lane == 0) red_ss[wave][m] = ss[m];
+      }
+      __syncthreads();
+      if (tid < 4) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < GS_NW; ++w) t += red_ss[w][tid];
+        rs_s[tid] = rsqrtf(t / (float)p.d_norm + p.eps);
+      }
+      __syncthreads();
+      // pass 2: this workgroup's k-range, f16(x * rs * gamma) (the rmsnorm kernel's rounding)
+      const int k8 = krange >> 3;
+      for (int c = tid; c < M * k8; c += GS_NT) {
+        const int m = c / k8, kl = (c - m * k8) * 8, kg = k0 + kl;
+        u32x4 o = {0u, 0u, 0u, 0u};
+        if (kg < p.d_norm) {
+          const float* xr = p.Xf + (size_t)m * p.ldxf + kg;
+          const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
+          const float4 ga = *reinterpret_cast<const float4*>(p.gamma + kg), gb = *reinterpret_cast<const float4*>(p.gamma + kg + 4);
+          const float sc = rs_s[m];
+          o = __builtin_bit_cast(u32x4, half8_t{(f16)(a.x * sc * ga.x), (f16)(a.y * sc * ga.y), (f16)(a.z * sc * ga.z),
+                                                (f16)(a.w * sc * ga.w), (f16)(b.x * sc * gb.x), (f16)(b.y * sc * gb.y),
+                                                (f16)(b.z * sc * gb.z), (f16)(b.w * sc * gb.w)});
+        }
+        *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = o;
+      }
+    }
+  } else {
+    // f16 activations [M][ldx] with a zero tail up to nsb * 256; loads batched by 4
+    const int k8 = krange >> 3, tot = M * k8;
+    for (int c0 = 0; c0 < tot; c0 += 4 * GS_NT) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + tid + u * GS_NT;
+        const int m = c / k8, kl = (c - m * k8) * 8;
+        if (c < tot) v[u] = *reinterpret_cast<const u32x4*>(p.X + (size_t)m * p.ldx + (size_t)sbA * 256 + kl);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + tid + u * GS_NT;
+        const int m = c / k8, kl = (c - m * k8) * 8;
+        if (c < tot) *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = v[u];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- weight stream: no barriers; slot s holds super-block wA + j + s
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const Consts kc = make_consts();
+  const f16* xrow = xs + (size_t)r * krange + t16_xoff(g, 0);   // valid for r < M only
+  const bool xr_ok = r < M;
+  auto step = [&](const int s, const int sbl) {   // sbl: super-block index relative to sbA
+    half8_t b[4];
+    D::template dequant<0>(ring[s], b, lane, kc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      half8_t a = {};
+      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 8 * i);
+      acc = mfma16x16x32(a, b[i], acc);
+    }
+    D::template dequant<1>(ring[s], b, lane, kc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      half8_t a = {};
+      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 32 + 8 * i);
+      acc = mfma16x16x32(a, b[i], acc);
+    }
+  };
+  const int n = wB - wA;
+  int j = 0;
+  for (; j + NS <= n; j += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      step(s, wA - sbA + j + s);
+      D::load(ring[s], BufSrc{wsrc, (j + s + NS) * CB}, lane);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (j + s < n) step(s, wA - sbA + j + s);
+
+  // ---- reduce the KSW k-slices of each tile, then the epilogue (one wave per tile)
+  float v[4];
+  if constexpr (KSW == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[i];
+  } else {
+    if (g == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave][i * 16 + r] = acc[i];
+    }
+    __syncthreads();
+    if (wave >= G) return;
+  }
+  // epilogue wave e = gi' handles tile blockIdx.x * G + e; lane -> (row i = lane >> 4, column r)
+  const int et = KSW == 1 ? tile : blockIdx.x * G + wave;
+  float val;
+  if constexpr (KSW == 1) {
+    // lane (g, r): rows 4g + i; only g = 0 is valid (M <= 4): move row i to lane 16 i + r
+    const int i = lane >> 4;
+    const float a0 = __shfl(v[0], r), a1 = __shfl(v[1], r), a2 = __shfl(v[2], r), a3 = __shfl(v[3], r);
+    val = i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : a3;
+  } else {
+    val = 0.f;
+#pragma unroll
+    for (int k = 0; k < KSW; ++k) val += red[wave * KSW + k][lane];
+  }
+  const int m = lane >> 4;
+  if (et >= p.ntiles) return;
+  if constexpr (EPI == EPI_SWIGLU) {
+    const float up = __shfl_xor(val, 8);
+    const int o = et * 8 + r;
+    if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(val) * up);
+  } else {
+    const int nc = et * 16 + r;
+    if (m < M && nc < p.n_valid) {
+      const float out = val + ((p.bias && blockIdx.y == 0) ? p.bias[nc] : 0.f);
+      float* dst = p.Y + (size_t)m * p.ldy + nc;
+      if constexpr (EPI == EPI_ATOMIC) {
+        if (nsplit == 1) *dst += out;   // single owner: plain read-modify-write (deterministic)
+        else unsafeAtomicAdd(dst, out);
+      } else {
+        *dst = out;
+      }
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+static int env_int(const char* k, int dflt) {
+  const char* e = getenv(k);
+  return e ? atoi(e) : dflt;
+}
+
+// Work split: G tiles per workgroup (KSW = 8 / G waves share each tile's k-range) and nsplit
+// k-splits over grid.y (ATOMIC only).  Aim: ~S_target super-blocks per wave, >= 512 workgroups
+// (two per CU), x k-range in LDS <= 96 KB.
+GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool deterministic) {
+  GemvsPlan pl;
+  const int s_target = env_int("MIPIPE_GEMVS_S", 16);   // 8B mb1 sweep (r4c): S 4 / 8 / 16 -> 468 / 499 / 502 tok/s
+  const int ks_needed = std::max(1, (nsb + s_target - 1) / s_target);
+  int G = ks_needed >= 8 ? 1 : ks_needed >= 5 ? 1 : ks_needed >= 3 ? 2 : ks_needed == 2 ? 4 : 8;
+  const int min_wg = env_int("MIPIPE_GEMVS_MINWG", 256);
+  while (G > 1 && (ntiles + G - 1) / G < min_wg) G >>= 1;
+  if (const int eg = env_int("MIPIPE_GEMVS_G", 0)) G = eg;
+  int nsplit = 1;
+  const bool can_split = epi == EPI_ATOMIC && !deterministic;
+  if (can_split && G == 1) {
+    while ((nsb + 8 * nsplit - 1) / (8 * nsplit) > s_target && (ntiles * nsplit) < 1024 && nsb / (2 * nsplit) >= 8)
+      nsplit *= 2;
+    if (const int es = env_int("MIPIPE_GEMVS_SPLIT", 0)) nsplit = es;
+  }
+  // LDS: M rows x the split's k-range of f16 x
+  auto lds_of = [&](int ns) { return (size_t)M * ((nsb + ns - 1) / ns) * 256 * 2; };
+  while (lds_of(nsplit) > 96 * 1024 && can_split) nsplit *= 2;
+  pl.G = G;
+  pl.sb_per_split = (nsb + nsplit - 1) / nsplit;
+  pl.nsplit = (nsb + pl.sb_per_split - 1) / pl.sb_per_split;
+  pl.lds = (size_t)M * pl.sb_per_split * 256 * 2;
+  return pl;
+}
+
+template <int PT, int EPI, int G, bool NORM>
+static void gemvs_go(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
+  static const bool attr = [] {   // dynamic LDS past the 64 KB default (gfx950: 160 KB per workgroup)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs_kernel<PT, EPI, G, NORM>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
+  }();
+  if (!attr && pl.lds > 60 * 1024) throw std::runtime_error("gemvs: cannot raise the dynamic LDS limit");
+  hipLaunchKernelGGL((mpk::gemvs_kernel<PT, EPI, G, NORM>), dim3((p.ntiles + G - 1) / G, pl.nsplit),
+                     dim3(mpk::GS_NT), pl.lds, st, p, pl.nsplit);
+}
+
+template <int PT, int EPI, bool NORM>
+static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
+  switch (pl.G) {
+    case 1: return gemvs_go<PT, EPI, 1, NORM>(p, pl, st);
+    case 2: return gemvs_go<PT, EPI, 2, NORM>(p, pl, st);
+    case 4: return gemvs_go<PT, EPI, 4, NORM>(p, pl, st);
+    case 8: return gemvs_go<PT, EPI, 8, NORM>(p, pl, st);
+    default: throw std::runtime_error("gemvs: G must be 1, 2, 4 or 8");
+  }
+}
+
+template <int PT>
+static void gemvs_pt(int epi, const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
+  const bool norm = p.Xf != nullptr;
+  switch (epi) {
+    case EPI_STORE: return norm ? gemvs_g<PT, EPI_STORE, true>(p, pl, st) : gemvs_g<PT, EPI_STORE, false>(p, pl, st);
+    case EPI_ATOMIC: return norm ? gemvs_g<PT, EPI_ATOMIC, true>(p, pl, st) : gemvs_g<PT, EPI_ATOMIC, false>(p, pl, st);
+    case EPI_SWIGLU: return norm ? gemvs_g<PT, EPI_SWIGLU, true>(p, pl, st) : gemvs_g<PT, EPI_SWIGLU, false>(p, pl, st);
+  }
+}
+
+void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G, int force_split) {
+  if (p.M < 1 || p.M > 4) throw std::runtime_error("launch_gemvs: M must be 1..4");
+  if (p.Xf && (p.d_norm <= 0 || (p.d_norm & 7) || p.d_norm > p.nsb * 256))
+    throw std::runtime_error("launch_gemvs: fused RMSNorm needs d_norm a multiple of 8 within the padded K");
+  if (!p.Xf && !p.X) throw std::runtime_error("launch_gemvs: no input");
+  GemvsPlan pl = plan_gemvs(p.ntiles, p.nsb, p.M, epi, p.Xf != nullptr, deterministic);
+  if (force_G) pl.G = force_G;
+  if (force_split) {   // tests: an explicit k-split over grid.y
+    pl.sb_per_split = (p.nsb + force_split - 1) / force_split;
+    pl.nsplit = (p.nsb + pl.sb_per_split - 1) / pl.sb_per_split;
+    pl.lds = (size_t)p.M * pl.sb_per_split * 256 * 2;
+  }
+  if (pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs: x k-range does not fit LDS");
+  if (epi != EPI_ATOMIC && pl.nsplit != 1) throw std::runtime_error("launch_gemvs: only ATOMIC splits K");
+  p.sb_per_split = pl.sb_per_split;
+  switch (ptype) {
+    case P_Q4_K: gemvs_pt<P_Q4_K>(epi, p, pl, st); break;
+    case P_Q5_K: gemvs_pt<P_Q5_K>(epi, p, pl, st); break;
+    case P_Q6_K: gemvs_pt<P_Q6_K>(epi, p, pl, st); break;
+    case P_Q8_0: gemvs_pt<P_Q8_0>(epi, p, pl, st); break;
+    case P_Q4_0: gemvs_pt<P_Q4_0>(epi, p, pl, st); break;
+    case P_F16: gemvs_pt<P_F16>(epi, p, pl, st); break;
+    default: throw std::runtime_error("launch_gemvs: unknown packed type");
+  }
+}
+
+}  // namespace mp

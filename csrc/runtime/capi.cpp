@@ -226,6 +226,23 @@ int mp_op_gemv_fused(int ptype, int epi, const void* W, int ntiles, int nsb, con
   API_CATCH(-1)
 }
 
+// small-M GEMV (gemvs.hip, M <= 4): Xf/gamma fuse the RMSNorm of the f32 rows Xf; ATOMIC adds into Y
+// (read-modify-write at one k-split, atomics above); G / nsplit 0 = the launcher's own plan
+int mp_op_gemvs(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+                int ldy, void* H, int ldh, int n_valid, const void* Xf, int ldxf, const void* gamma, float eps,
+                int d_norm, const void* bias, int G, int nsplit, int deterministic, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  p.Xf = (const float*)Xf; p.ldxf = ldxf; p.gamma = (const float*)gamma; p.eps = eps; p.d_norm = d_norm;
+  p.bias = (const float*)bias;
+  launch_gemvs(ptype, epi, p, deterministic != 0, (hipStream_t)stream, G, nsplit);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_rmsnorm(const void* x, int ldx, const void* w, int d, float eps, void* out, int ldo, int M, void* stream) {
   API_TRY
   launch_rmsnorm((const float*)x, ldx, (const float*)w, d, eps, (f16*)out, ldo, M, nullptr, 0, (hipStream_t)stream);

@@ -299,6 +299,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.prefill_flash = j.get_bool("prefill_flash", true);
   so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";
   so.fused_norm = j.get_bool("fused_norm", false) && !so.deterministic;   // its sums of squares are atomics
+  so.small_gemv = j.get_bool("small_gemv", true);
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);
 

@@ -741,6 +741,30 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
                              const int32_t* slot, bool decode, hipStream_t st) {
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
+  if (small_path(M)) {
+    // gemvs: RMSNorms fused into the qkv / gate-up GEMVs, complete outputs per workgroup (q|k|v
+    // stored with its bias, o / down added into the residual by their single owner)
+    for (const MatSeg& s : L.qkv)
+      gemv_small(s.m, EPI_STORE, nullptr, 0, x, L.attn_norm, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N,
+                 L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st);
+    attention(li, M, pos, kvlen, slot, decode, st, false);
+    gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
+    if (L.moe) {
+      launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, moe_logits_, (int64_t)M * 64, st);
+      moe_ffn(L, M, st, x);
+      return;
+    }
+    if (L.fused_gateup) {
+      gemv_small(L.gateup, EPI_SWIGLU, nullptr, 0, x, L.ffn_norm, M, nullptr, 0, h_, Kff_, cfg_.d_ff, nullptr, st);
+    } else {
+      const int F = cfg_.d_ff;
+      gemv_small(L.gate, EPI_STORE, nullptr, 0, x, L.ffn_norm, M, gu_, 2 * F, nullptr, 0, F, nullptr, st);
+      gemv_small(L.up, EPI_STORE, nullptr, 0, x, L.ffn_norm, M, gu_ + F, 2 * F, nullptr, 0, F, nullptr, st);
+      launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
+    }
+    gemv_small(L.down, EPI_ATOMIC, h_, Kff_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
+    return;
+  }
   // M <= 4 (fuse_norm): the RMSNorms are folded into the consuming GEMVs (gemv2.hip deferred
   // norm).  qkv: the split-K GEMV publishes per-row sums of squares to ssq_ and the fused decode
   // attention applies rsqrt and the bias when it reads q|k|v.  The o-proj then clears ssq_ + the
@@ -762,6 +786,44 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     for (const MatSeg& s : L.qkv)
       gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
   }
+  attention(li, M, pos, kvlen, slot, decode, st, qkv_deferred);
+  if (small) {
+    GemvParams z{};
+    z.zero = ssq_; z.zero_n = 64 + (int64_t)M * qkv_n_;
+    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st, &z);
+  } else {
+    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
+    if (opt_.fused_norm && li + 1 == (int)layers_.size())
+      HIP_OK(hipMemsetAsync(ssq_, 0, (64 + (size_t)M * qkv_n_) * 4, st));
+  }
+  const bool ffn_fused = small && !L.moe;
+  // MoE: the same launch clears the router logits, which the router GEMV then accumulates split-K
+  if (!ffn_fused)
+    launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
+  if (L.moe) {
+    moe_ffn(L, M, st, x);
+    return;
+  }
+  GemvParams fx = nx;
+  fx.gamma = L.ffn_norm;
+  const GemvParams* fe = ffn_fused ? &fx : nullptr;
+  const f16* xin = ffn_fused ? nullptr : xn_;
+  if (L.fused_gateup) {
+    gemv(L.gateup, EPI_SWIGLU, xin, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st, fe);
+  } else {
+    const int F = cfg_.d_ff;
+    gemv(L.gate, EPI_STORE, xin, Kd_, M, gu_, 2 * F, nullptr, 0, F, false, st, fe);
+    gemv(L.up, EPI_STORE, xin, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st, fe);
+    launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
+  }
+  gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
+}
+
+void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
+                         hipStream_t st, bool qkv_deferred) {
+  const LayerW& L = layers_[li];
+  const int d = cfg_.d_model;
+  (void)d;
   if (decode && opt_.fused_attn) {
     DecodeAttnParams dp{};
     dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
@@ -846,36 +908,15 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     }
     }
   }
-  if (small) {
-    GemvParams z{};
-    z.zero = ssq_; z.zero_n = 64 + (int64_t)M * qkv_n_;
-    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st, &z);
-  } else {
-    gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
-    if (opt_.fused_norm && li + 1 == (int)layers_.size())
-      HIP_OK(hipMemsetAsync(ssq_, 0, (64 + (size_t)M * qkv_n_) * 4, st));
-  }
-  const bool ffn_fused = small && !L.moe;
-  // MoE: the same launch clears the router logits, which the router GEMV then accumulates split-K
-  if (!ffn_fused)
-    launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
-  if (L.moe) {
-    moe_ffn(L, M, st, x);
-    return;
-  }
-  GemvParams fx = nx;
-  fx.gamma = L.ffn_norm;
-  const GemvParams* fe = ffn_fused ? &fx : nullptr;
-  const f16* xin = ffn_fused ? nullptr : xn_;
-  if (L.fused_gateup) {
-    gemv(L.gateup, EPI_SWIGLU, xin, Kd_, M, nullptr, 0, h_, Kff_, cfg_.d_ff, false, st, fe);
-  } else {
-    const int F = cfg_.d_ff;
-    gemv(L.gate, EPI_STORE, xin, Kd_, M, gu_, 2 * F, nullptr, 0, F, false, st, fe);
-    gemv(L.up, EPI_STORE, xin, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st, fe);
-    launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
-  }
-  gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
+}
+
+void HipStage::gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, const float* Xf, const float* gamma,
+                          int M, float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st) {
+  GemvParams p{};
+  p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
+  p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid; p.bias = bias;
+  if (Xf) { p.Xf = Xf; p.ldxf = cfg_.d_model; p.gamma = gamma; p.eps = cfg_.eps; p.d_norm = cfg_.d_model; }
+  launch_gemvs(m.ptype, epi, p, opt_.deterministic, st);
 }
 
 bool HipStage::fuse_norm(int M) const { return opt_.fused_norm && M <= 4; }
@@ -884,8 +925,12 @@ void HipStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t sa
   const int d = cfg_.d_model;
   // (the LM head keeps the standalone norm: the deferred-norm GEMV variant needs ~50 more VGPRs,
   // which halves the head's occupancy: 90.5 vs 72.7 + 4.6 us at 8B, profiles/r2h_prof_8b_mb1.txt)
-  launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
-  gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
+  if (small_path(M)) {
+    gemv_small(out_, EPI_STORE, nullptr, 0, x, out_norm_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, nullptr, st);
+  } else {
+    launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+    gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
+  }
   const bool pen = penalties_on() && hist_;
   int32_t* hist = pen ? hist_ + (size_t)mb * opt_.mb_size * hist_n_ : nullptr;
   if (pen) {

@@ -127,6 +127,12 @@ class HipStage : public Stage {
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
   bool fuse_norm(int M) const;
+  void attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
+                 hipStream_t st, bool qkv_deferred);
+  bool small_path(int M) const { return opt_.small_gemv && M <= 4; }
+  // gemvs (M <= 4): Xf != nullptr fuses the RMSNorm of the f32 rows Xf with gamma
+  void gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, const float* Xf, const float* gamma, int M,
+                  float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st);
   size_t kv_eb() const { return opt_.kv_fp8 ? 1 : 2; }   // bytes per cached K/V element
   int det_splits(int ntiles, int nsb, int M, int epi, bool allow_split = true) const;   // RMSNorm folded into the consuming GEMVs at this row count
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,

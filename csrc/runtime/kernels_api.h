@@ -41,6 +41,13 @@ struct GemvParams {
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
+// Small-M GEMV (gemvs.hip, M <= 4): whole k-range of x staged in LDS once per workgroup (fused
+// RMSNorm when p.Xf is set), split-K inside the workgroup; STORE / SWIGLU write complete outputs,
+// EPI_ATOMIC adds into Y by read-modify-write (nsplit 1, deterministic) or atomics (nsplit > 1)
+struct GemvsPlan { int G = 1, nsplit = 1, sb_per_split = 0; size_t lds = 0; };
+GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool deterministic);
+void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G = 0,
+                  int force_split = 0);
 void set_gemv_tpw(int tiles_per_wave);    // M > 32 tiles per wave: 0 = auto, 1, 2 (tuning knob)
 int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)

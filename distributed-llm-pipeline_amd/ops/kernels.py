@@ -81,6 +81,33 @@ def gemv(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
     return y
 
 
+def gemv_small(w: PackedWeight, epi: int = EPI_STORE, *, x: torch.Tensor | None = None,
+               xf: torch.Tensor | None = None, gamma: torch.Tensor | None = None, eps: float = 1e-5,
+               bias: torch.Tensor | None = None, y: torch.Tensor | None = None, G: int = 0, nsplit: int = 0,
+               deterministic: bool = False) -> torch.Tensor:
+    """Small-M decode GEMV (gemvs.hip, M <= 4), the engine's single-stream path.
+    xf/gamma: fused RMSNorm -- the GEMV runs on f16(xf * rsqrt(mean(xf^2) + eps) * gamma), the
+    standalone rmsnorm kernel's rounding.  ATOMIC adds into `y`.  G (tiles per workgroup) and nsplit
+    (k-splits over the grid, ATOMIC only) override the launcher's plan (0 = auto)."""
+    if xf is not None:
+        assert xf.dtype == torch.float32 and xf.is_contiguous()
+        M, d = xf.shape
+    else:
+        assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
+        M, d = x.shape[0], 0
+    F = w.n // 2
+    if epi == EPI_SWIGLU:
+        h = torch.zeros(M, F, dtype=torch.float16, device=w.dev.device) if y is None else y
+        Y, ldy, H, ldh, nv = None, 0, h, h.stride(0), F
+    else:
+        y = torch.zeros(M, w.n, dtype=torch.float32, device=w.dev.device) if y is None else y
+        Y, ldy, H, ldh, nv = y, y.stride(0), None, 0, w.n
+    N.check(N.lib().mp_op_gemvs(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad if x is not None else 0,
+                                M, _ptr(Y), ldy, _ptr(H), ldh, nv, _ptr(xf), d, _ptr(gamma), eps, d, _ptr(bias),
+                                G, nsplit, int(deterministic), _stream()), "gemv_small")
+    return h if epi == EPI_SWIGLU else y
+
+
 def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor | None = None,
          n_valid: int | None = None, v: int = 2) -> torch.Tensor:
     """Prefill GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC = single-owner add).
