@@ -86,7 +86,9 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   if (j.get_bool("trace", false)) enable_trace(true);
   M_ = std::max(1, j.get_int("n_mb", 1));
   B_ = std::max(1, j.get_int("mb_size", 1));
-  if (B_ > 64) throw std::runtime_error("mb_size > 64 not supported (the decode GEMV holds at most 4 MFMA row groups)");
+  // > 64 rows per micro-batch: the decode projections run on the prompt GEMM (gemm2, 128 rows per
+  // workgroup), which turns the M = 64 GEMV's exposed MFMA issue into a throughput-bound GEMM
+  if (B_ > 1024) throw std::runtime_error("mb_size > 1024 not supported");
   // max_ctx 0 or "auto": sized from HBM capacity after partitioning (below)
   const bool auto_ctx = (j.has("max_ctx") && j["max_ctx"].is_str() && j["max_ctx"].str() == "auto") ||
                         (j.has("max_ctx") && j["max_ctx"].is_num() && j["max_ctx"].num() == 0);

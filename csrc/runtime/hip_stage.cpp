@@ -451,7 +451,7 @@ void HipStage::alloc_runtime() {
     size_t need = 0;
     auto acc = [&](const PackedMat& m) {
       if (!m.d) return;
-      for (int M : {1, 16, 32, 64}) {
+      for (int M : {1, 2, 3, 4, 8, 16, 32, 64}) {
         const int ns = det_splits((int)m.dims.ntiles, (int)m.dims.nsb, M, EPI_ATOMIC);
         if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
       }
@@ -916,6 +916,12 @@ void HipStage::gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, co
   p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
   p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid; p.bias = bias;
   if (Xf) { p.Xf = Xf; p.ldxf = cfg_.d_model; p.gamma = gamma; p.eps = cfg_.eps; p.d_norm = cfg_.d_model; }
+  if (!Xf && plan_gemvs(p.ntiles, p.nsb, M, epi, false, opt_.deterministic).lds > 150 * 1024) {
+    // deterministic mode cannot split K over grid.y, so a wide K (70B down: 28672) with M >= 3
+    // rows overflows LDS: take the v2 GEMV with its fixed-order split-K reduction instead
+    gemv(m, epi, X, ldx, M, Y, ldy, H, ldh, n_valid, epi == EPI_ATOMIC, st);
+    return;
+  }
   launch_gemvs(m.ptype, epi, p, opt_.deterministic, st);
 }
 

@@ -86,6 +86,20 @@ def test_cpu_microbatch_invariance(native, model_dir):
     assert o == singles
 
 
+def test_cpu_microbatch_over_64_rows(native, model_dir):
+    """mb_size > 64 (decode projections on the prompt GEMM on the HIP backend): the runtime's
+    slot bookkeeping, token ring and pager take micro-batches wider than one GEMV row block."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(72)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, size=int(rng.integers(1, 6)))] for _ in range(72)]
+    with Engine(gguf=path, backend="cpu", max_ctx=64) as eng:
+        singles = [eng.generate([p], 4)[0][0] for p in (prompts[0], prompts[65], prompts[71])]
+    with Engine(gguf=path, backend="cpu", max_ctx=64, n_mb=1, mb_size=72) as eng:
+        o, _ = eng.generate(prompts, 4)
+    assert [o[0], o[65], o[71]] == singles
+
+
 def test_cpu_sampling_seeded(native, model_dir):
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")

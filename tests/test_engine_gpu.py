@@ -177,9 +177,10 @@ def test_microbatch_invariance(cuda, native, model_dir):
     assert o == singles
 
 
-@pytest.mark.parametrize("mb_size", [24, 40, 64])
+@pytest.mark.parametrize("mb_size", [24, 40, 64, 96, 200])
 def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
-    """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment."""
+    """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment;
+    above 64 rows the decode projections and the LM head run on the prompt GEMM (gemm2)."""
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
     rng = np.random.default_rng(mb_size)
