@@ -10,9 +10,12 @@ Weights are random-init directly in HBM with the exact Llama-3-70B architecture 
 format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
 cost-balanced split with the LM head on the last stage); activations move stage to stage with
 RCCL send/recv over xGMI; M = N micro-batches of `--mb-size` sequences circulate through the
-piped ring (default 64 sequences per micro-batch: the decode GEMV shares each dequantized weight
-fragment across 4 MFMA row groups; --mb-size 1 gives the single-stream latency).  Weak scaling: per-GPU work is fixed (every stage streams its own weights once per
-micro-batch per round), global batch = N * mb_size sequences.
+piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the decode
+projections run on the dequant MFMA GEMM (128 rows x 256 columns per workgroup), which reads each
+weight super-block once per 128 rows instead of issuing 4 MFMA row groups per fragment in the GEMV
+(70B PP=1: mb64 3.85k, mb256 5.36k, mb512 5.61k tok/s, profiles/r5a_wide_mb_sweep.txt);
+--mb-size 1 gives the single-stream latency.  Weak scaling: per-GPU work is fixed (every stage
+streams its own weights once per micro-batch per round), global batch = N * mb_size sequences.
 The timed region is exactly K decode rounds (every sequence emits one token per round),
 bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
 """
@@ -48,7 +51,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="llama3-70b", choices=sorted(MODELS))
     ap.add_argument("--ftype", default="Q4_K")
-    ap.add_argument("--mb-size", type=int, default=64, help="sequences per micro-batch (<= 64; > 16 runs the decode projections on the MFMA GEMM)")
+    ap.add_argument("--mb-size", type=int, default=256,
+                    help="sequences per micro-batch (<= 1024; > 64 runs the decode projections on the MFMA GEMM)")
     ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = pipeline depth)")
     ap.add_argument("--pp", type=int, default=0,
                     help="pipeline depth (default: = #GPUs); --pp P < N runs N/P data-parallel pipeline replicas")
