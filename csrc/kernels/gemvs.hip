@@ -274,7 +274,9 @@ static int env_int(const char* k, int dflt) {
 // (two per CU), x k-range in LDS <= 96 KB.
 GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool deterministic) {
   GemvsPlan pl;
-  const int s_target = env_int("MIPIPE_GEMVS_S", 16);   // 8B mb1 sweep (r4c): S 4 / 8 / 16 -> 468 / 499 / 502 tok/s
+  // super-blocks per wave target.  8B mb1 sweep (r4c): S 4 / 8 / 16 -> 468 / 499 / 502 tok/s, flat above;
+  // 70B mb1 (r5g/r5h): S 8 / 16 / 32 / 64 / 128 -> 97.9 / 101.2 / 103.6-104.8 / 105.1 / 105.3
+  const int s_target = env_int("MIPIPE_GEMVS_S", 64);
   const int ks_needed = std::max(1, (nsb + s_target - 1) / s_target);
   int G = ks_needed >= 8 ? 1 : ks_needed >= 5 ? 1 : ks_needed >= 3 ? 2 : ks_needed == 2 ? 4 : 8;
   const int min_wg = env_int("MIPIPE_GEMVS_MINWG", 256);
