@@ -9,13 +9,13 @@ node) + p50/token, Llama-3-70B PP=8 and 8B PP=1"; reference headline 2-3 tok/s f
 Weights are random-init directly in HBM with the exact Llama-3-70B architecture and Q4_K block
 format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
 cost-balanced split with the LM head on the last stage); activations move stage to stage with
-RCCL send/recv over xGMI; M = N micro-batches of `--mb-size` sequences circulate through the
-piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the decode
+RCCL send/recv over xGMI; N + 1 micro-batches (N > 1) of `--mb-size` sequences circulate through
+the piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the decode
 projections run on the dequant MFMA GEMM (128 rows x 256 columns per workgroup), which reads each
 weight super-block once per 128 rows instead of issuing 4 MFMA row groups per fragment in the GEMV
 (70B PP=1: mb64 3.85k, mb256 5.36k, mb512 5.61k tok/s, profiles/r5a_wide_mb_sweep.txt);
 --mb-size 1 gives the single-stream latency.  Weak scaling: per-GPU work is fixed (every stage
-streams its own weights once per micro-batch per round), global batch = N * mb_size sequences.
+streams its own weights once per micro-batch per round), global batch = n_mb * mb_size sequences.
 The timed region is exactly K decode rounds (every sequence emits one token per round),
 bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
 """
@@ -53,7 +53,9 @@ def main():
     ap.add_argument("--ftype", default="Q4_K")
     ap.add_argument("--mb-size", type=int, default=256,
                     help="sequences per micro-batch (<= 1024; > 64 runs the decode projections on the MFMA GEMM)")
-    ap.add_argument("--n-mb", type=int, default=0, help="micro-batches in flight (default: = pipeline depth)")
+    ap.add_argument("--n-mb", type=int, default=0,
+                    help="micro-batches in flight (default: 1 at PP=1, pipeline depth + 1 above: one spare micro-batch "
+                         "covers the token ring's hand-off latency, parallel/pipeline.py simulate_piped_ring)")
     ap.add_argument("--pp", type=int, default=0,
                     help="pipeline depth (default: = #GPUs); --pp P < N runs N/P data-parallel pipeline replicas")
     ap.add_argument("--prompt-len", type=int, default=128)
@@ -77,7 +79,7 @@ def main():
         print(f"bench.py: --pp {pp} does not divide {world} GPUs", file=sys.stderr)
         sys.exit(2)
     replicas = world // pp
-    n_mb = args.n_mb or pp
+    n_mb = args.n_mb or (pp + 1 if pp > 1 else 1)
     max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
     cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
                prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
