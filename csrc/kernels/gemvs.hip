@@ -41,8 +41,9 @@ using namespace mp;
 constexpr int GS_NW = 8;
 constexpr int GS_NT = GS_NW * 64;
 
+// bx: this workgroup's tile-group index (blockIdx.x, or its offset inside a segment of gemvs2)
 template <int PT, int EPI, int G, bool NORM>
-__global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const int nsplit) {
+__device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int KSW = GS_NW / G;
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const 
 
   // this wave's tile and contiguous k-slice [wA, wB) of the workgroup's super-blocks
   const int gi = wave / KSW, ks = wave % KSW;
-  const int tile = blockIdx.x * G + gi;
+  const int tile = bx * G + gi;
   const int per = (sbB - sbA + KSW - 1) / KSW;
   const int wA = min(sbA + ks * per, sbB), wB = min(wA + per, sbB);
   const bool live = tile < p.ntiles;
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const 
     if (wave >= G) return;
   }
   // epilogue wave e = gi' handles tile blockIdx.x * G + e; lane -> (row i = lane >> 4, column r)
-  const int et = KSW == 1 ? tile : blockIdx.x * G + wave;
+  const int et = KSW == 1 ? tile : bx * G + wave;
   float val;
   if constexpr (KSW == 1) {
     // lane (g, r): rows 4g + i; only g = 0 is valid (M <= 4): move row i to lane 16 i + r
@@ -258,6 +259,20 @@ __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const 
       }
     }
   }
+}
+
+template <int PT, int EPI, int G, bool NORM>
+__global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const int nsplit) {
+  gemvs_body<PT, EPI, G, NORM>(p, nsplit, blockIdx.x);
+}
+
+// two weight segments with different quant types over the same normed input in ONE launch (the
+// q+k and v projections of a mixed-type layer, e.g. Q4_K_M's Q6_K attn_v): workgroups [0, nwg1)
+// take segment 1, the rest segment 2.  STORE epilogue, RMSNorm fused, no k-split.
+template <int PT, int PT2, int G>
+__global__ __launch_bounds__(GS_NT) void gemvs2_kernel(const GemvParams p, const GemvParams p2, const int nwg1) {
+  if ((int)blockIdx.x < nwg1) gemvs_body<PT, EPI_STORE, G, true>(p, 1, blockIdx.x);
+  else gemvs_body<PT2, EPI_STORE, G, true>(p2, 1, blockIdx.x - nwg1);
 }
 
 }  // namespace mpk
@@ -328,6 +343,50 @@ static void gemvs_pt(int epi, const GemvParams& p, const GemvsPlan& pl, hipStrea
     case EPI_STORE: return norm ? gemvs_g<PT, EPI_STORE, true>(p, pl, st) : gemvs_g<PT, EPI_STORE, false>(p, pl, st);
     case EPI_ATOMIC: return norm ? gemvs_g<PT, EPI_ATOMIC, true>(p, pl, st) : gemvs_g<PT, EPI_ATOMIC, false>(p, pl, st);
     case EPI_SWIGLU: return norm ? gemvs_g<PT, EPI_SWIGLU, true>(p, pl, st) : gemvs_g<PT, EPI_SWIGLU, false>(p, pl, st);
+  }
+}
+
+template <int PT, int PT2, int G>
+static void gemvs2_go(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs2_kernel<PT, PT2, G>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
+  }();
+  if (!attr && lds > 60 * 1024) throw std::runtime_error("gemvs2: cannot raise the dynamic LDS limit");
+  const int nwg1 = (p.ntiles + G - 1) / G, nwg2 = (p2.ntiles + G - 1) / G;
+  hipLaunchKernelGGL((mpk::gemvs2_kernel<PT, PT2, G>), dim3(nwg1 + nwg2), dim3(mpk::GS_NT), lds, st, p, p2, nwg1);
+}
+
+template <int PT, int PT2>
+static void gemvs2_g(int G, const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
+  switch (G) {
+    case 1: return gemvs2_go<PT, PT2, 1>(p, p2, lds, st);
+    case 2: return gemvs2_go<PT, PT2, 2>(p, p2, lds, st);
+    case 4: return gemvs2_go<PT, PT2, 4>(p, p2, lds, st);
+    case 8: return gemvs2_go<PT, PT2, 8>(p, p2, lds, st);
+    default: throw std::runtime_error("gemvs2: G must be 1, 2, 4 or 8");
+  }
+}
+
+bool gemvs2_supported(int pt, int pt2) {
+  return (pt == P_Q4_K || pt == P_Q5_K) && (pt2 == P_Q6_K || pt2 == P_Q8_0);
+}
+
+void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st) {
+  if (!gemvs2_supported(pt, pt2)) throw std::runtime_error("launch_gemvs2: unsupported type pair");
+  if (p.M < 1 || p.M > 4 || p2.M != p.M) throw std::runtime_error("launch_gemvs2: M must be 1..4 and equal");
+  if (!p.Xf || !p2.Xf || p.nsb != p2.nsb || p.d_norm != p2.d_norm || (p.d_norm & 7) || p.d_norm > p.nsb * 256)
+    throw std::runtime_error("launch_gemvs2: both segments need the same fused-norm input and K");
+  // one plan for the union of the tiles (the shared G sizes both segments' workgroups)
+  const GemvsPlan pl = plan_gemvs(p.ntiles + p2.ntiles, p.nsb, p.M, EPI_STORE, true, true);
+  if (pl.nsplit != 1 || pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs2: x k-range does not fit LDS");
+  p.sb_per_split = p2.sb_per_split = pl.sb_per_split;
+  if (pt == P_Q4_K) {
+    if (pt2 == P_Q6_K) gemvs2_g<P_Q4_K, P_Q6_K>(pl.G, p, p2, pl.lds, st);
+    else gemvs2_g<P_Q4_K, P_Q8_0>(pl.G, p, p2, pl.lds, st);
+  } else {
+    if (pt2 == P_Q6_K) gemvs2_g<P_Q5_K, P_Q6_K>(pl.G, p, p2, pl.lds, st);
+    else gemvs2_g<P_Q5_K, P_Q8_0>(pl.G, p, p2, pl.lds, st);
   }
 }
 

@@ -744,9 +744,26 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   if (small_path(M)) {
     // gemvs: RMSNorms fused into the qkv / gate-up GEMVs, complete outputs per workgroup (q|k|v
     // stored with its bias, o / down added into the residual by their single owner)
-    for (const MatSeg& s : L.qkv)
-      gemv_small(s.m, EPI_STORE, nullptr, 0, x, L.attn_norm, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N,
-                 L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st);
+    static const bool two = [] { const char* e = getenv("MIPIPE_GEMVS2"); return !e || atoi(e) != 0; }();
+    const int first = L.qkv.size() == 2 && gemvs2_supported(L.qkv[1].m.ptype, L.qkv[0].m.ptype) ? 1 : 0;
+    if (two && L.qkv.size() == 2 && gemvs2_supported(L.qkv[first].m.ptype, L.qkv[1 - first].m.ptype) &&
+        L.qkv[0].m.dims.nsb == L.qkv[1].m.dims.nsb) {
+      // mixed-type q+k | v (Q4_K_M's Q6_K attn_v): both segments in one launch
+      GemvParams ps[2];
+      for (int i = 0; i < 2; ++i) {
+        const MatSeg& sg = L.qkv[i == 0 ? first : 1 - first];
+        GemvParams& q = ps[i];
+        q.W = sg.m.d; q.M = M; q.Y = qkv_ + sg.y_off; q.ldy = qkv_n_;
+        q.ntiles = (int)sg.m.dims.ntiles; q.nsb = (int)sg.m.dims.nsb; q.n_valid = (int)sg.m.dims.N;
+        q.bias = L.qkv_bias ? L.qkv_bias + sg.y_off : nullptr;
+        q.Xf = x; q.ldxf = d; q.gamma = L.attn_norm; q.eps = cfg_.eps; q.d_norm = d;
+      }
+      launch_gemvs2(L.qkv[first].m.ptype, L.qkv[1 - first].m.ptype, ps[0], ps[1], st);
+    } else {
+      for (const MatSeg& s : L.qkv)
+        gemv_small(s.m, EPI_STORE, nullptr, 0, x, L.attn_norm, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N,
+                   L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st);
+    }
     attention(li, M, pos, kvlen, slot, decode, st, false);
     gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
     if (L.moe) {

@@ -46,6 +46,9 @@ void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
 // EPI_ATOMIC adds into Y by read-modify-write (nsplit 1, deterministic) or atomics (nsplit > 1)
 struct GemvsPlan { int G = 1, nsplit = 1, sb_per_split = 0; size_t lds = 0; };
 GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool deterministic);
+// q+k and v of a mixed-type layer in one launch (gemvs.hip): STORE, fused RMSNorm, same K
+bool gemvs2_supported(int pt, int pt2);
+void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st);
 void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G = 0,
                   int force_split = 0);
 void set_gemv_tpw(int tiles_per_wave);    // M > 32 tiles per wave: 0 = auto, 1, 2 (tuning knob)

@@ -157,12 +157,14 @@ def test_gemvs_rejects_bad_shapes(cuda, native):
         gemv_small(w, EPI_STORE, x=_xh(1, 1024, w.k_pad, 1).cuda(), nsplit=2)   # STORE cannot split K
 
 
-@pytest.mark.parametrize("name", ["tiny-gqa", "tiny-qwen2", "tiny-moe"])
-def test_engine_small_gemv_matches_v2_path(cuda, native, model_dir, name):
-    """Single-stream engine logits with the gemvs path (default) vs the v2 GEMV + rmsnorm path."""
+@pytest.mark.parametrize("name,ftype", [("tiny-gqa", "Q4_K"), ("tiny-qwen2", "Q4_K"), ("tiny-moe", "Q4_K"),
+                                        ("tiny-gqa", "Q4_K_M"), ("tiny-qwen2", "Q4_K_M")])
+def test_engine_small_gemv_matches_v2_path(cuda, native, model_dir, name, ftype):
+    """Single-stream engine logits with the gemvs path (default) vs the v2 GEMV + rmsnorm path.
+    Q4_K_M: the layers whose attn_v is Q6_K take the two-segment q+k | v launch (gemvs2)."""
     from conftest import make_model
     from mipipe.engine import Engine
-    path, cfg = make_model(model_dir, name, "Q4_K")
+    path, cfg = make_model(model_dir, name, ftype)
     prompts = [[3, 4, 5, 6, 7], [9, 10]]
     outs = {}
     for sg in (True, False):
