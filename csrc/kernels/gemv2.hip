@@ -307,9 +307,9 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
   }
 }
 
-template <int PT, int EPI>
+template <int PT, int EPI, int TW>
 static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st) {
-  constexpr int NW = 8, TW = 2, MT = 8;
+  constexpr int NW = 8, MT = 8;
   p.m_blocks = (p.M + 16 * MT - 1) / (16 * MT);
   const int groups = (p.ntiles + NW * TW - 1) / (NW * TW);
   // narrow outputs (8B down / qkv, 70B o / down: 16-32 tile groups) leave CUs idle: split K over
@@ -324,13 +324,26 @@ static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st) {
   hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, MT, TW, false>), dim3(wgs, nsplit), dim3(NW * 64), 0, st, p);
 }
 
+template <int PT, int TW>
+static void gemm2_cfg(int epi, const GemvParams& p, bool allow_split, hipStream_t st) {
+  switch (epi) {
+    case EPI_STORE: return gemm2_go<PT, EPI_STORE, TW>(p, allow_split, st);
+    case EPI_ATOMIC: return gemm2_go<PT, EPI_ATOMIC, TW>(p, allow_split, st);
+    case EPI_SWIGLU: return gemm2_go<PT, EPI_SWIGLU, TW>(p, allow_split, st);
+  }
+}
+
 template <int PT>
 static void gemm2_pt(int epi, const GemvParams& p, bool allow_split, hipStream_t st) {
-  switch (epi) {
-    case EPI_STORE: return gemm2_go<PT, EPI_STORE>(p, allow_split, st);
-    case EPI_ATOMIC: return gemm2_go<PT, EPI_ATOMIC>(p, allow_split, st);
-    case EPI_SWIGLU: return gemm2_go<PT, EPI_SWIGLU>(p, allow_split, st);
-  }
+  // a grid of at most half as many two-tile workgroups as CUs that cannot split K (SWIGLU / STORE,
+  // or deterministic) takes one tile per wave: twice the workgroups for twice the A-fragment LDS
+  // reads.  Measured (r5m): 8B mb128 (gate/up 112 workgroups) 15.9k -> 17.3k tok/s, but 8B mb256
+  // and 70B mb128 (224 workgroups) lose 4-7 %, hence the threshold of 128
+  static const int min_wg = [] { const char* e = getenv("MIPIPE_GEMM2_TW1_BELOW"); return e ? atoi(e) : 128; }();
+  const int wgs2 = (p.ntiles + 15) / 16 * ((p.M + 127) / 128);
+  const bool splits = epi == EPI_ATOMIC && allow_split;
+  if (!splits && wgs2 < min_wg) gemm2_cfg<PT, 1>(epi, p, allow_split, st);
+  else gemm2_cfg<PT, 2>(epi, p, allow_split, st);
 }
 
 void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split) {
