@@ -318,7 +318,8 @@ static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st) {
   // 409 -> 261 us, o 136 -> 99, 8B down 206 -> 94; a second round cost 70B qkv 142 -> 170)
   int nsplit = 1;
   const int wgs = groups * p.m_blocks;
-  if (EPI == EPI_ATOMIC && allow_split && wgs < 256) nsplit = std::min(256 / wgs, std::max(1, p.nsb / 4));
+  static const int split_wg = [] { const char* e = getenv("MIPIPE_GEMM2_SPLIT_WG"); return e ? atoi(e) : 256; }();
+  if (EPI == EPI_ATOMIC && allow_split && wgs < split_wg) nsplit = std::min(split_wg / wgs, std::max(1, p.nsb / 4));
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
   hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, MT, TW, false>), dim3(wgs, nsplit), dim3(NW * 64), 0, st, p);
