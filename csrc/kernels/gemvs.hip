@@ -42,12 +42,12 @@ constexpr int GS_NW = 8;
 constexpr int GS_NT = GS_NW * 64;
 
 // bx: this workgroup's tile-group index (blockIdx.x, or its offset inside a segment of gemvs2)
-template <int PT, int EPI, int G, bool NORM>
+template <int PT, int EPI, int G, bool NORM, int NSO = 0>
 __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int KSW = GS_NW / G;
-  constexpr int NS = PT == P_F16 ? 2 : 4;
+  constexpr int NS = NSO ? NSO : PT == P_F16 ? 2 : 4;   // weight super-blocks in flight per wave
   extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange]
   __shared__ float red[GS_NW][64];
   __shared__ float red_ss[GS_NW][4];
@@ -261,9 +261,9 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   }
 }
 
-template <int PT, int EPI, int G, bool NORM>
+template <int PT, int EPI, int G, bool NORM, int NSO = 0>
 __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const int nsplit) {
-  gemvs_body<PT, EPI, G, NORM>(p, nsplit, blockIdx.x);
+  gemvs_body<PT, EPI, G, NORM, NSO>(p, nsplit, blockIdx.x);
 }
 
 // two weight segments with different quant types over the same normed input in ONE launch (the
@@ -314,26 +314,39 @@ GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool determ
   return pl;
 }
 
-template <int PT, int EPI, int G, bool NORM>
+template <int PT, int EPI, int G, bool NORM, int NSO = 0>
 static void gemvs_go(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   static const bool attr = [] {   // dynamic LDS past the 64 KB default (gfx950: 160 KB per workgroup)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs_kernel<PT, EPI, G, NORM>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs_kernel<PT, EPI, G, NORM, NSO>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
   }();
   if (!attr && pl.lds > 60 * 1024) throw std::runtime_error("gemvs: cannot raise the dynamic LDS limit");
-  hipLaunchKernelGGL((mpk::gemvs_kernel<PT, EPI, G, NORM>), dim3((p.ntiles + G - 1) / G, pl.nsplit),
+  hipLaunchKernelGGL((mpk::gemvs_kernel<PT, EPI, G, NORM, NSO>), dim3((p.ntiles + G - 1) / G, pl.nsplit),
                      dim3(mpk::GS_NT), pl.lds, st, p, pl.nsplit);
+}
+
+template <int PT, int EPI, bool NORM, int NSO>
+static void gemvs_gn(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
+  switch (pl.G) {
+    case 1: return gemvs_go<PT, EPI, 1, NORM, NSO>(p, pl, st);
+    case 2: return gemvs_go<PT, EPI, 2, NORM, NSO>(p, pl, st);
+    case 4: return gemvs_go<PT, EPI, 4, NORM, NSO>(p, pl, st);
+    case 8: return gemvs_go<PT, EPI, 8, NORM, NSO>(p, pl, st);
+    default: throw std::runtime_error("gemvs: G must be 1, 2, 4 or 8");
+  }
 }
 
 template <int PT, int EPI, bool NORM>
 static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
-  switch (pl.G) {
-    case 1: return gemvs_go<PT, EPI, 1, NORM>(p, pl, st);
-    case 2: return gemvs_go<PT, EPI, 2, NORM>(p, pl, st);
-    case 4: return gemvs_go<PT, EPI, 4, NORM>(p, pl, st);
-    case 8: return gemvs_go<PT, EPI, 8, NORM>(p, pl, st);
-    default: throw std::runtime_error("gemvs: G must be 1, 2, 4 or 8");
+  // weight super-blocks in flight per wave: 2 by default -- residency beats per-wave depth here
+  // (NS 2: 80 VGPRs, 3 workgroups per CU; NS 4: 104 VGPRs, 2; NS 8: 3 waves/SIMD).  r5o / r5p:
+  // 8B Q4_K_M mb1 NS 2 / 3 / 4 / 8 -> 548 / 541 / 524 / 441 tok/s, 70B Q4_K 105.4 / 106.6 / 104.4 / 91.1
+  static const int ns = [] { const char* e = getenv("MIPIPE_GEMVS_NS"); return e ? atoi(e) : 2; }();
+  if constexpr (PT != P_F16) {
+    if (ns == 2) return gemvs_gn<PT, EPI, NORM, 2>(p, pl, st);
+    if (ns == 3) return gemvs_gn<PT, EPI, NORM, 3>(p, pl, st);
   }
+  gemvs_gn<PT, EPI, NORM, 0>(p, pl, st);
 }
 
 template <int PT>
