@@ -10,6 +10,7 @@
 // Online softmax in registers; 4 waves interleave chunks and are merged through LDS; splits are
 // merged by attn_combine (LSE merge).  KV pages hold 64 tokens: K [64][Dp], V^T [Dp][64].
 #include <type_traits>
+#include "../runtime/tuning.h"
 
 #include "kcommon.h"
 #include "../runtime/kernels_api.h"
@@ -651,7 +652,7 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
   // the next-chunk prefetch variant (2 workgroups per CU) for a single split per (token, kv head)
   // while the grid is small; many workgroups (long contexts, or wide micro-batches: M * Hkv above
   // MIPIPE_ATTN_PF_MAXWG) need occupancy more than per-wave latency: the 3-per-CU variant
-  static const int pf_max = [] { const char* e = getenv("MIPIPE_ATTN_PF_MAXWG"); return e ? atoi(e) : 1 << 30; }();
+  const int pf_max = knob(KNOB_ATTN_PF_MAXWG);
   const bool pf = p.n_split == 1 && p.M * p.Hkv <= pf_max;
   if (p.kv_fp8) pf ? attn_decode_go<true, true>(p, st) : attn_decode_go<true, false>(p, st);
   else pf ? attn_decode_go<false, true>(p, st) : attn_decode_go<false, false>(p, st);

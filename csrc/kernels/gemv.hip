@@ -9,6 +9,7 @@
 // (The round-1 per-wave-x v1 kernel and its bandwidth probes were retired: the LDS-shared v2 won
 // every shape, profiles/r1b_gemv_*.)
 #include "kcommon.h"
+#include "../runtime/tuning.h"
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
@@ -52,13 +53,9 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
 // M = 64): gate/up 115.9 -> 104.3 us with two tiles per wave; the split-K projections (qkv, o,
 // down) gain nothing at their best split.
 static int g_nw = 8, g_tw2 = 0;
-static bool g_env = false;
-static void read_env() {
-  if (g_env) return;
-  g_env = true;
-  if (const char* w = getenv("MIPIPE_GEMV_NW")) g_nw = atoi(w) == 4 ? 4 : 8;
-
-  if (const char* w = getenv("MIPIPE_GEMV2_TW")) g_tw2 = atoi(w) == 2 ? 2 : atoi(w) == 1 ? 1 : 0;
+static void read_env() {   // the knobs (tuning.h), re-read per launch: set_gemv_tpw overrides the TW one
+  g_nw = knob(KNOB_GEMV_NW);
+  g_tw2 = knob(KNOB_GEMV2_TW);
 }
 static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
   read_env();
@@ -70,10 +67,7 @@ static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
 }
 
 int gemv_tiles_per_wave(int M, int epi) { return gemv2_tw(M, epi); }
-void set_gemv_tpw(int t) {
-  read_env();
-  g_tw2 = (t == 1 || t == 2) ? t : 0;
-}
+void set_gemv_tpw(int t) { set_knob("GEMV2_TW", (t == 1 || t == 2) ? t : 0); }
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {
   read_env();

@@ -14,6 +14,7 @@
 // Ordering: x(sb+1) is issued BEFORE the weight refill of the current step, so waiting for it
 // (vmcnt) never drains the weight prefetches issued after it (vmcnt retires in issue order).
 #include "kcommon.h"
+#include "../runtime/tuning.h"
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
@@ -318,7 +319,7 @@ static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st) {
   // 409 -> 261 us, o 136 -> 99, 8B down 206 -> 94; a second round cost 70B qkv 142 -> 170)
   int nsplit = 1;
   const int wgs = groups * p.m_blocks;
-  static const int split_wg = [] { const char* e = getenv("MIPIPE_GEMM2_SPLIT_WG"); return e ? atoi(e) : 256; }();
+  const int split_wg = knob(KNOB_GEMM2_SPLIT_WG);
   if (EPI == EPI_ATOMIC && allow_split && wgs < split_wg) nsplit = std::min(split_wg / wgs, std::max(1, p.nsb / 4));
   p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
   nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
@@ -340,7 +341,7 @@ static void gemm2_pt(int epi, const GemvParams& p, bool allow_split, hipStream_t
   // or deterministic) takes one tile per wave: twice the workgroups for twice the A-fragment LDS
   // reads.  Measured (r5m): 8B mb128 (gate/up 112 workgroups) 15.9k -> 17.3k tok/s, but 8B mb256
   // and 70B mb128 (224 workgroups) lose 4-7 %, hence the threshold of 128
-  static const int min_wg = [] { const char* e = getenv("MIPIPE_GEMM2_TW1_BELOW"); return e ? atoi(e) : 128; }();
+  const int min_wg = knob(KNOB_GEMM2_TW1_BELOW);
   const int wgs2 = (p.ntiles + 15) / 16 * ((p.M + 127) / 128);
   const bool splits = epi == EPI_ATOMIC && allow_split;
   if (!splits && wgs2 < min_wg) gemm2_cfg<PT, 1>(epi, p, allow_split, st);

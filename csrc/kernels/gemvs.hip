@@ -28,6 +28,7 @@
 // for r < M, zero above (LDS holds M rows only).  C: lane (g, r) holds rows 4g + i: the M <= 4
 // valid rows are in lanes 0-15 (g = 0), acc[i] = row i, column r.
 #include "kcommon.h"
+#include "../runtime/tuning.h"
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
@@ -279,11 +280,6 @@ __global__ __launch_bounds__(GS_NT) void gemvs2_kernel(const GemvParams p, const
 
 namespace mp {
 
-static int env_int(const char* k, int dflt) {
-  const char* e = getenv(k);
-  return e ? atoi(e) : dflt;
-}
-
 // Work split: G tiles per workgroup (KSW = 8 / G waves share each tile's k-range) and nsplit
 // k-splits over grid.y (ATOMIC only).  Aim: ~S_target super-blocks per wave, >= 512 workgroups
 // (two per CU), x k-range in LDS <= 96 KB.
@@ -291,18 +287,18 @@ GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool determ
   GemvsPlan pl;
   // super-blocks per wave target.  8B mb1 sweep (r4c): S 4 / 8 / 16 -> 468 / 499 / 502 tok/s, flat above;
   // 70B mb1 (r5g/r5h): S 8 / 16 / 32 / 64 / 128 -> 97.9 / 101.2 / 103.6-104.8 / 105.1 / 105.3
-  const int s_target = env_int("MIPIPE_GEMVS_S", 64);
+  const int s_target = knob(KNOB_GEMVS_S);
   const int ks_needed = std::max(1, (nsb + s_target - 1) / s_target);
   int G = ks_needed >= 8 ? 1 : ks_needed >= 5 ? 1 : ks_needed >= 3 ? 2 : ks_needed == 2 ? 4 : 8;
-  const int min_wg = env_int("MIPIPE_GEMVS_MINWG", 256);
+  const int min_wg = knob(KNOB_GEMVS_MINWG);
   while (G > 1 && (ntiles + G - 1) / G < min_wg) G >>= 1;
-  if (const int eg = env_int("MIPIPE_GEMVS_G", 0)) G = eg;
+  if (const int eg = knob(KNOB_GEMVS_G)) G = eg;
   int nsplit = 1;
   const bool can_split = epi == EPI_ATOMIC && !deterministic;
   if (can_split && G == 1) {
     while ((nsb + 8 * nsplit - 1) / (8 * nsplit) > s_target && (ntiles * nsplit) < 1024 && nsb / (2 * nsplit) >= 8)
       nsplit *= 2;
-    if (const int es = env_int("MIPIPE_GEMVS_SPLIT", 0)) nsplit = es;
+    if (const int es = knob(KNOB_GEMVS_SPLIT)) nsplit = es;
   }
   // LDS: M rows x the split's k-range of f16 x
   auto lds_of = [&](int ns) { return (size_t)M * ((nsb + ns - 1) / ns) * 256 * 2; };
@@ -341,12 +337,13 @@ static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   // weight super-blocks in flight per wave: 2 by default -- residency beats per-wave depth here
   // (NS 2: 80 VGPRs, 3 workgroups per CU; NS 4: 104 VGPRs, 2; NS 8: 3 waves/SIMD).  r5o / r5p:
   // 8B Q4_K_M mb1 NS 2 / 3 / 4 / 8 -> 548 / 541 / 524 / 441 tok/s, 70B Q4_K 105.4 / 106.6 / 104.4 / 91.1
-  static const int ns = [] { const char* e = getenv("MIPIPE_GEMVS_NS"); return e ? atoi(e) : 2; }();
+  // (the knob only admits 2, 3 and 4; 16-bit weights always run the default depth)
+  const int ns = knob(KNOB_GEMVS_NS);
   if constexpr (PT != P_F16) {
     if (ns == 2) return gemvs_gn<PT, EPI, NORM, 2>(p, pl, st);
     if (ns == 3) return gemvs_gn<PT, EPI, NORM, 3>(p, pl, st);
   }
-  gemvs_gn<PT, EPI, NORM, 0>(p, pl, st);
+  gemvs_gn<PT, EPI, NORM, 0>(p, pl, st);   // NS 4
 }
 
 template <int PT>

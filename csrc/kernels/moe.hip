@@ -3,6 +3,7 @@
 // router writes per-expert token lists, the expert kernels read the counts and exit early for
 // idle experts, so a decode step streams only the weights of the experts actually selected.
 #include "kcommon.h"
+#include "../runtime/tuning.h"
 #include <cstdlib>
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
@@ -261,7 +262,7 @@ static void moe2_mt(const MoeGemvParams& p, int nsplit, hipStream_t st) {
 
 template <int PT>
 static void moe_launch_pt(int epi, const MoeGemvParams& p, int nsplit, hipStream_t st) {
-  static const bool v1 = [] { const char* e = getenv("MIPIPE_MOE_V"); return e && atoi(e) == 1; }();
+  const bool v1 = knob(KNOB_MOE_V) == 1;
   if (!v1 && p.M >= 1 && p.M <= 64) {   // every expert's rows fit one pass of <= 4 row groups
     if (epi == EPI_SWIGLU) moe2_mt<PT, EPI_SWIGLU>(p, nsplit, st);
     else moe2_mt<PT, EPI_ATOMIC>(p, nsplit, st);

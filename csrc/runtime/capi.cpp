@@ -2,6 +2,7 @@
 // Every entry point catches exceptions, records the message (mp_last_error) and returns an
 // error code / nullptr.
 #include <hip/hip_runtime.h>
+#include "tuning.h"
 
 #include <algorithm>
 #include <chrono>
@@ -163,6 +164,27 @@ int mp_op_gemm2(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
   p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
   launch_gemm2(ptype, epi, p, (hipStream_t)stream);
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_gemm3(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+                int ldy, void* H, int ldh, int n_valid, int allow_split, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  launch_gemm3(ptype, epi, p, (hipStream_t)stream, allow_split != 0);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+void mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) { set_gemm3_tuning(bm, bn, nsplit, split_wg); }
+
+int mp_set_knob(const char* name, int value) {
+  API_TRY
+  set_knob(name, value);
   return 0;
   API_CATCH(-1)
 }

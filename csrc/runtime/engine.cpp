@@ -137,6 +137,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   const std::string kv_dtype = j.get_str("kv_dtype", "f16");
   if (kv_dtype != "f16" && kv_dtype != "fp8") throw std::runtime_error("kv_dtype must be f16 or fp8");
   const bool kv_fp8 = kv_dtype == "fp8";
+  kv_fp8_ = kv_fp8;
   if (kv_fp8 && (j.get_str("backend", "hip") == "cpu" || !j.get_bool("fused_attn", true) || !j.get_bool("prefill_flash", true)))
     throw std::runtime_error("kv_dtype fp8 needs the HIP backend with fused_attn and prefill_flash");
   std::vector<int> devices(S_);
@@ -246,7 +247,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       if (sp.first()) w += embd_b;
       if (sp.last()) w += head_cost;
       const double kv = (double)(sp.layer_end - sp.layer_begin) * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() *
-                        (cpu_ ? 4.0 : 2.0) * ((double)kv_pages_ + 1) * 64;
+                        (cpu_ ? 4.0 : kv_fp8 ? 1.0 : 2.0) * ((double)kv_pages_ + 1) * 64;
       auto& e = need[devices[sp.stage]];
       e.first += w;
       e.second += kv;
@@ -296,7 +297,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
-  so.prefill_gemm_v = j.get_int("prefill_gemm_v", 2);
+  so.prefill_gemm_v = j.get_int("prefill_gemm_v", 3);
   so.deterministic = j.get_bool("deterministic", false);
   so.prefill_flash = j.get_bool("prefill_flash", true);
   so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";
@@ -964,11 +965,15 @@ void Engine::refresh_slot_cache() {
 }
 
 // ---------------------------------------------------------------- checkpoint / resume
-static Json state_fingerprint(const ModelConfig& c, int S, int M, int B, int max_ctx) {
+// everything the saved KV bytes depend on: model shape, pipeline shape, and the KV element type
+// (f32 on the CPU backend, f16 or fp8 e4m3 on HIP) -- a checkpoint written with one KV dtype must
+// not be imported page by page into another
+static Json state_fingerprint(const ModelConfig& c, int S, int M, int B, int max_ctx, bool cpu, bool kv_fp8) {
   Json f = Json::object();
   f["n_layer"] = c.n_layer; f["d_model"] = c.d_model; f["n_head"] = c.n_head; f["n_head_kv"] = c.n_head_kv;
   f["d_ff"] = c.d_ff; f["vocab"] = c.vocab; f["n_stages"] = S; f["n_mb"] = M; f["mb_size"] = B;
   f["max_ctx"] = max_ctx;
+  f["kv_dtype"] = cpu ? "f32" : kv_fp8 ? "fp8" : "f16";
   return f;
 }
 
@@ -978,7 +983,7 @@ Json Engine::save_state(const std::string& dir) {
   if (!resumable_) throw std::runtime_error("save_state: not supported after speculative decoding");
   ::mkdir(dir.c_str(), 0755);
   sync_all();
-  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_);
+  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_, cpu_, kv_fp8_);
   // tokens already in each slot's KV: prompt + generated - 1 (the newest token is the next input)
   std::vector<int> n_tok((size_t)M_ * B_, 0);
   for (size_t i = 0; i < prompts_.size(); ++i)
@@ -1053,7 +1058,7 @@ Json Engine::load_state(const std::string& dir) {
     if (!f) throw std::runtime_error("load_state: cannot read " + path);
     return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
   };
-  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_);
+  const Json fp = state_fingerprint(cfg_, S_, M_, B_, max_ctx_, cpu_, kv_fp8_);
   const Json sj = Json::parse(slurp(dir + "/session.json"));
   if (sj.get_str("magic", "") != "mipipe-session" || sj["fingerprint"].dump() != fp.dump())
     throw std::runtime_error("load_state: session was saved by a different model / pipeline shape");
@@ -1116,6 +1121,15 @@ Json Engine::load_state(const std::string& dir) {
     const uint8_t* end = reinterpret_cast<const uint8_t*>(raw.data()) + raw.size();
     const auto& lens = h["n_tok"].arr();
     if ((int)lens.size() != M_ * B_) throw std::runtime_error("load_state: bad n_tok in " + path);
+    // the KV payload must be exactly what this stage exports for those lengths (element size
+    // included) and exactly what the file holds after its header
+    size_t want_bytes = 0;
+    for (size_t i = 0; i < lens.size(); ++i) {
+      const int n = (int)lens[i].num();
+      if (n > 0 && n < max_ctx_) want_bytes += st.kv_state_bytes(n);
+    }
+    if ((double)want_bytes != h.get_num("kv_bytes", -1) || want_bytes != (size_t)(end - kv))
+      throw std::runtime_error("load_state: " + path + " KV payload size does not match this stage (kv dtype?)");
     for (size_t i = 0; i < lens.size(); ++i) {
       const int n = (int)lens[i].num();
       // the stage file must describe exactly the KV the session implies (active slots only)

@@ -162,6 +162,7 @@ class Engine {
   int32_t* out_host_ = nullptr;                    // pinned [rounds_cap][M*B]
   std::vector<int32_t> out_vec_;                   // CPU backend storage of out_host_
   bool cpu_ = false;
+  bool kv_fp8_ = false;      // kv_dtype "fp8" (checkpoint fingerprint: the KV bytes' element type)
   bool trace_ = false, failed_ = false;
   bool packed_prefill_ = true;   // several sequences per prefill chunk (config "packed_prefill")
   int act_dtype_ = 0;            // stage-boundary activation wire format (ActDtype; config "act_dtype")

@@ -1,4 +1,5 @@
 #include "hip_stage.h"
+#include "tuning.h"
 
 #include <chrono>
 #include <cstring>
@@ -427,7 +428,7 @@ void HipStage::alloc_runtime() {
   if (split <= 0) {
     // auto: enough (sequence, kv head, split) workgroups to cover the CUs, but >= 256 keys per
     // split (a split merge costs a publish/acquire round trip; short contexts use one split)
-    static const int target = [] { const char* e = getenv("MIPIPE_ATTN_WG_TARGET"); return e ? std::max(1, atoi(e)) : 256; }();
+    const int target = knob(KNOB_ATTN_WG_TARGET);
     const int pairs = std::max(1, B * Hkv);
     const int want = std::max(1, std::min((target + pairs - 1) / pairs, (opt_.max_ctx + 255) / 256));
     split = (opt_.max_ctx + want - 1) / want;
@@ -643,13 +644,17 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // profiles/r1g_prefill_gemm_vs_gemv.txt)
   // v2 GEMM (128 rows x 256 columns per workgroup, the decode GEMV's dequant + LDS-shared rows):
   // every shape, f16 weights excepted (they take the 64 x 64 GEMM)
+  // v3 GEMM (gemm3.hip: 128|256 x 128|256 workgroup tiles, each weight element dequantized once
+  // per workgroup into LDS): every type, 16-bit weights included
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
+  const bool v3 = opt_.prefill_gemm_v == 3;
   const bool v2 = opt_.prefill_gemm_v == 2 && m.ptype != P_F16;
-  if (M > 64 && opt_.prefill_gemm && (v2 || !wide_swiglu)) {
+  if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
-    if (v2) launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+    if (v3) launch_gemm3(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+    else if (v2) launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
     else launch_gemm(m.ptype, epi, p, st);
     return;
   }
@@ -690,7 +695,7 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
   // prompt chunks run in slices of <= 64 tokens, so every slice takes the workgroup-shared MoE
   // GEMV (weights streamed once per 64 tokens, not once per 16 routed rows as in v1)
-  const bool v1 = [] { const char* e = getenv("MIPIPE_MOE_V"); return e && atoi(e) == 1; }();
+  const bool v1 = knob(KNOB_MOE_V) == 1;
   const int step = v1 ? M : 64;
   for (int r0 = 0; r0 < M; r0 += step) moe_ffn_rows(L, r0, std::min(step, M - r0), st, x);
 }
@@ -744,7 +749,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   if (small_path(M)) {
     // gemvs: RMSNorms fused into the qkv / gate-up GEMVs, complete outputs per workgroup (q|k|v
     // stored with its bias, o / down added into the residual by their single owner)
-    static const bool two = [] { const char* e = getenv("MIPIPE_GEMVS2"); return !e || atoi(e) != 0; }();
+    const bool two = knob(KNOB_GEMVS2) != 0;
     const int first = L.qkv.size() == 2 && gemvs2_supported(L.qkv[1].m.ptype, L.qkv[0].m.ptype) ? 1 : 0;
     if (two && L.qkv.size() == 2 && gemvs2_supported(L.qkv[first].m.ptype, L.qkv[1 - first].m.ptype) &&
         L.qkv[0].m.dims.nsb == L.qkv[1].m.dims.nsb) {

@@ -168,14 +168,20 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     std::vector<int32_t> prompt;
     int pages = 0;
   };
-  const int cap = capacity(), max_ctx = eng_->max_ctx();
+  // engine geometry: re-read after a failover (the replacement runs on fewer GPUs, so its KV
+  // pool, context and slot count can all be smaller)
+  int cap = capacity(), max_ctx = eng_->max_ctx();
   // paged KV (kvpager.h): a request is admitted only when the pool can hold its prompt plus every
   // token it may generate on top of what the running requests may still grow into, so a decode
   // round never runs out of pages; requests that do not fit wait (FIFO) for pages to come back
-  const int pool = eng_->kv_pages();
+  int pool = eng_->kv_pages();
   int reserved = 0;
   std::deque<Pending> waiting;
   std::vector<std::unique_ptr<Live>> live(cap);
+  auto pages_for = [&](long prompt_len, int n_predict) {
+    const long want = prompt_len + std::max(0, n_predict) + 1;
+    return (int)std::min<long>({(want + 63) / 64, (long)max_ctx / 64, (long)pool});
+  };
   auto consume = [&](int slot, int32_t t) -> bool {   // false: the request is finished
     Live& L = *live[slot];
     GenResult& r = L.res;
@@ -220,17 +226,40 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       ++failovers_;
       MP_LOGW("serve: failed over after \"%s\" (%d); re-admitting the running requests", e.what(), failovers_);
     }
+    cap = capacity();
+    max_ctx = eng_->max_ctx();
+    pool = eng_->kv_pages();
     std::vector<std::unique_ptr<Live>> moved;
     for (auto& l : live)
       if (l) moved.push_back(std::move(l));
-    if (moved.empty()) return false;
+    live.clear();
+    live.resize(cap);
+    reserved = 0;
+    for (auto& pd : waiting) pd.pages = pages_for((long)pd.prompt.size(), pd.s.req.n_predict);
+    // re-admit in order while the new engine has a slot, the context and the pages for the
+    // request's prompt + produced tokens + what it may still generate; the rest stop ("context")
     std::vector<std::vector<int32_t>> prompts;
-    for (size_t i = 0; i < moved.size(); ++i) {
-      std::vector<int32_t> pr = moved[i]->prompt;
-      pr.insert(pr.end(), moved[i]->res.tokens.begin(), moved[i]->res.tokens.end());
-      prompts.push_back(std::move(pr));
-      live[i] = std::move(moved[i]);
+    for (auto& m : moved) {
+      std::vector<int32_t> pr = m->prompt;
+      pr.insert(pr.end(), m->res.tokens.begin(), m->res.tokens.end());
+      const int pages = pages_for((long)m->prompt.size(), m->s.req.n_predict);
+      if ((int)prompts.size() < cap && (int)pr.size() + 1 < max_ctx && reserved + pages <= pool) {
+        m->pages = pages;
+        reserved += pages;
+        live[prompts.size()] = std::move(m);
+        prompts.push_back(std::move(pr));
+        continue;
+      }
+      Live& L = *m;
+      L.res.stop = "context";
+      if (!L.acc.buf.empty()) {
+        L.res.text += L.acc.buf;
+        if (L.s.req.on_piece) L.s.req.on_piece(L.acc.buf);
+      }
+      L.res.decode_ms = now_ms() - L.t1;
+      if (L.s.done) L.s.done(L.res);
     }
+    if (prompts.empty()) return false;
     eng_->start(prompts);   // a replacement fault propagates (the handler already had its turn)
     for (size_t i = 0; i < prompts.size(); ++i)
       if (!consume((int)i, eng_->last_token((int)i))) finish((int)i);
@@ -245,8 +274,7 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
         Pending pd;
         pd.prompt = encode(f.req.prompt);
         if ((int)pd.prompt.size() >= max_ctx) pd.prompt.erase(pd.prompt.begin(), pd.prompt.end() - (max_ctx / 2));
-        const long want = (long)pd.prompt.size() + std::max(0, f.req.n_predict) + 1;
-        pd.pages = (int)std::min<long>({(want + 63) / 64, (long)max_ctx / 64, (long)pool});
+        pd.pages = pages_for((long)pd.prompt.size(), f.req.n_predict);
         pd.s = std::move(f);
         waiting.push_back(std::move(pd));
       }

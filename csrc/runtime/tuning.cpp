@@ -1,0 +1,80 @@
+#include "tuning.h"
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+namespace mp {
+
+namespace {
+
+struct KnobDef {
+  const char* name;   // MIPIPE_<name>
+  int dflt, lo, hi;   // valid range [lo, hi]
+  bool (*valid)(int); // extra check (nullptr: range only)
+};
+
+bool ns_ok(int v) { return v == 2 || v == 3 || v == 4; }
+bool nw_ok(int v) { return v == 4 || v == 8; }
+bool g_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; }
+
+const KnobDef kDefs[KNOB_COUNT] = {
+    {"ATTN_PF_MAXWG", 1 << 30, 0, 1 << 30, nullptr},
+    {"ATTN_WG_TARGET", 256, 1, 1 << 20, nullptr},
+    {"GEMM2_SPLIT_WG", 256, 1, 1 << 20, nullptr},
+    {"GEMM2_TW1_BELOW", 128, 0, 1 << 20, nullptr},
+    {"GEMVS_NS", 2, 2, 4, ns_ok},
+    {"GEMVS_S", 64, 1, 1 << 20, nullptr},
+    {"GEMVS2", 1, 0, 1, nullptr},
+    {"GEMVS_MINWG", 256, 1, 1 << 20, nullptr},
+    {"GEMVS_G", 0, 0, 8, g_ok},
+    {"GEMVS_SPLIT", 0, 0, 1 << 16, nullptr},
+    {"MOE_V", 2, 1, 2, nullptr},
+    {"GEMV_NW", 8, 4, 8, nw_ok},
+    {"GEMV2_TW", 0, 0, 2, nullptr},
+};
+
+std::atomic<int> g_vals[KNOB_COUNT];
+std::once_flag g_once;
+
+bool ok(const KnobDef& d, int v) { return v >= d.lo && v <= d.hi && (!d.valid || d.valid(v)); }
+
+void init() {
+  for (int i = 0; i < KNOB_COUNT; ++i) {
+    const KnobDef& d = kDefs[i];
+    int v = d.dflt;
+    const std::string env = std::string("MIPIPE_") + d.name;
+    if (const char* e = std::getenv(env.c_str())) {
+      char* end = nullptr;
+      const long x = std::strtol(e, &end, 10);
+      if (end != e && *end == 0 && ok(d, (int)x)) v = (int)x;
+      else std::fprintf(stderr, "mipipe: ignoring %s=%s (invalid value; using %d)\n", env.c_str(), e, d.dflt);
+    }
+    g_vals[i].store(v, std::memory_order_relaxed);
+  }
+}
+
+}  // namespace
+
+int knob(Knob k) {
+  std::call_once(g_once, init);
+  return g_vals[k].load(std::memory_order_relaxed);
+}
+
+void set_knob(const char* name, int value) {
+  std::call_once(g_once, init);
+  for (int i = 0; i < KNOB_COUNT; ++i)
+    if (std::strcmp(kDefs[i].name, name) == 0) {
+      if (!ok(kDefs[i], value))
+        throw std::invalid_argument(std::string("set_knob: value out of range for ") + name);
+      g_vals[i].store(value, std::memory_order_relaxed);
+      return;
+    }
+  throw std::invalid_argument(std::string("set_knob: unknown knob ") + name);
+}
+
+}  // namespace mp

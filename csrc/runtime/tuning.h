@@ -1,0 +1,33 @@
+// Kernel-launch tuning knobs: one registry instead of per-call-site `static getenv` lambdas.
+//
+// Every knob starts from its default, is overridden once from its MIPIPE_* environment variable
+// (read on first use, invalid values rejected with a warning), and can be changed at any time with
+// set_knob() (C API mp_set_knob), so an in-process A/B run measures the value it names instead of
+// whatever the first launch froze.  Reads are a relaxed atomic load: cheap on launch paths.
+#pragma once
+
+namespace mp {
+
+enum Knob : int {
+  KNOB_ATTN_PF_MAXWG = 0,   // decode attention: next-chunk prefetch variant while M * Hkv <= this
+  KNOB_ATTN_WG_TARGET,      // decode attention: workgroup target of the automatic KV split
+  KNOB_GEMM2_SPLIT_WG,      // gemm2: workgroup target of its split-K
+  KNOB_GEMM2_TW1_BELOW,     // gemm2: one tile per wave below this many two-tile workgroups
+  KNOB_GEMVS_NS,            // gemvs: weight super-blocks in flight per wave (2, 3 or 4)
+  KNOB_GEMVS_S,             // gemvs: super-blocks per wave target of the work split
+  KNOB_GEMVS2,              // gemvs: q+k | v of mixed-type layers in one launch (0 / 1)
+  KNOB_GEMVS_MINWG,         // gemvs: fewest workgroups before halving the tiles per workgroup
+  KNOB_GEMVS_G,             // gemvs: force tiles per workgroup (0 auto, 1, 2, 4, 8)
+  KNOB_GEMVS_SPLIT,         // gemvs: force the k-split over the grid (0 auto)
+  KNOB_MOE_V,               // MoE GEMV version (1 | 2)
+  KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
+  KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
+  KNOB_COUNT
+};
+
+int knob(Knob k);
+// name is the knob's environment variable without the MIPIPE_ prefix (e.g. "GEMVS_NS");
+// throws std::invalid_argument for an unknown name or a value outside the knob's range
+void set_knob(const char* name, int value);
+
+}  // namespace mp

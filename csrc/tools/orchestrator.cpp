@@ -328,9 +328,19 @@ void serve_model(Server& S, ModelSlot* slot, const std::string& model) {
     if (!slot->eng) return nullptr;
     const Json cfg2 = Engine::failover_config(slot->cfg, slot->eng->health());
     MP_LOGW("orchestrator: engine of model %s faulted (%s); failing over", slot->name.c_str(), err.c_str());
+    // free the faulted engine's weights and KV on the surviving GPUs BEFORE the replacement sizes
+    // and allocates its own there (it carries more layers per GPU and an auto-sized KV pool)
+    std::unique_ptr<Engine> old;
+    bool dflt = false;
+    {
+      std::lock_guard<std::mutex> l(S.eng_mu);
+      dflt = S.eng == slot->eng.get();
+      if (dflt) S.eng = nullptr;
+      old = std::move(slot->eng);
+    }
+    old.reset();
     std::unique_ptr<Engine> e(new Engine(cfg2));
     std::lock_guard<std::mutex> l(S.eng_mu);
-    const bool dflt = S.eng == slot->eng.get();
     slot->eng = std::move(e);
     slot->cfg = cfg2;
     slot->restarts++;

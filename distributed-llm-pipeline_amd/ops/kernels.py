@@ -109,23 +109,35 @@ def gemv_small(w: PackedWeight, epi: int = EPI_STORE, *, x: torch.Tensor | None 
 
 
 def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor | None = None,
-         n_valid: int | None = None, v: int = 2) -> torch.Tensor:
-    """Prefill GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC = single-owner add).
-    v=2: 128-row x 256-column workgroup tiles (launch_gemm2); v=1: the 64 x 64 tile GEMM."""
+         n_valid: int | None = None, v: int = 3, allow_split: bool = True) -> torch.Tensor:
+    """Prefill / wide-decode GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC adds).
+    v=3: BM x BN in {128, 256}^2 workgroup tiles, weights dequantized once per workgroup into LDS
+    (launch_gemm3; ATOMIC may split K over workgroups unless allow_split is False); v=2: 128-row x
+    256-column tiles with per-wave register dequant (launch_gemm2); v=1: the 64 x 64 tile GEMM."""
     assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
     M = x.shape[0]
-    fn = N.lib().mp_op_gemm2 if v == 2 else N.lib().mp_op_gemm
+    L = N.lib()
+    if v == 3:
+        fn = lambda *a: L.mp_op_gemm3(*a[:-1], int(allow_split), a[-1])
+    else:
+        fn = L.mp_op_gemm2 if v == 2 else L.mp_op_gemm
     if epi == EPI_SWIGLU:
         F = w.n // 2
         h = torch.zeros(M, F, dtype=torch.float16, device=x.device) if y is None else y
         N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, None, 0,
-                                   _ptr(h), h.stride(0), F if n_valid is None else n_valid, _stream()), "gemm")
+                   _ptr(h), h.stride(0), F if n_valid is None else n_valid, _stream()), "gemm")
         return h
     if y is None:
         y = torch.zeros(M, w.n, dtype=torch.float32, device=x.device)
     N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
-                               y.stride(0), None, 0, w.n if n_valid is None else n_valid, _stream()), "gemm")
+               y.stride(0), None, 0, w.n if n_valid is None else n_valid, _stream()), "gemm")
     return y
+
+
+def set_gemm3_tuning(bm: int = 0, bn: int = 0, nsplit: int = 0, split_wg: int = 0) -> None:
+    """Force the v3 GEMM's tile rows / columns (128 | 256) and ATOMIC split-K factor (0 = auto);
+    split_wg: workgroup target of the automatic split (default 256)."""
+    N.lib().mp_set_gemm3_tuning(bm, bn, nsplit, split_wg)
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, k_pad: int | None = None) -> torch.Tensor:

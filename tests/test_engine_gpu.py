@@ -95,6 +95,11 @@ def test_fp8_kv_cache_checkpoint_and_batch(cuda, native, model_dir, tmp_path):
         eng.load_state(str(tmp_path / "st"))
         eng.decode(5)
         assert eng.tokens() == full
+    # an fp8 checkpoint is refused by an f16-KV engine (and vice versa): the fingerprint names the
+    # KV dtype and the payload size is checked against the stage's own kv_state_bytes
+    with Engine(**dict(kw, kv_dtype="f16")) as eng:
+        with pytest.raises(RuntimeError, match="load_state"):
+            eng.load_state(str(tmp_path / "st"))
     alone = []
     with Engine(gguf=path, max_ctx=512, prefill_chunk=64, kv_dtype="fp8") as eng:
         for p in prompts:

@@ -127,4 +127,29 @@ def test_elastic_rank_restart_resumes_from_checkpoint(native, model_dir, tmp_pat
     outs = [json.loads(l[4:]) for l in p.stdout.splitlines() if l.startswith("OUT ")]
     assert {o["restart"] for o in outs} == {"1"}, outs       # only the restarted attempt finished
     assert all(o["out"] == ref for o in outs)
-    assert (ckpt / "replica0" / "round_00000009" / "COMPLETE").exists()   # last checkpoint before the end
+    assert not list((ckpt / "replica0").glob("round_*"))   # a finished run removes its checkpoints
+
+
+def test_elastic_checkpoint_of_another_run_is_ignored(native, model_dir, tmp_path):
+    """A checkpoint left by one run (other prompts / n_predict) on the same directory is not resumed
+    by the next run: the next run generates its own prompts from scratch."""
+    from mipipe.engine import Engine
+    from mipipe.parallel import elastic as E
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    kw = dict(gguf=path, backend="cpu", max_ctx=128, prefill_chunk=16)
+    root = tmp_path / "ckpt"
+    # a stale, COMPLETE checkpoint of an older run (other prompts) in replica 0's directory
+    with Engine(**kw) as eng:
+        eng.start([[11, 12, 13]])
+        eng.decode(4)
+        d = root / "replica0" / "round_00000004"
+        d.parent.mkdir(parents=True)
+        eng.save_state(str(d))
+        (d / "RUN").write_text(E.run_digest([[11, 12, 13]], 20, dict(kw, pp=None, every=4)))
+        (d / "COMPLETE").write_text("")
+    prompts = [[5, 6, 7, 8]]
+    with Engine(**kw) as eng:
+        ref, _ = eng.generate(prompts, 9)
+    out = E.generate_elastic(prompts, 9, str(root), every=4, **kw)
+    assert out == ref
+    assert (root / "replica0" / "round_00000004").exists()   # another run's checkpoint is left alone

@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--target", type=int, default=2048)
     ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 store, 1 atomic): timing probes")
     ap.add_argument("--copies", type=int, default=0, help="weight copies cycled (default: enough to defeat the 256 MiB MALL; 1 = hot)")
-    ap.add_argument("--gemm", type=int, default=0, help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256)")
+    ap.add_argument("--gemm", type=int, default=0,
+                    help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256 per-wave dequant, 3: LDS-shared dequant)")
+    ap.add_argument("--g3", default="0,0,0", help="v3 GEMM tuning BM,BN,nsplit (0 = auto); ';'-separated list sweeps")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -58,8 +60,10 @@ def main():
                 X = torch.randn(M, k_pad, device="cuda").half()
                 Y = torch.zeros(M, n, device="cuda")
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
-                for tpw in [int(t) for t in a.tpw.split(",")]:
+                for tpw, g3 in [(int(t), g) for t in a.tpw.split(",") for g in a.g3.split(";")]:
                     L.mp_set_gemv_tpw(tpw)
+                    bm, bn, g3s = [int(v) for v in g3.split(",")]
+                    L.mp_set_gemm3_tuning(bm, bn, g3s, 0)
                     waves = (ntiles + max(tpw, 1) - 1) // max(tpw, 1)
                     if a.gemm or epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
                         splits = [1]
@@ -69,6 +73,12 @@ def main():
                         splits = [int(s) for s in a.splits.split(",")]
                     for nsplit in splits:
                         def run(W):
+                            if a.gemm == 3:
+                                N.check(L.mp_op_gemm3(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
+                                                      ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
+                                                      n, ctypes.c_void_p(H.data_ptr()), n // 2,
+                                                      n if epi != EPI_SWIGLU else n // 2, 1, st()), "gemm3")
+                                return
                             if a.gemm:
                                 fn = L.mp_op_gemm2 if a.gemm == 2 else L.mp_op_gemm
                                 N.check(fn(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
@@ -92,7 +102,8 @@ def main():
                         us = e0.elapsed_time(e1) * 1e3 / a.iters
                         print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
                                               GBps=round(nbytes / us / 1e3, 1),
-                                              TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm)), flush=True)
+                                              TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
+                                              g3=g3 if a.gemm == 3 else None)), flush=True)
             del Ws
             torch.cuda.empty_cache()
 
