@@ -9,15 +9,20 @@ node) + p50/token, Llama-3-70B PP=8 and 8B PP=1"; reference headline 2-3 tok/s f
 Weights are random-init directly in HBM with the exact Llama-3-70B architecture and Q4_K block
 format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
 cost-balanced split with the LM head on the last stage); activations move stage to stage with
-RCCL send/recv over xGMI; N + 1 micro-batches (N > 1) of `--mb-size` sequences circulate through
-the piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the decode
-projections run on the dequant MFMA GEMM (128 rows x 256 columns per workgroup), which reads each
-weight super-block once per 128 rows instead of issuing 4 MFMA row groups per fragment in the GEMV
-(70B PP=1: mb64 3.85k, mb256 5.36k, mb512 5.61k tok/s, profiles/r5a_wide_mb_sweep.txt);
---mb-size 1 gives the single-stream latency.  Weak scaling: per-GPU work is fixed (every stage
-streams its own weights once per micro-batch per round), global batch = n_mb * mb_size sequences.
-The timed region is exactly K decode rounds (every sequence emits one token per round),
-bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
+RCCL send/recv over xGMI (bf16 wire); N + 1 micro-batches (N > 1) of `--mb-size` sequences
+circulate through the piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of
+HBM: above 64 rows the decode projections run on the dequant MFMA GEMM v3 (gemm3.hip: weights
+dequantized once per workgroup into LDS, 256 x 256 tiles).  Weak scaling: per-GPU work is fixed
+(every stage streams its own weights once per micro-batch per round), global batch =
+n_mb * mb_size sequences.  The timed region is exactly K decode rounds (every sequence emits one
+token per round), bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over
+ranks is reported.
+
+At N = 1 the same run also measures, with the same bracket, the other named BASELINE config
+(Llama-3-8B Q4_K_M PP=1, single stream) and the round-1 like-for-like point (70B, 64 sequences):
+"secondary" in the JSON line (--no-secondary skips them).  For N > 1 the line reports the data
+plane the engine built ("link": transport kind, RCCL communicator sizes as ncclCommCount returns
+them, bf16 wire bytes per token per boundary).
 """
 import argparse
 import json
@@ -43,6 +48,51 @@ MODELS = {
                       vocab=32000, rope_base=10000.0),
 }
 
+# (label, model, ftype, mb_size): the other BASELINE config and the round-1 like-for-like point
+SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1),
+             ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64)]
+
+
+def parse_set(items):
+    out = {}
+    for kv in items:
+        k, v = kv.split("=", 1)
+        out[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
+    return out
+
+
+def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu):
+    """Start n_seq synthetic prompts, warm up, time exactly `steps` decode rounds; returns
+    (ms, p50 ms, engine info) with ms and p50 the MAX over ranks."""
+    eng = eng_factory()
+    try:
+        g = torch.Generator().manual_seed(0)
+        prompts = torch.randint(3, vocab, (n_seq, prompt_len), generator=g).tolist()
+        eng.start(prompts)
+        if warmup:
+            eng.decode(warmup)
+
+        def bracket():
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+
+        bracket()
+        t0 = time.perf_counter()
+        st = eng.decode(steps)
+        bracket()
+        ms = (time.perf_counter() - t0) * 1e3
+        tms = sorted(st.get("token_ms", []))
+        p50 = tms[len(tms) // 2] if tms else 0.0
+        vals = torch.tensor([ms, p50], dtype=torch.float64, device="cpu" if pg_cpu else "cuda")
+        if world > 1:
+            dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
+        from mipipe import _native as N
+        info = N.jcall(N.lib().mp_engine_info, eng._h, what="engine info")
+        return float(vals[0]), float(vals[1]), info
+    finally:
+        eng.close()
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -61,13 +111,16 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--link", default="rccl", choices=["rccl", "tcp"], help="stage-to-stage transport (N > 1)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on GPU 0 with a gloo process group and TCP links: rehearses the N > 1 path on a "
+                         "1-GPU box (RCCL refuses two ranks of a communicator on one GPU)")
+    ap.add_argument("--no-secondary", action="store_true", help="N = 1: skip the secondary configs")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra engine option (A/B runs), e.g. --set fused_norm=false")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             print("bench.py: --gpus > 1 must be launched with torchrun (one rank per GPU)", file=sys.stderr)
@@ -79,45 +132,47 @@ def main():
         print(f"bench.py: --pp {pp} does not divide {world} GPUs", file=sys.stderr)
         sys.exit(2)
     replicas = world // pp
+    link = "tcp" if args.same_device else args.link
+    tr_kw = dict(device=0, pg_backend="gloo") if args.same_device else {}
+    pg_cpu = args.same_device
+
+    def factory(model, ftype, mb_size, n_mb):
+        max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
+        cfg = dict(synthetic=MODELS[model], ftype=ftype, n_mb=n_mb, mb_size=mb_size, max_ctx=max_ctx,
+                   prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
+        cfg.update(parse_set(args.set))
+        # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
+        # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
+        return lambda: init_from_torchrun(pp=pp, link=link, **tr_kw, **cfg)
+
     n_mb = args.n_mb or (pp + 1 if pp > 1 else 1)
-    max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
-    cfg = dict(synthetic=MODELS[args.model], ftype=args.ftype, n_mb=n_mb, mb_size=args.mb_size, max_ctx=max_ctx,
-               prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
-    for kv in args.set:
-        k, v = kv.split("=", 1)
-        cfg[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
-    # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
-    # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
-    eng = init_from_torchrun(pp=pp, link=args.link, **cfg)
-    g = torch.Generator().manual_seed(0)
-    prompts = torch.randint(3, MODELS[args.model]["vocab"], (n_mb * args.mb_size, args.prompt_len),
-                            generator=g).tolist()
-    eng.start(prompts)
-    if args.warmup:
-        eng.decode(args.warmup)
-
-    def bracket():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    bracket()
-    t0 = time.perf_counter()
-    st = eng.decode(args.steps)
-    bracket()
-    ms = (time.perf_counter() - t0) * 1e3
-
-    tms = sorted(st.get("token_ms", []))
-    p50 = tms[len(tms) // 2] if tms else 0.0
-    vals = torch.tensor([ms, p50], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
-    ms, p50 = float(vals[0]), float(vals[1])
+    ms, p50, info = run(factory(args.model, args.ftype, args.mb_size, n_mb), MODELS[args.model]["vocab"],
+                        n_mb * args.mb_size, args.prompt_len, args.steps, args.warmup, world, pg_cpu)
     n_tok = args.steps * n_mb * args.mb_size * replicas
     value = n_tok / (ms / 1e3)
+
+    secondary = {}
+    if world == 1 and not args.no_secondary:
+        for label, model, ftype, mb in SECONDARY:
+            if model == args.model and ftype == args.ftype and mb == args.mb_size:
+                continue
+            sms, sp50, _ = run(factory(model, ftype, mb, 1), MODELS[model]["vocab"], mb, args.prompt_len,
+                               args.steps, args.warmup, world, pg_cpu)
+            secondary[label] = dict(tok_s=round(args.steps * mb / (sms / 1e3), 2), ms_per_round=round(sms / args.steps, 4),
+                                    p50_token_ms=round(sp50, 4))
+
+    link_info = None
+    if world > 1:
+        links = info.get("links", [])
+        link_info = dict(kind=sorted({l["kind"] for l in links}), comm_nranks=sorted({l["comm_nranks"] for l in links}),
+                         links_per_rank=len(links), act_dtype=info.get("act_dtype"),
+                         wire_bytes_per_token=info.get("wire_bytes_per_token"),
+                         torch_pg_world=dist.get_world_size(), torch_pg_backend=dist.get_backend(),
+                         same_device=args.same_device)
+
     if rank == 0:
         m = MODELS[args.model]
-        print(json.dumps({
+        line = {
             "metric": "decode tokens/sec (whole node) + p50/token",
             "value": round(value, 2),
             "unit": "tokens/s",
@@ -137,10 +192,14 @@ def main():
             "config": {"model": f"{m['name']} {args.ftype}", "global_batch": n_mb * args.mb_size * replicas,
                        "seq_len": args.prompt_len,
                        "parallelism": f"pp{pp}" if replicas == 1 else f"dp{replicas}xpp{pp}",
-                       "micro_batches": n_mb, "mb_size": args.mb_size, "max_ctx": max_ctx,
-                       "stages": eng.info["stages"]},
-        }), flush=True)
-    eng.close()
+                       "micro_batches": n_mb, "mb_size": args.mb_size, "max_ctx": info["max_ctx"],
+                       "stages": info["stages"]},
+        }
+        if secondary:
+            line["secondary"] = secondary
+        if link_info:
+            line["link"] = link_info
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

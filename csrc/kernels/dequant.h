@@ -270,6 +270,16 @@ template <> struct Deq<P_Q4_0> {
   }
 };
 
+// bf16 pair (low, high halves of w) -> f16 pair: exact for every bf16 inside f16's normal range
+// (8 significant bits into 11); v_cvt_pkrtz rounds toward zero, so a bf16 beyond 65504 becomes
+// +-65504 (saturation) instead of an infinity
+__device__ __forceinline__ uint32_t bf2_to_h2(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)));
+}
+__device__ __forceinline__ half8_t bf8_to_h8(const u32x4& v) {
+  return pack8(bf2_to_h2(v.x), bf2_to_h2(v.y), bf2_to_h2(v.z), bf2_to_h2(v.w));
+}
+
 // ------------------------------------------------------------------ F16 (plain)
 template <> struct Deq<P_F16> {
   static constexpr int CB = chunk_bytes(P_F16);
@@ -286,6 +296,25 @@ template <> struct Deq<P_F16> {
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = __builtin_bit_cast(half8_t, r.v[4 * H + s]);
+  }
+};
+
+// ------------------------------------------------------------------ BF16 (F16 layout, bf16 bits)
+template <> struct Deq<P_BF16> {
+  static constexpr int CB = chunk_bytes(P_BF16);
+  struct Raw { u32x4 v[8]; };
+  __device__ static __forceinline__ void load(Raw& r, const uint8_t* c, int lane) { load(r, PtrSrc{c}, lane); }
+  template <class S>
+  __device__ static __forceinline__ void load(Raw& r, const S& c, int lane) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = c.q16nt(i * 1024 + lane * 16);
+  }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts&) { dequant<H>(r, b, lane); }
+  template <int H>
+  __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) b[s] = bf8_to_h8(r.v[4 * H + s]);
   }
 };
 

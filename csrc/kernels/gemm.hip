@@ -131,6 +131,7 @@ void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st) {
     case P_Q8_0: gemm_pt<P_Q8_0>(epi, p, st); break;
     case P_Q4_0: gemm_pt<P_Q4_0>(epi, p, st); break;
     case P_F16: gemm_pt<P_F16>(epi, p, st); break;
+    case P_BF16: gemm_pt<P_BF16>(epi, p, st); break;
   }
 }
 

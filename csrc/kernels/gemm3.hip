@@ -40,13 +40,13 @@ __device__ __forceinline__ int g3_swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int g3_off(int row, int c) { return row * 128 + ((c ^ g3_swz(row)) << 4); }
 __device__ __forceinline__ int g3_perm(int r) { return ((r & 7) << 1) | (r >> 3); }
 
-// global -> LDS DMA of SZ bytes per lane (LDS destination: wave-uniform base + lane * SZ); the size
-// operand must be a literal
+// global -> LDS DMA of SZ (16 | 4) bytes per lane (LDS destination: wave-uniform base + lane * SZ;
+// the sub-dword forms are not used: they land a dword per lane); the size must be a literal
 template <int SZ>
 __device__ __forceinline__ void glds(const void* g, char* lds) {
+  static_assert(SZ == 16 || SZ == 4, "glds: 16 or 4 bytes per lane");
   if constexpr (SZ == 16) __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 16, 0, 0);
-  else if constexpr (SZ == 4) __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 4, 0, 0);
-  else __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 2, 0, 0);
+  else __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 4, 0, 0);
 }
 
 // Q4_K / Q5_K scale words of quarter g (= stage q of the super-block): (d sc(2g), d sc(2g+1)),
@@ -74,8 +74,14 @@ __device__ __forceinline__ uint32_t g3_word(const u32x4& v, int part, int j) {
 // super-block.  Dequant entry e (< 32 NT): h = e / (16 NT) (k half of the quarter: wave-uniform),
 // tile T = (e >> 4) % NT, column perm(e & 15); dequant<NS> produces its 8-k chunks part * NS + j,
 // j < NS (NS = 4: one thread per entry; NS = 2: two, part wave-uniform).  Segments are filled by 1-KB wave pieces
-// (64 lanes x 16 B, or 64 x 4 B / 64 x 2 B for the small fields), entry i of a segment at i * ES.
+// (64 lanes x 16 B, or 64 x 4 B for the small fields), entry i of a segment at i * ES.
 template <int PT> struct G3;
+// how a stage's weights reach the f16 B image:
+//   G3_RAW_LDS: raw quant bytes by global_load_lds into R, dequantized LDS -> VALU -> LDS
+//   G3_DIRECT:  the packed f16 bytes by global_load_lds straight into B (16-bit f16 weights)
+//   G3_REG:     16-B loads into registers one stage ahead, converted and written (bf16 weights:
+//               their raw bytes are as large as the f16 image, too big for an LDS raw buffer)
+enum { G3_RAW_LDS = 0, G3_DIRECT = 1, G3_REG = 2 };
 
 struct G3Ctx {           // per-stage source addressing (wave-uniform)
   const uint8_t* W;      // packed matrix
@@ -96,7 +102,7 @@ __device__ __forceinline__ void g3_segment(char* dst, int n, int wave, int lane,
 
 template <> struct G3<P_Q4_K> {
   static constexpr int CB = chunk_bytes(P_Q4_K);
-  static constexpr bool DIRECT = false;
+  static constexpr int MODE = G3_RAW_LDS;
   static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 256; }
   __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
     g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
@@ -126,7 +132,7 @@ template <> struct G3<P_Q4_K> {
 
 template <> struct G3<P_Q5_K> {
   static constexpr int CB = chunk_bytes(P_Q5_K);
-  static constexpr bool DIRECT = false;
+  static constexpr int MODE = G3_RAW_LDS;
   static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 128 + NT * 256; }
   __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
     g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
@@ -165,9 +171,10 @@ template <> struct G3<P_Q5_K> {
 
 template <> struct G3<P_Q6_K> {
   static constexpr int CB = chunk_bytes(P_Q6_K);
-  static constexpr bool DIRECT = false;
-  // quants 16 B, high bits 8 B (two 4-B entries), int8 scales 4 B per row, d 2 B per row
-  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 256 + NT * 64 + NT * 32; }
+  static constexpr int MODE = G3_RAW_LDS;
+  // quants 16 B, high bits 8 B (two 4-B entries), int8 scales 4 B per row, and per row the dword
+  // holding its f16 d (rows 2i, 2i+1 share one; the sub-dword LDS-DMA forms write a dword per lane)
+  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 256 + NT * 64 + NT * 64; }
   __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
     g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
       const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
@@ -178,7 +185,7 @@ template <> struct G3<P_Q6_K> {
       return c.chunk(T, CB) + 2048 + h * 512 + (16 * c.q + r) * 8 + 4 * (i & 1);
     });
     g3_segment<4>(R + NT * 768, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 3072 + (i & 15) * 16 + 4 * c.q; });
-    g3_segment<2>(R + NT * 832, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 3328 + (i & 15) * 2; });
+    g3_segment<4>(R + NT * 832, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 3328 + ((i & 15) >> 1) * 4; });
   }
   template <int NS>
   __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts& k, half8_t* b) {
@@ -186,7 +193,8 @@ template <> struct G3<P_Q6_K> {
     const u32x4 w4 = *reinterpret_cast<const u32x4*>(R + e * 16);
     const u32x2 qh = *reinterpret_cast<const u32x2*>(R + NT * 512 + e * 8);
     const uint32_t sc = *reinterpret_cast<const uint32_t*>(R + NT * 768 + (T * 16 + r) * 4);
-    const uint16_t dd = *reinterpret_cast<const uint16_t*>(R + NT * 832 + (T * 16 + r) * 2);
+    const uint32_t dw = *reinterpret_cast<const uint32_t*>(R + NT * 832 + (T * 16 + r) * 4);
+    const uint16_t dd = (uint16_t)((r & 1) ? dw >> 16 : dw);
     const f16 dh = __builtin_bit_cast(f16, dd);
     const uint32_t u = sc ^ 0x80808080u;
     const half2_t S2 = (as_h2(__builtin_amdgcn_perm(0x64646464u, u, h ? 0x04030402u : 0x04010400u)) - h2c(1152.f)) *
@@ -210,7 +218,7 @@ template <> struct G3<P_Q6_K> {
 
 template <> struct G3<P_Q8_0> {
   static constexpr int CB = chunk_bytes(P_Q8_0);
-  static constexpr bool DIRECT = false;
+  static constexpr int MODE = G3_RAW_LDS;
   static constexpr int raw_bytes(int NT) { return NT * 1024 + NT * 64; }
   __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
     g3_segment<16>(R, 64 * NT, wave, lane, [&](int i) {
@@ -241,7 +249,7 @@ template <> struct G3<P_Q8_0> {
 
 template <> struct G3<P_Q4_0> {
   static constexpr int CB = chunk_bytes(P_Q4_0);
-  static constexpr bool DIRECT = false;
+  static constexpr int MODE = G3_RAW_LDS;
   static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 64; }
   __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
     g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
@@ -270,7 +278,7 @@ template <> struct G3<P_Q4_0> {
 // 16-bit weights: the stage's B image is loaded directly (no raw image, no dequant)
 template <> struct G3<P_F16> {
   static constexpr int CB = chunk_bytes(P_F16);
-  static constexpr bool DIRECT = true;
+  static constexpr int MODE = G3_DIRECT;
   static constexpr int raw_bytes(int) { return 0; }
   // B image bytes [col][128 B]: piece of 1 KB = 8 columns; lane l -> column 8 pc + (l >> 3), image
   // chunk l & 7 = source chunk c ^ swz(col); source chunk c (k = 8c..8c+7 of the quarter) is packed
@@ -281,6 +289,26 @@ template <> struct G3<P_F16> {
       const int ch = (lane & 7) ^ g3_swz(col);
       glds<16>(c.chunk(col >> 4, CB) + ch * 1024 + (16 * c.q + (col & 15)) * 16, B + pc * 1024);
     }
+  }
+};
+
+// bf16 weights (F16 chunk layout, bf16 bits): entry e's chunks 4h + part NS + j of the quarter
+// (k = 8 c .. 8 c + 7 of column perm(r)) are element i = c of lane (q, r): byte c * 1024 + (16 q + r) * 16
+template <> struct G3<P_BF16> {
+  static constexpr int CB = chunk_bytes(P_BF16);
+  static constexpr int MODE = G3_REG;
+  static constexpr int raw_bytes(int) { return 0; }
+  template <int NS>
+  __device__ static __forceinline__ void load(const G3Ctx& c, int NT, int e, int part, u32x4* v) {
+    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
+    const uint8_t* src = c.chunk(T, CB) + (16 * c.q + r) * 16;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) v[j] = ld16_nt(src + (4 * h + NS * part + j) * 1024);
+  }
+  template <int NS>
+  __device__ static __forceinline__ void convert(const u32x4* v, half8_t* b) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j) b[j] = bf8_to_h8(v[j]);
   }
 };
 
@@ -329,12 +357,6 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
       glds<16>(p.X + (size_t)gr * p.ldx + k0 + 8 * ch, As + buf * A_BYTES + pc * 1024);
     }
   };
-  auto issue_b = [&](int s, int buf) {
-    ctx.sb = s >> 2; ctx.q = s & 3;
-    if constexpr (Q::DIRECT) Q::issue_b(Bs + buf * B_BYTES, ctx, NT, wave, lane);
-    else Q::issue(Rs + buf * R_BYTES, ctx, NT, wave, lane);
-  };
-  const Consts kc = make_consts();
   // all 512 threads dequantize: NT = 16 one entry each; NT = 8 half an entry each, waves 2k and
   // 2k + 1 sharing the entries of lanes 64 k .. (part = wave parity; h stays wave-uniform)
   constexpr int DQ_NS = 32 * NT == 512 ? 4 : 2;
@@ -342,13 +364,32 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   const int dq_e = DQ_NS == 4 ? tid : (lane | ((wave >> 1) << 6));
   const int dq_h = dq_e / (16 * NT);
   const int dq_col = 16 * ((dq_e >> 4) % NT) + g3_perm(dq_e & 15);
-  auto dequant = [&](int s, int buf) {   // raw R[buf] of stage s -> B[buf]
-    if constexpr (!Q::DIRECT) {
-      half8_t b[DQ_NS];
-      Q::template dequant<DQ_NS>(Rs + buf * R_BYTES, NT, dq_e, dq_part, s & 3, kc, b);
-      char* B = Bs + buf * B_BYTES;
+  u32x4 breg[G3<PT>::MODE == G3_REG ? DQ_NS : 1];   // G3_REG: raw of the next stage to convert
+  auto issue_b = [&](int s, int buf) {
+    ctx.sb = s >> 2; ctx.q = s & 3;
+    if constexpr (Q::MODE == G3_DIRECT) Q::issue_b(Bs + buf * B_BYTES, ctx, NT, wave, lane);
+    else if constexpr (Q::MODE == G3_RAW_LDS) Q::issue(Rs + buf * R_BYTES, ctx, NT, wave, lane);
+  };
+  auto load_breg = [&](int s, u32x4* v) {
+    if constexpr (Q::MODE == G3_REG) {
+      ctx.sb = s >> 2; ctx.q = s & 3;
+      Q::template load<DQ_NS>(ctx, NT, dq_e, dq_part, v);
+    }
+  };
+  const Consts kc = make_consts();
+  auto store_b = [&](const half8_t* b, int buf) {
+    char* B = Bs + buf * B_BYTES;
 #pragma unroll
-      for (int j = 0; j < DQ_NS; ++j) *reinterpret_cast<half8_t*>(B + g3_off(dq_col, 4 * dq_h + DQ_NS * dq_part + j)) = b[j];
+    for (int j = 0; j < DQ_NS; ++j) *reinterpret_cast<half8_t*>(B + g3_off(dq_col, 4 * dq_h + DQ_NS * dq_part + j)) = b[j];
+  };
+  auto dequant = [&](int s, int buf) {   // raw R[buf] (registers for G3_REG) of stage s -> B[buf]
+    half8_t b[DQ_NS];
+    if constexpr (Q::MODE == G3_RAW_LDS) {
+      Q::template dequant<DQ_NS>(Rs + buf * R_BYTES, NT, dq_e, dq_part, s & 3, kc, b);
+      store_b(b, buf);
+    } else if constexpr (Q::MODE == G3_REG) {
+      Q::template convert<DQ_NS>(breg, b);
+      store_b(b, buf);
     }
   };
 
@@ -361,10 +402,14 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   // prologue: A(0), B/raw(0), raw(1) -> dequant(0)
   issue_a(s_begin, 0);
   issue_b(s_begin, 0);
-  if constexpr (!Q::DIRECT) {
+  if constexpr (Q::MODE == G3_RAW_LDS) {
     if (s_begin + 1 < s_end) issue_b(s_begin + 1, 1);
     __syncthreads();
     dequant(s_begin, 0);
+  } else if constexpr (Q::MODE == G3_REG) {
+    load_breg(s_begin, breg);
+    dequant(s_begin, 0);
+    load_breg(min(s_begin + 1, s_end - 1), breg);
   }
   __syncthreads();
 
@@ -380,11 +425,10 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
     // stage into buffers nobody reads, the last dequant converts stale bytes into an unread buffer)
     const int s1 = min(s + 1, s_end - 1);
     issue_a(s1, cur ^ 1);
-    if constexpr (Q::DIRECT) {
-      issue_b(s1, cur ^ 1);
-    } else {
-      issue_b(min(s + 2, s_end - 1), cur);
-    }
+    if constexpr (Q::MODE == G3_DIRECT) issue_b(s1, cur ^ 1);
+    else issue_b(min(s + 2, s_end - 1), cur);
+    u32x4 bnext[Q::MODE == G3_REG ? DQ_NS : 1];   // G3_REG: raw(s+2), loaded while stage s computes
+    load_breg(min(s + 2, s_end - 1), bnext);
     const char* Ab = As + cur * A_BYTES;
     const char* Bb = Bs + cur * B_BYTES;
 #pragma unroll
@@ -404,6 +448,10 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
     // two B buffers), so written first it would serialise the whole dequant ahead of the first
     // MFMA; written here, its VALU is free to fill the MFMA stream and only the 4 stores trail it.
     dequant(s + 1, cur ^ 1);
+    if constexpr (Q::MODE == G3_REG) {
+#pragma unroll
+      for (int j = 0; j < DQ_NS; ++j) breg[j] = bnext[j];
+    }
     __syncthreads();
   }
 
@@ -512,6 +560,7 @@ void launch_gemm3(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_s
     case P_Q8_0: gemm3_pt<P_Q8_0>(epi, p, allow_split, st); break;
     case P_Q4_0: gemm3_pt<P_Q4_0>(epi, p, allow_split, st); break;
     case P_F16: gemm3_pt<P_F16>(epi, p, allow_split, st); break;
+    case P_BF16: gemm3_pt<P_BF16>(epi, p, allow_split, st); break;
   }
 }
 

@@ -88,6 +88,7 @@ void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, i
     case P_Q8_0: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q8_0>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
     case P_Q4_0: hipLaunchKernelGGL(mpk::unpack_kernel<P_Q4_0>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
     case P_F16: hipLaunchKernelGGL(mpk::unpack_kernel<P_F16>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
+    case P_BF16: hipLaunchKernelGGL(mpk::unpack_kernel<P_BF16>, grid, dim3(64), 0, st, W, nsb, out, ldo); break;
   }
 }
 

@@ -253,7 +253,7 @@ template <int PT, int EPI, int NW, int TW>
 static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
   if constexpr (TW == 1) {
     if (p.Xf) {   // fused RMSNorm: M <= 4 (checked by launch_gemv)
-      constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+      constexpr int NS = is16(PT) ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
       hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, NS, 1, 1, true>), dim3((p.ntiles + NW - 1) / NW, nsplit),
                          dim3(NW * 64), 0, st, p);
       return;
@@ -262,7 +262,7 @@ static void gemv2_go(const GemvParams& p, int nsplit, hipStream_t st) {
   // super-blocks in flight per wave: 4, fewer for the fat chunks so the kernel stays within
   // 128 VGPRs (4 waves per SIMD = two 8-wave workgroups per CU); two row groups (M <= 32) hold
   // twice the x ring, so one slot less
-  constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+  constexpr int NS = is16(PT) ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
   const dim3 block(NW * 64);
   if constexpr (TW == 1) {
     const dim3 grid((p.ntiles + NW - 1) / NW, nsplit);
@@ -289,7 +289,7 @@ static void gemv2_cfg(int epi, const GemvParams& p, int nsplit, hipStream_t st) 
 
 template <int PT>
 static void gemv2_pt(int epi, const GemvParams& p, int nsplit, int nw, int tw, hipStream_t st) {
-  if (PT != P_F16 && tw == 2 && p.M > 32) {
+  if (!is16(PT) && tw == 2 && p.M > 32) {
     if (nw == 8) gemv2_cfg<PT, 8, 2>(epi, p, nsplit, st);
     else gemv2_cfg<PT, 4, 2>(epi, p, nsplit, st);
   } else if (nw == 8) gemv2_cfg<PT, 8, 1>(epi, p, nsplit, st);
@@ -305,6 +305,7 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
     case P_Q8_0: gemv2_pt<P_Q8_0>(epi, p, nsplit, nw, tw, st); break;
     case P_Q4_0: gemv2_pt<P_Q4_0>(epi, p, nsplit, nw, tw, st); break;
     case P_F16: gemv2_pt<P_F16>(epi, p, nsplit, nw, tw, st); break;
+    case P_BF16: gemv2_pt<P_BF16>(epi, p, nsplit, nw, tw, st); break;
   }
 }
 

@@ -48,7 +48,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr int KSW = GS_NW / G;
-  constexpr int NS = NSO ? NSO : PT == P_F16 ? 2 : 4;   // weight super-blocks in flight per wave
+  constexpr int NS = NSO ? NSO : is16(PT) ? 2 : 4;   // weight super-blocks in flight per wave
   extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange]
   __shared__ float red[GS_NW][64];
   __shared__ float red_ss[GS_NW][4];
@@ -339,7 +339,7 @@ static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   // 8B Q4_K_M mb1 NS 2 / 3 / 4 / 8 -> 548 / 541 / 524 / 441 tok/s, 70B Q4_K 105.4 / 106.6 / 104.4 / 91.1
   // (the knob only admits 2, 3 and 4; 16-bit weights always run the default depth)
   const int ns = knob(KNOB_GEMVS_NS);
-  if constexpr (PT != P_F16) {
+  if constexpr (!is16(PT)) {
     if (ns == 2) return gemvs_gn<PT, EPI, NORM, 2>(p, pl, st);
     if (ns == 3) return gemvs_gn<PT, EPI, NORM, 3>(p, pl, st);
   }
@@ -422,6 +422,7 @@ void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStrea
     case P_Q8_0: gemvs_pt<P_Q8_0>(epi, p, pl, st); break;
     case P_Q4_0: gemvs_pt<P_Q4_0>(epi, p, pl, st); break;
     case P_F16: gemvs_pt<P_F16>(epi, p, pl, st); break;
+    case P_BF16: gemvs_pt<P_BF16>(epi, p, pl, st); break;
     default: throw std::runtime_error("launch_gemvs: unknown packed type");
   }
 }

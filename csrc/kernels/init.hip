@@ -24,12 +24,13 @@ __global__ void init_packed_kernel(uint8_t* W, size_t nbytes, int pt, float scal
   uint32_t v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = hash32(seed * 0x9E3779B97F4A7C15ULL + i * 4 + k);
-  if (pt == P_F16) {
+  if (pt == P_F16 || pt == P_BF16) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float a = ((v[k] & 0xFFFF) / 65536.f - 0.5f) * 3.4f * scale;
       const float b = ((v[k] >> 16) / 65536.f - 0.5f) * 3.4f * scale;
-      v[k] = (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16);
+      v[k] = pt == P_F16 ? (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16)
+                         : (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xFFFF0000u);   // bf16 (truncated)
     }
   } else if (pt == P_Q4_K || pt == P_Q5_K) {
     const int hdr0 = pt == P_Q4_K ? 2048 : 2560;

@@ -246,7 +246,7 @@ template <int PT, int EPI, int MT>
 static void moe2_go(const MoeGemvParams& p, int nsplit, hipStream_t st) {
   constexpr int NW = 8;
   // super-blocks in flight: as gemv2 (<= 128 VGPRs), one less per extra row group
-  constexpr int NS = PT == P_F16 ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
+  constexpr int NS = is16(PT) ? 2 : (PT == P_Q6_K || PT == P_Q8_0) ? 3 : 4;
   constexpr int NSL = MT == 1 ? NS : MT == 2 ? (NS > 2 ? NS - 1 : 2) : 2;
   const dim3 grid((p.ntiles + NW - 1) / NW, nsplit, p.E);
   hipLaunchKernelGGL((mpk::moe_gemv2_kernel<PT, EPI, NW, NSL, MT>), grid, dim3(NW * 64), 0, st, p);
@@ -284,6 +284,7 @@ void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_
     case P_Q8_0: moe_launch_pt<P_Q8_0>(epi, p, nsplit, st); break;
     case P_Q4_0: moe_launch_pt<P_Q4_0>(epi, p, nsplit, st); break;
     case P_F16: moe_launch_pt<P_F16>(epi, p, nsplit, st); break;
+    case P_BF16: moe_launch_pt<P_BF16>(epi, p, nsplit, st); break;
   }
 }
 

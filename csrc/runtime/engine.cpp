@@ -1627,6 +1627,27 @@ Json Engine::info() const {
   for (auto& w : workers_) { wb += w->stage->weight_bytes(); kb += w->stage->kv_bytes(); }
   j["weight_bytes_local"] = (int64_t)wb;
   j["kv_bytes_local"] = (int64_t)kb;
+  // the data plane as the transports report it: what each local stage sends and receives over,
+  // the communicator sizes RCCL itself returns, and the bytes one token moves across a boundary
+  Json ls = Json::array();
+  for (auto& w : workers_) {
+    for (int dir = 0; dir < 2; ++dir) {
+      const Link* l = dir ? w->in : w->out;
+      if (!l) continue;
+      Json o = Json::object();
+      o["stage"] = w->stage->spec().stage;
+      o["dir"] = dir ? "in" : "out";
+      o["kind"] = std::string(l->kind());
+      o["comm_nranks"] = l->comm_nranks();
+      o["bytes"] = (int64_t)l->bytes_sent;
+      o["msgs"] = (int64_t)l->msgs_sent;
+      ls.push(o);
+    }
+  }
+  j["links"] = ls;
+  const int ab = act_dtype_ == ACT_F32 ? 4 : 2;
+  j["act_dtype"] = act_dtype_ == ACT_F32 ? "f32" : act_dtype_ == ACT_F16 ? "f16" : "bf16";
+  j["wire_bytes_per_token"] = S_ > 1 ? (int64_t)cfg_.d_model * ab : 0;   // per stage boundary
   return j;
 }
 

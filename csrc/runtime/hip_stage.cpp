@@ -648,7 +648,7 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // per workgroup into LDS): every type, 16-bit weights included
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
   const bool v3 = opt_.prefill_gemm_v == 3;
-  const bool v2 = opt_.prefill_gemm_v == 2 && m.ptype != P_F16;
+  const bool v2 = opt_.prefill_gemm_v == 2 && !is16(m.ptype);
   if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;

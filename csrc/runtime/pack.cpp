@@ -147,6 +147,13 @@ static void pack_chunk(int t, int pt, const uint8_t* src, int64_t K, int64_t k0,
       }
       break;
     }
+    case P_BF16: {   // bits as stored in the GGUF (T_BF16 only)
+      for (int w = 0; w < 256 && k0 + w < K; ++w) {
+        const Pos p = pos_of(w, r);
+        std::memcpy(chunk + p.h * 4096 + p.s * 1024 + p.lane * 16 + p.j * 2, src + 2 * w, 2);
+      }
+      break;
+    }
     case P_F16: {
       for (int w = 0; w < 256 && k0 + w < K; ++w) {
         float v;

@@ -53,12 +53,16 @@ MP_HD inline int block_bytes(int t) {
 }
 inline size_t row_bytes(int t, int64_t n) { return (size_t)(n / block_elems(t)) * block_bytes(t); }
 
-// Packed kernel types (what the GEMV/GEMM kernels stream).  F32/BF16 weights are packed as F16.
-enum PackType : int { P_F16 = 0, P_Q8_0 = 1, P_Q4_K = 2, P_Q5_K = 3, P_Q6_K = 4, P_Q4_0 = 5 };
+// Packed kernel types (what the GEMV/GEMM kernels stream).  F32 weights are packed as F16; BF16
+// weights stay bf16 (P_BF16, same chunk layout as F16): no narrowing at pack time, the kernels
+// widen them on the fly.
+enum PackType : int { P_F16 = 0, P_Q8_0 = 1, P_Q4_K = 2, P_Q5_K = 3, P_Q6_K = 4, P_Q4_0 = 5, P_BF16 = 6 };
+constexpr bool is16(int p) { return p == P_F16 || p == P_BF16; }
 
 inline int pack_type_of(int ggml_type) {
   switch (ggml_type) {
-    case T_F32: case T_F16: case T_BF16: return P_F16;
+    case T_F32: case T_F16: return P_F16;
+    case T_BF16: return P_BF16;
     case T_Q8_0: return P_Q8_0; case T_Q4_0: return P_Q4_0;
     case T_Q4_K: return P_Q4_K; case T_Q5_K: return P_Q5_K; case T_Q6_K: return P_Q6_K;
     default: return -1;
@@ -67,7 +71,7 @@ inline int pack_type_of(int ggml_type) {
 
 // bytes of one (16-row tile, 256-k super-block) chunk
 constexpr int chunk_bytes(int p) {
-  return p == P_F16 ? 8192 : p == P_Q8_0 ? 4352 : p == P_Q4_K ? 2304 : p == P_Q5_K ? 2816
+  return is16(p) ? 8192 : p == P_Q8_0 ? 4352 : p == P_Q4_K ? 2304 : p == P_Q5_K ? 2816
        : p == P_Q6_K ? 3360 : p == P_Q4_0 ? 2304 : 0;
 }
 

@@ -124,6 +124,11 @@ void RcclLink::abort() {
   if (comm_ && owns_) ncclCommAbort((ncclComm_t)comm_);
   comm_ = nullptr;
 }
+int RcclLink::comm_nranks() const {
+  int n = 0;
+  if (comm_ && ncclCommCount((ncclComm_t)comm_, &n) != ncclSuccess) n = -1;
+  return n;
+}
 void RcclLink::send(const void* buf, size_t bytes, hipStream_t st) {
   if (!comm_) throw std::runtime_error("RcclLink: aborted");
   NCCL_OK(ncclSend(buf, bytes, ncclUint8, peer_, (ncclComm_t)comm_, st));

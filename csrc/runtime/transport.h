@@ -27,6 +27,9 @@ class Link {
   virtual void send(const void* buf, size_t bytes, hipStream_t st) = 0;
   virtual void recv(void* buf, size_t bytes, hipStream_t st) = 0;
   virtual const char* kind() const = 0;
+  // ranks of the communicator behind this link as the transport itself reports them (RCCL:
+  // ncclCommCount); 0 for transports without one
+  virtual int comm_nranks() const { return 0; }
   virtual void abort() {}
   // blocking waits give up after this long (a dead or stalled peer surfaces as an error)
   virtual void set_timeout(double s) { timeout_s = s; }
@@ -89,6 +92,7 @@ class RcclLink : public Link {
   void send(const void* buf, size_t bytes, hipStream_t st) override;
   void recv(void* buf, size_t bytes, hipStream_t st) override;
   const char* kind() const override { return "rccl"; }
+  int comm_nranks() const override;
   void abort() override;
   int rank() const { return rank_; }
   int peer() const { return peer_; }

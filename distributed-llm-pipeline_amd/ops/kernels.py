@@ -14,7 +14,7 @@ from .. import _native as N
 from ..utils import quants as Q
 
 EPI_STORE, EPI_ATOMIC, EPI_SWIGLU = 0, 1, 2
-P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0 = 0, 1, 2, 3, 4, 5
+P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0, P_BF16 = 0, 1, 2, 3, 4, 5, 6
 
 
 def _ptr(t: torch.Tensor | None):

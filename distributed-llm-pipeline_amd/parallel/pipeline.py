@@ -84,7 +84,7 @@ def simulate_piped_ring(stage_ms, n_mb: int, rounds: int = 16, link_ms: float = 
                 bubble=max(0.0, 1.0 - n_mb * max(stage_ms) / round_ms))
 
 
-def init_from_torchrun(pp: int | None = None, **cfg):
+def init_from_torchrun(pp: int | None = None, device: int | None = None, pg_backend: str | None = None, **cfg):
     """Build this rank's Engine stage under torchrun, with one process per GPU.
 
     `pp` is the pipeline depth (default: the world size). The world splits into world // pp
@@ -96,6 +96,11 @@ def init_from_torchrun(pp: int | None = None, **cfg):
     of each link creates its RCCL unique id, and the ids are exchanged with torch.distributed
     (backend "nccl", which is RCCL on ROCm). Keyword arguments are engine config keys (see
     mipipe.engine).
+
+    `device` overrides the GPU of this rank (default LOCAL_RANK) and `pg_backend` the
+    torch.distributed backend (default: "nccl" for GPU stages, "gloo" for CPU stages).  Several
+    ranks on ONE GPU (a rehearsal of the multi-rank path on a 1-GPU box) need device=0,
+    pg_backend="gloo" and link="tcp": RCCL refuses two ranks of one communicator on one GPU.
     """
     import torch
     import torch.distributed as dist
@@ -113,8 +118,9 @@ def init_from_torchrun(pp: int | None = None, **cfg):
     cpu = cfg.get("backend", "hip") == "cpu"
     if cpu:
         link = "tcp"   # RCCL moves device buffers; CPU stages talk over TCP
-    else:
-        torch.cuda.set_device(local_rank)
+    dev = local_rank if device is None else int(device)
+    if not cpu:
+        torch.cuda.set_device(dev)
     if world > 1 and not dist.is_initialized():
         kw = {}
         restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
@@ -126,27 +132,28 @@ def init_from_torchrun(pp: int | None = None, **cfg):
             base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
                                  timeout=timedelta(seconds=300))
             kw = dict(store=dist.PrefixStore(f"mipipe/attempt_{restart}", base), rank=rank, world_size=world)
-        if cpu:
+        backend = pg_backend or ("gloo" if cpu else "nccl")
+        if backend == "gloo":
             dist.init_process_group("gloo", **kw)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **kw)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev), **kw)
     if pp == 1:
         cfg.setdefault("mode", "local")
         cfg.setdefault("stages", 1)
-        cfg.setdefault("devices", [local_rank])
+        cfg.setdefault("devices", [dev])
         return Engine(**cfg)
     if cfg.get("device_speed") == "probe":
         # Halda: every rank measures its own device, the list is gathered so all ranks of the
         # replica derive the same cost-balanced partition
         from ..engine import device_probe
-        mine = device_probe(-1 if cpu else local_rank)["speed"]
+        mine = device_probe(-1 if cpu else dev)["speed"]
         speeds = [None] * world
         if world > 1:
             dist.all_gather_object(speeds, mine)
         else:
             speeds = [mine]
         cfg["device_speed"] = speeds[group * pp:(group + 1) * pp]
-    cfg.update(mode="mp", world=pp, rank=stage, device=local_rank, link=link)
+    cfg.update(mode="mp", world=pp, rank=stage, device=dev, link=link)
     if link == "rccl":
         ids = [None] * world
         dist.all_gather_object(ids, rccl_unique_id_hex())

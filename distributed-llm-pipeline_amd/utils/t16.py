@@ -10,14 +10,19 @@ import numpy as np
 
 from . import quants as Q
 
-P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0 = 0, 1, 2, 3, 4, 5
-CHUNK = {P_F16: 8192, P_Q8_0: 4352, P_Q4_K: 2304, P_Q5_K: 2816, P_Q6_K: 3360, P_Q4_0: 2304}
-PACK_OF = {Q.F32: P_F16, Q.F16: P_F16, Q.BF16: P_F16, Q.Q8_0: P_Q8_0, Q.Q4_0: P_Q4_0,
+P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0, P_BF16 = 0, 1, 2, 3, 4, 5, 6
+CHUNK = {P_F16: 8192, P_Q8_0: 4352, P_Q4_K: 2304, P_Q5_K: 2816, P_Q6_K: 3360, P_Q4_0: 2304, P_BF16: 8192}
+PACK_OF = {Q.F32: P_F16, Q.F16: P_F16, Q.BF16: P_BF16, Q.Q8_0: P_Q8_0, Q.Q4_0: P_Q4_0,
            Q.Q4_K: P_Q4_K, Q.Q5_K: P_Q5_K, Q.Q6_K: P_Q6_K}
 
 
 def _f16(b2):
     return np.frombuffer(np.ascontiguousarray(b2).tobytes(), np.float16).astype(np.float32)
+
+
+def _bf16(b2):
+    u = np.frombuffer(np.ascontiguousarray(b2).tobytes(), np.uint16).astype(np.uint32) << 16
+    return u.view(np.float32)
 
 
 def unpack_t16(packed: np.ndarray, ptype: int, n: int, k: int) -> np.ndarray:
@@ -73,9 +78,9 @@ def unpack_t16(packed: np.ndarray, ptype: int, n: int, k: int) -> np.ndarray:
                             blk = 2 * g + h
                             d = _f16(np.stack([c[4096 + 16 * rr + 2 * bb: 4096 + 16 * rr + 2 * bb + 2] for rr, bb in zip(r, blk)]))
                             v = d * (u - 128)
-                        else:  # F16
+                        else:  # F16 / BF16 (same layout)
                             b2 = np.stack([c[h * 4096 + s * 1024 + l * 16 + 2 * j: h * 4096 + s * 1024 + l * 16 + 2 * j + 2]
                                            for l in lane])
-                            v = _f16(b2)
+                            v = _bf16(b2) if ptype == P_BF16 else _f16(b2)
                         out[row, kk] = v
     return out[:n, :k]

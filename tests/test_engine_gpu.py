@@ -468,7 +468,7 @@ def test_bench_contract_line(cuda, native):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--model", "tinyllama", "--ftype", "Q4_K_M",
-                        "--steps", "3", "--warmup", "1", "--mb-size", "4", "--prompt-len", "16"],
+                        "--steps", "3", "--warmup", "1", "--mb-size", "4", "--prompt-len", "16", "--no-secondary"],
                        capture_output=True, text=True, timeout=240, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -479,6 +479,35 @@ def test_bench_contract_line(cuda, native):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["value"] > 0
     assert d["config"]["parallelism"] == "pp1" and d["config"]["global_batch"] == 4
+
+
+def test_bench_two_ranks_torchrun(cuda, native):
+    """The N > 1 bench path end to end on one GPU: torchrun with 2 ranks (both on GPU 0, gloo
+    process group, TCP stage links -- RCCL refuses two ranks of one communicator on one GPU),
+    init_from_torchrun, the MAX-over-ranks bracket and the JSON line with the data plane the
+    engine reports (2 stages, 3 micro-batches, link kind, torch world size)."""
+    import json as _json
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(repo, "bench.py"),
+           "--gpus", "2", "--same-device", "--model", "tinyllama", "--ftype", "Q4_K_M", "--steps", "3",
+           "--warmup", "1", "--mb-size", "4", "--prompt-len", "16", "--set", f"base_port={port + 7}"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = _json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["config"]["parallelism"] == "pp2" and d["config"]["micro_batches"] == 3
+    assert d["config"]["global_batch"] == 12 and len(d["config"]["stages"]) == 2
+    assert d["link"]["kind"] == ["tcp"] and d["link"]["torch_pg_world"] == 2 and d["link"]["links_per_rank"] == 2
 
 
 @pytest.mark.parametrize("stages", [1, 2])

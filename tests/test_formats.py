@@ -103,7 +103,7 @@ def test_t16_pack_layout(native, qt):
     ref = Q.dequantize(raw, qt).reshape(n, k)
     packed = pack_t16(raw, qt, n, k)
     got = unpack_t16(packed, PACK_OF[qt], n, k)
-    tol = 1e-3 if qt in (Q.F32, Q.BF16) else 1e-6
+    tol = 1e-3 if qt == Q.F32 else 1e-6   # BF16 stays bf16 (P_BF16): exact
     np.testing.assert_allclose(got, ref, rtol=tol, atol=tol * np.abs(ref).max())
 
 
