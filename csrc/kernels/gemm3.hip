@@ -28,6 +28,7 @@
 #include "kcommon.h"
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
+#include "../runtime/tuning.h"
 
 #include <algorithm>
 
@@ -312,7 +313,9 @@ template <> struct G3<P_BF16> {
   }
 };
 
-template <int PT, int EPI, int BM, int BN>
+// PROBE (timing probes only, never in the engine): bit 0 skips the MFMAs (operand reads kept
+// live), bit 1 the dequant, bit 2 all global->LDS staging
+template <int PT, int EPI, int BM, int BN, int PROBE = 0>
 __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages) {
   using Q = G3<PT>;
@@ -347,6 +350,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
 
   // A (x) stage: piece pc (8 rows) of this wave; lane -> row 8 pc + (l >> 3), image chunk l & 7
   auto issue_a = [&](int s, int buf) {
+    if constexpr (PROBE & 4) return;
     const int k0 = s * 64;
 #pragma unroll
     for (int i = 0; i < A_PER_WAVE; ++i) {
@@ -366,6 +370,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   const int dq_col = 16 * ((dq_e >> 4) % NT) + g3_perm(dq_e & 15);
   u32x4 breg[G3<PT>::MODE == G3_REG ? DQ_NS : 1];   // G3_REG: raw of the next stage to convert
   auto issue_b = [&](int s, int buf) {
+    if constexpr (PROBE & 4) return;
     ctx.sb = s >> 2; ctx.q = s & 3;
     if constexpr (Q::MODE == G3_DIRECT) Q::issue_b(Bs + buf * B_BYTES, ctx, NT, wave, lane);
     else if constexpr (Q::MODE == G3_RAW_LDS) Q::issue(Rs + buf * R_BYTES, ctx, NT, wave, lane);
@@ -383,6 +388,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
     for (int j = 0; j < DQ_NS; ++j) *reinterpret_cast<half8_t*>(B + g3_off(dq_col, 4 * dq_h + DQ_NS * dq_part + j)) = b[j];
   };
   auto dequant = [&](int s, int buf) {   // raw R[buf] (registers for G3_REG) of stage s -> B[buf]
+    if constexpr (PROBE & 2) return;
     half8_t b[DQ_NS];
     if constexpr (Q::MODE == G3_RAW_LDS) {
       Q::template dequant<DQ_NS>(Rs + buf * R_BYTES, NT, dq_e, dq_part, s & 3, kc, b);
@@ -438,10 +444,17 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
       for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const half8_t*>(Ab + g3_off(rbase + 16 * i, 4 * kk + g));
 #pragma unroll
       for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const half8_t*>(Bb + g3_off(cbase + 16 * j, 4 * kk + g));
+      if constexpr (PROBE & 1) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(a[i]));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(b[j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      }
     }
     // dequant raw(s+1) -> B[cur^1] (landed at the end of iteration s-1).  Placed AFTER the MFMA
     // code: its ds_writes may not move above the operand ds_reads (the compiler cannot separate the
@@ -515,6 +528,16 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
+  if constexpr (PT == P_Q4_K && EPI == EPI_SWIGLU && BM == 256 && BN == 256) {
+    switch (knob(KNOB_GEMM3_PROBE)) {   // timing probes (tools/gemv_bench.py --knob GEMM3_PROBE=k)
+      case 1: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 1>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      case 2: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 2>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      case 3: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 3>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      case 4: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 4>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      case 6: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 6>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      default: break;
+    }
+  }
   hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages);
 }
 

@@ -36,6 +36,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"MOE_V", 2, 1, 2, nullptr},
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
+    {"GEMM3_PROBE", 0, 0, 7, nullptr},
 };
 
 std::atomic<int> g_vals[KNOB_COUNT];

@@ -22,6 +22,7 @@ enum Knob : int {
   KNOB_MOE_V,               // MoE GEMV version (1 | 2)
   KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
+  KNOB_GEMM3_PROBE,         // gemm3 timing probes (Q4_K SwiGLU 256x256 only; 0 = the real kernel)
   KNOB_COUNT
 };
 

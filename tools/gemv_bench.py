@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--gemm", type=int, default=0,
                     help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256 per-wave dequant, 3: LDS-shared dequant)")
     ap.add_argument("--g3", default="0,0,0", help="v3 GEMM tuning BM,BN,nsplit (0 = auto); ';'-separated list sweeps")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=V[,V..]",
+                    help="tuning knob (csrc/runtime/tuning.h) swept per shape, e.g. GEMM3_PROBE=0,1,2")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -60,7 +62,13 @@ def main():
                 X = torch.randn(M, k_pad, device="cuda").half()
                 Y = torch.zeros(M, n, device="cuda")
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
-                for tpw, g3 in [(int(t), g) for t in a.tpw.split(",") for g in a.g3.split(";")]:
+                knobs = [[]]
+                for kv in a.knob:
+                    name, vals = kv.split("=", 1)
+                    knobs = [k + [(name, int(v))] for k in knobs for v in vals.split(",")]
+                for tpw, g3, kn in [(int(t), g, k) for t in a.tpw.split(",") for g in a.g3.split(";") for k in knobs]:
+                    for name, v in kn:
+                        N.check(L.mp_set_knob(name.encode(), v), "set_knob")
                     L.mp_set_gemv_tpw(tpw)
                     bm, bn, g3s = [int(v) for v in g3.split(",")]
                     L.mp_set_gemm3_tuning(bm, bn, g3s, 0)
@@ -103,7 +111,7 @@ def main():
                         print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
                                               GBps=round(nbytes / us / 1e3, 1),
                                               TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
-                                              g3=g3 if a.gemm == 3 else None)), flush=True)
+                                              g3=g3 if a.gemm == 3 else None, knobs=dict(kn) or None)), flush=True)
             del Ws
             torch.cuda.empty_cache()
 
