@@ -1,36 +1,40 @@
-// Dequant GEMM v3 (M >= 128: wide decode micro-batches and prompt chunks).
+// Dequant GEMM v3 (M > 64: wide decode micro-batches and prompt chunks).
 //
 // Y[M][N] (+)= X[M][K] W[N][K]^T with W in the T16 packed quant layout (csrc/runtime/qtypes.h).
-// Workgroup tile BM x BN (BM 128 | 256 rows, BN 128 | 256 columns = 8 | 16 T16 tiles), 8 waves,
-// K in stages of 64.  Unlike gemm2 (each wave dequantizes its own two 16-column tiles in registers,
-// 3.5 VALU per MFMA at 2 waves/SIMD, 39 % MFMA busy: profiles/r5f_gemm2_m256_pmc.txt), every weight
-// element is dequantized ONCE per workgroup, into an f16 LDS image that all waves read:
 //
-//   stage s (64 k):  X rows  --global_load_lds-->  A[s&1]  (f16, [BM][64], swizzled)
-//                    W quant --global_load_lds-->  R[s&1]  (raw bytes of the stage, per-type image)
-//                    R  --ds_read, VALU dequant, ds_write-->  B[s&1]  (f16, [BN][64], swizzled)
+// Workgroup tile BM x BN (BM = 128 | 256 rows, BN = 128 | 256 columns), 8 waves, K in stages of
+// 64.  Every wave OWNS TW = BN / 128 weight tiles (16 columns each) for all BM rows: it dequantizes
+// each weight element of its tiles exactly once per workgroup, straight into MFMA B fragments in
+// registers (no f16 weight image in LDS, no ds_write, no duplicated dequant), and runs
+// v_mfma_f32_16x16x32_f16 against the A (x) fragments that all 8 waves share from LDS.
 //
-// Iteration s: issue the loads of A(s+1) and R(s+2), run the 2 FM FN MFMAs per wave of stage s
-// from A(s&1)/B(s&1) (v_mfma_f32_16x16x32_f16, wave tile 16FM x 16FN, accumulators in registers),
-// and dequantize R(s+1) into B((s+1)&1) (VALU).  The dequant of a stage and the MFMAs of the
-// previous one are independent, so the two pipes overlap inside every wave; one barrier per stage.
+//   stage s:  X rows [BM][64]      --global_load_lds-->  A[s % NB]  (f16, swizzled, shared)
+//             each wave's raw quant --global_load_lds-->  R[s % NB][wave]  (its TW tiles' bytes)
 //
-// LDS images: rows (A) / columns (B) of 128 B = 8 chunks of 16 B (8 consecutive k); chunk c of row
-// r sits at chunk c ^ ((r >> 1) & 7), which makes every ds_read_b128 of an MFMA operand (16 rows x
-// 8 chunk groups) bank-conflict free.  global_load_lds writes lane-linear, so the swizzle is applied
-// to the per-lane SOURCE address (cdna_hip_programming.md rule 21).  Dequant threads own column
-// perm(r) = ((r & 7) << 1) | (r >> 3) of their tile so that each 8-lane ds_write_b128 group hits 8
-// distinct chunks.
+// Everything reaches LDS by LDS-DMA (global_load_lds), so the load pipeline is NB = 3 stages deep
+// with a COUNTED s_waitcnt vmcnt(loads of one stage) before each raw s_barrier: stage s+2 stays in
+// flight while stage s computes (the round-1/2 GEMMs and the first v3 drained every load at every
+// barrier: profiles/r6c_gemm3_probes.txt -- at one stage in flight the x/weight staging alone took
+// 134 us of a 240-280 us 70B gate/up).  Per lane, a B fragment needs one dword of 4-bit quants (8
+// weights) plus its row's scales: the raw image is laid out so that read is conflict-free.
 //
-// Workgroups are mapped XCD-aware (blocks b, b + 8, ... share an XCD; consecutive logical ids =
-// the row blocks of one column group, whose weight reads after the first then hit that XCD's L2).
-// EPI_ATOMIC splits the stage range over blockIdx.y.
+// Measured history: v3 with an LDS-shared f16 image (dequant by all threads, ds_write, B read back):
+// 882 TF on 70B gate/up M=256 (profiles/r6a_gemm3_first_light.txt), dequant not overlapped with the
+// MFMAs and staging latency-bound (r6b / r6c).
+//
+// A image: rows of 128 B = 8 chunks of 16 B (8 consecutive k); chunk c of row r at c ^ ((r >> 1) &
+// 7): every ds_read_b128 of an A fragment is bank-conflict free; global_load_lds writes
+// lane-linear, so the swizzle is applied to the per-lane SOURCE address (cdna_hip_programming.md
+// rule 21).  Workgroups are mapped XCD-aware (blocks b = x mod 8 share an XCD and get consecutive
+// logical ids: the row blocks of one column group).  EPI_ATOMIC splits the stage range over
+// blockIdx.y.
 #include "kcommon.h"
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 #include "../runtime/tuning.h"
 
 #include <algorithm>
+#include <utility>
 
 namespace mpk {
 using namespace mp;
@@ -39,15 +43,34 @@ typedef __attribute__((address_space(3))) void lds_t;
 
 __device__ __forceinline__ int g3_swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int g3_off(int row, int c) { return row * 128 + ((c ^ g3_swz(row)) << 4); }
-__device__ __forceinline__ int g3_perm(int r) { return ((r & 7) << 1) | (r >> 3); }
 
 // global -> LDS DMA of SZ (16 | 4) bytes per lane (LDS destination: wave-uniform base + lane * SZ;
-// the sub-dword forms are not used: they land a dword per lane); the size must be a literal
+// the sub-dword forms are not used: they land a dword per lane).  Issued as inline asm on purpose:
+// the compiler's own form (__builtin_amdgcn_global_load_lds) makes hipcc wait vmcnt(0) before the
+// first ds_read after it (it cannot tell which LDS bytes a DMA writes), which drains the whole
+// prefetch pipeline every stage.  These loads are invisible to the compiler's waitcnt pass: every
+// wait on them is the kernel's own counted s_waitcnt vmcnt (wait_vmcnt) before a barrier.
 template <int SZ>
 __device__ __forceinline__ void glds(const void* g, char* lds) {
   static_assert(SZ == 16 || SZ == 4, "glds: 16 or 4 bytes per lane");
-  if constexpr (SZ == 16) __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 16, 0, 0);
-  else __builtin_amdgcn_global_load_lds(g, (lds_t*)lds, 4, 0, 0);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_t*)lds);
+  if constexpr (SZ == 16)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+// one LDS-DMA wave instruction whose lanes >= n are masked off (every wave issues it: uniform
+// vmcnt accounting)
+template <int SZ, class F>
+__device__ __forceinline__ void glds_n(char* lds, int n, int lane, F src) {
+  if (lane < n) glds<SZ>(src(lane), lds);
+}
+
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima), gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 // Q4_K / Q5_K scale words of quarter g (= stage q of the super-block): (d sc(2g), d sc(2g+1)),
@@ -63,278 +86,360 @@ __device__ __forceinline__ void kq_scales(const u32x4& hdr, uint32_t g, half2_t&
   M = __builtin_elementwise_fma(as_h2(b), n2, n2 * h2c(-1024.f));
 }
 
-// word j of the dwords [part * NS, part * NS + NS) of v (part wave-uniform)
-template <int NS>
-__device__ __forceinline__ uint32_t g3_word(const u32x4& v, int part, int j) {
-  if constexpr (NS == 4) return v[j];
-  else return part ? v[2 + j] : v[j];
+// 8 nibbles of a dword (T16 order: j = 2i at bit 4i, 2i+1 at bit 16 + 4i) -> 8 f16 = S q + M
+__device__ __forceinline__ half8_t nib8(uint32_t w, half2_t S, half2_t M, const Consts& k) {
+  const uint32_t t = w >> 8;
+  return pack8(as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mlo, k.mag_hi)) - h2c(1024.f), S, M)),
+               as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mhi, k.mag_lo)) - h2c(64.f), S, M)),
+               as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mlo, k.mag_hi)) - h2c(1024.f), S, M)),
+               as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mhi, k.mag_lo)) - h2c(64.f), S, M)));
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-type raw stage image + dequant.  A stage of NT T16 tiles covers, per tile, quarter q of one
-// super-block.  Dequant entry e (< 32 NT): h = e / (16 NT) (k half of the quarter: wave-uniform),
-// tile T = (e >> 4) % NT, column perm(e & 15); dequant<NS> produces its 8-k chunks part * NS + j,
-// j < NS (NS = 4: one thread per entry; NS = 2: two, part wave-uniform).  Segments are filled by 1-KB wave pieces
-// (64 lanes x 16 B, or 64 x 4 B for the small fields), entry i of a segment at i * ES.
-template <int PT> struct G3;
-// how a stage's weights reach the f16 B image:
-//   G3_RAW_LDS: raw quant bytes by global_load_lds into R, dequantized LDS -> VALU -> LDS
-//   G3_DIRECT:  the packed f16 bytes by global_load_lds straight into B (16-bit f16 weights)
-//   G3_REG:     16-B loads into registers one stage ahead, converted and written (bf16 weights:
-//               their raw bytes are as large as the f16 image, too big for an LDS raw buffer)
-enum { G3_RAW_LDS = 0, G3_DIRECT = 1, G3_REG = 2 };
-
-struct G3Ctx {           // per-stage source addressing (wave-uniform)
-  const uint8_t* W;      // packed matrix
-  int t0, ntiles, nsb, sb, q;
-  __device__ __forceinline__ const uint8_t* chunk(int T, int CB) const {
-    const int t = min(t0 + T, ntiles - 1);
+// Per-type raw image of ONE wave for one stage: its TW tiles (u < TW) x quarter q of super-block sb.
+// The MFMA B fragment of k-half kk (32 k) for lane l = 16 g + r is column r of the tile, k = 32 kk
+// + 8 g + j: in the T16 chunk that is dword g of row r's 16-B piece of half h = kk (dequant.h).
+//   issue():  NI(TW) LDS-DMA wave instructions (uniform per wave)
+//   prep():   per-stage, per-tile values (scales) of this lane's row
+//   frag():   the B fragment (u, kk)
+struct W3Src {
+  const uint8_t* W;
+  int t0, ntiles, nsb, sb, q;   // t0: the wave's first tile
+  __device__ __forceinline__ const uint8_t* chunk(int u, int CB) const {
+    const int t = min(t0 + u, ntiles - 1);
     return W + ((size_t)t * nsb + sb) * CB;
   }
 };
 
-// issue the global_load_lds pieces of one segment: n entries of ES bytes, pieces of 64 entries
-// dealt round-robin over the 8 waves; src(i) = source of entry i
-template <int ES, class F>
-__device__ __forceinline__ void g3_segment(char* dst, int n, int wave, int lane, F src) {
-  const int pieces = n / 64;
-  for (int pc = wave; pc < pieces; pc += 8) glds<ES>(src(pc * 64 + lane), dst + pc * 64 * ES);
+template <int PT> struct W3;
+
+// LDS reads issued as inline asm (the kernel counts lgkmcnt itself, so A fragments can be kept
+// in flight AD deep: left to the compiler, each ds_read was followed by lgkmcnt(0) before its two
+// MFMAs -- one LDS round trip per 32 MFMA cycles)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_t*)p; }
+__device__ __forceinline__ void ds_b32(uint32_t& v, const void* p) {
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+__device__ __forceinline__ void ds_u16(uint32_t& v, const void* p) {
+  asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+__device__ __forceinline__ void ds_b64(u32x2& v, const void* p) {
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+__device__ __forceinline__ void ds_b128(u32x4& v, const void* p) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+template <int OFF>   // immediate byte offset on an LDS address
+__device__ __forceinline__ void ds_b128o(u32x4& v, uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+}
+// compile-time loop: f(std::integral_constant<int, J>) for J < N
+template <class F, int... J>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, J...>) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }
+
+// s_waitcnt lgkmcnt(N) (vmcnt / expcnt at their maxima) + a scheduling fence: the compiler does not
+// know the asm reads' results arrive late, so nothing may move above the wait
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt");
+  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-template <> struct G3<P_Q4_K> {
+// Q4_K: quants [u][h][r] 16 B, header [u][r] 16 B
+template <> struct W3<P_Q4_K> {
   static constexpr int CB = chunk_bytes(P_Q4_K);
-  static constexpr int MODE = G3_RAW_LDS;
-  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 256; }
-  __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
-    g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
-      const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
-      return c.chunk(T, CB) + h * 1024 + (16 * c.q + r) * 16;
+  static constexpr int RAW(int TW) { return TW * 768; }
+  static constexpr int NI(int) { return 2; }
+  static constexpr int NR(int TW) { return 3 * TW; }
+  template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2]; };
+  struct Prep { half2_t S2, M2; };
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+      return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    g3_segment<16>(R + NT * 512, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 2048 + (i & 15) * 16; });
+    glds_n<16>(R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16; });
   }
-  template <int NS>
-  __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts& k, half8_t* b) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const u32x4 w4 = *reinterpret_cast<const u32x4*>(R + e * 16);
-    const u32x4 hdr = *reinterpret_cast<const u32x4*>(R + NT * 512 + (T * 16 + r) * 16);
-    half2_t S2, M2;
-    kq_scales(hdr, (uint32_t)q, S2, M2);
-    const half2_t S = h ? h2hi(S2) : h2lo(S2), M = h ? h2hi(M2) : h2lo(M2);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+    const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t w = g3_word<NS>(w4, part, s), t = w >> 8;
-      b[s] = pack8(as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mlo, k.mag_hi)) - h2c(1024.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mhi, k.mag_lo)) - h2c(64.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mlo, k.mag_hi)) - h2c(1024.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mhi, k.mag_lo)) - h2c(64.f), S, M)));
+    for (int u = 0; u < TW; ++u) {
+      ds_b128(w.hdr[u], R + TW * 512 + (u * 16 + r) * 16);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ds_b32(w.q[u][kk], R + ((u * 2 + kk) * 16 + r) * 16 + 4 * g);
     }
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>& w, int u, int q, int) {
+    Prep p;
+    kq_scales(w.hdr[u], (uint32_t)q, p.S2, p.M2);
+    return p;
+  }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep& p, int u, int kk, int, const Consts& k) {
+    return nib8(w.q[u][kk], kk ? h2hi(p.S2) : h2lo(p.S2), kk ? h2hi(p.M2) : h2lo(p.M2), k);
   }
 };
 
-template <> struct G3<P_Q5_K> {
+// Q5_K: quants [u][h][r] 16 B, high bits [u][h][r] 4 B, header [u][r] 16 B
+template <> struct W3<P_Q5_K> {
   static constexpr int CB = chunk_bytes(P_Q5_K);
-  static constexpr int MODE = G3_RAW_LDS;
-  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 128 + NT * 256; }
-  __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
-    g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
-      const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
-      return c.chunk(T, CB) + h * 1024 + (16 * c.q + r) * 16;
+  static constexpr int RAW(int TW) { return TW * 896; }
+  static constexpr int NI(int) { return 3; }
+  static constexpr int NR(int TW) { return 5 * TW; }
+  template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2], qh[TW][2]; };
+  struct Prep { half2_t S2, M2; };
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+      return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    g3_segment<4>(R + NT * 512, 32 * NT, wave, lane, [&](int i) {
-      const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
-      return c.chunk(T, CB) + 2048 + h * 256 + (16 * c.q + r) * 4;
+    // 16-B entries = 4 rows' high-bit words: entry f -> (u, h, rows 4 (f & 3) ..)
+    glds_n<16>(R + TW * 512, 8 * TW, lane, [&](int f) {
+      return c.chunk(f >> 3, CB) + 2048 + ((f >> 2) & 1) * 256 + (16 * c.q + 4 * (f & 3)) * 4;
     });
-    g3_segment<16>(R + NT * 640, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 2560 + (i & 15) * 16; });
+    glds_n<16>(R + TW * 640, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2560 + (e & 15) * 16; });
   }
-  template <int NS>
-  __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts& k, half8_t* b) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const u32x4 w4 = *reinterpret_cast<const u32x4*>(R + e * 16);
-    const uint32_t qh = *reinterpret_cast<const uint32_t*>(R + NT * 512 + e * 4) >> (8 * NS * part);
-    const u32x4 hdr = *reinterpret_cast<const u32x4*>(R + NT * 640 + (T * 16 + r) * 16);
-    half2_t S2, M2;
-    kq_scales(hdr, (uint32_t)q, S2, M2);
-    const half2_t S = h ? h2hi(S2) : h2lo(S2), M = h ? h2hi(M2) : h2lo(M2);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+    const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t w = g3_word<NS>(w4, part, s), t = w >> 8;
-      const uint32_t hb = (qh >> (8 * s)) & 0xFFu;
-      const uint32_t x = hb | (hb << 12);
-      const uint32_t h0 = ((x << 4) & 0x00100010u) | k.mag_hi, h1 = ((x << 7) & 0x01000100u) | k.mag_lo;
-      const uint32_t h2 = ((x << 2) & 0x00100010u) | k.mag_hi, h3 = ((x << 5) & 0x01000100u) | k.mag_lo;
-      b[s] = pack8(as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mlo, h0)) - h2c(1024.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(w, k.mhi, h1)) - h2c(64.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mlo, h2)) - h2c(1024.f), S, M)),
-                   as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mhi, h3)) - h2c(64.f), S, M)));
+    for (int u = 0; u < TW; ++u) {
+      ds_b128(w.hdr[u], R + TW * 640 + (u * 16 + r) * 16);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ds_b32(w.q[u][kk], R + ((u * 2 + kk) * 16 + r) * 16 + 4 * g);
+        ds_b32(w.qh[u][kk], R + TW * 512 + ((u * 2 + kk) * 16 + r) * 4);
+      }
     }
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>& w, int u, int q, int) {
+    Prep p;
+    kq_scales(w.hdr[u], (uint32_t)q, p.S2, p.M2);
+    return p;
+  }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep& p, int u, int kk, int lane, const Consts& k) {
+    const int g = lane >> 4;
+    const uint32_t hb = (w.qh[u][kk] >> (8 * g)) & 0xFFu;
+    const uint32_t x = hb | (hb << 12);
+    const half2_t S = kk ? h2hi(p.S2) : h2lo(p.S2), M = kk ? h2hi(p.M2) : h2lo(p.M2);
+    const uint32_t v = w.q[u][kk], t = v >> 8;
+    const uint32_t h0 = ((x << 4) & 0x00100010u) | k.mag_hi, h1 = ((x << 7) & 0x01000100u) | k.mag_lo;
+    const uint32_t h2 = ((x << 2) & 0x00100010u) | k.mag_hi, h3 = ((x << 5) & 0x01000100u) | k.mag_lo;
+    return pack8(as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mlo, h0)) - h2c(1024.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mhi, h1)) - h2c(64.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mlo, h2)) - h2c(1024.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(t, k.mhi, h3)) - h2c(64.f), S, M)));
   }
 };
 
-template <> struct G3<P_Q6_K> {
+// Q6_K: quants [u][h][r] 16 B, high bits [u][h][r] 8 B, int8 scales [u][r] 4 B (dword q of the
+// row's 16), d [u][r] 2 B (per tile the 32 contiguous bytes, two 16-B entries)
+template <> struct W3<P_Q6_K> {
   static constexpr int CB = chunk_bytes(P_Q6_K);
-  static constexpr int MODE = G3_RAW_LDS;
-  // quants 16 B, high bits 8 B (two 4-B entries), int8 scales 4 B per row, and per row the dword
-  // holding its f16 d (rows 2i, 2i+1 share one; the sub-dword LDS-DMA forms write a dword per lane)
-  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 256 + NT * 64 + NT * 64; }
-  __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
-    g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
-      const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
-      return c.chunk(T, CB) + h * 1024 + (16 * c.q + r) * 16;
+  static constexpr int RAW(int TW) { return TW * 896; }
+  static constexpr int NI(int) { return 4; }
+  static constexpr int NR(int TW) { return 6 * TW; }
+  template <int TW> struct Raw { uint32_t sc[TW], d[TW], q[TW][2], qd[TW][2]; };
+  struct Prep { uint32_t sc; f16 d; };
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+      return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    g3_segment<4>(R + NT * 512, 64 * NT, wave, lane, [&](int i) {
-      const int e = i >> 1, h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-      return c.chunk(T, CB) + 2048 + h * 512 + (16 * c.q + r) * 8 + 4 * (i & 1);
+    glds_n<16>(R + TW * 512, 16 * TW, lane, [&](int f) {   // (u, h): 16 rows x 8 B contiguous
+      return c.chunk(f >> 4, CB) + 2048 + ((f >> 3) & 1) * 512 + 16 * c.q * 8 + (f & 7) * 16;
     });
-    g3_segment<4>(R + NT * 768, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 3072 + (i & 15) * 16 + 4 * c.q; });
-    g3_segment<4>(R + NT * 832, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 3328 + ((i & 15) >> 1) * 4; });
+    glds_n<4>(R + TW * 768, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 3072 + (e & 15) * 16 + 4 * c.q; });
+    glds_n<16>(R + TW * 832, 2 * TW, lane, [&](int f) { return c.chunk(f >> 1, CB) + 3328 + (f & 1) * 16; });
   }
-  template <int NS>
-  __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts& k, half8_t* b) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const u32x4 w4 = *reinterpret_cast<const u32x4*>(R + e * 16);
-    const u32x2 qh = *reinterpret_cast<const u32x2*>(R + NT * 512 + e * 8);
-    const uint32_t sc = *reinterpret_cast<const uint32_t*>(R + NT * 768 + (T * 16 + r) * 4);
-    const uint32_t dw = *reinterpret_cast<const uint32_t*>(R + NT * 832 + (T * 16 + r) * 4);
-    const uint16_t dd = (uint16_t)((r & 1) ? dw >> 16 : dw);
-    const f16 dh = __builtin_bit_cast(f16, dd);
-    const uint32_t u = sc ^ 0x80808080u;
-    const half2_t S2 = (as_h2(__builtin_amdgcn_perm(0x64646464u, u, h ? 0x04030402u : 0x04010400u)) - h2c(1152.f)) *
-                       half2_t{dh, dh};
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+    const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int hi = NS == 4 ? (j >> 1) : part;   // sub-block (16 k) of chunk part * NS + j
-      const half2_t S = hi ? h2hi(S2) : h2lo(S2);
-      const uint32_t w = g3_word<NS>(w4, part, j), t = w >> 8;
-      const uint32_t h16 = ((hi ? qh[1] : qh[0]) >> (16 * (j & 1))) & 0xFFFFu;
-      const uint32_t x = h16 | (h16 << 8);
-      const uint32_t h0 = ((x << 4) & 0x00300030u) | k.mag_hi, h1 = ((x << 6) & 0x03000300u) | k.mag_lo;
-      const uint32_t h2 = (x & 0x00300030u) | k.mag_hi, h3 = ((x << 2) & 0x03000300u) | k.mag_lo;
-      b[j] = pack8(as_u32((as_h2(and_or(w, k.mlo, h0)) - h2c(1056.f)) * S),
-                   as_u32((as_h2(and_or(w, k.mhi, h1)) - h2c(96.f)) * S),
-                   as_u32((as_h2(and_or(t, k.mlo, h2)) - h2c(1056.f)) * S),
-                   as_u32((as_h2(and_or(t, k.mhi, h3)) - h2c(96.f)) * S));
+    for (int u = 0; u < TW; ++u) {
+      ds_b32(w.sc[u], R + TW * 768 + (u * 16 + r) * 4);
+      ds_u16(w.d[u], R + TW * 832 + (u * 16 + r) * 2);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ds_b32(w.q[u][kk], R + ((u * 2 + kk) * 16 + r) * 16 + 4 * g);
+        ds_b32(w.qd[u][kk], R + TW * 512 + ((u * 2 + kk) * 16 + r) * 8 + 4 * (g >> 1));
+      }
     }
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>& w, int u, int, int) {
+    return Prep{w.sc[u] ^ 0x80808080u, __builtin_bit_cast(f16, (uint16_t)w.d[u])};
+  }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep& p, int u, int kk, int lane, const Consts& k) {
+    const int g = lane >> 4;
+    const uint32_t h16 = (w.qd[u][kk] >> (16 * (g & 1))) & 0xFFFFu;
+    // int8 scale of sub-block 4q + 2kk + (g >> 1): byte 2kk + (g >> 1) of the dword, (sc + 128) by
+    // the exponent magic, minus 1152, times d
+    const uint32_t sb = (p.sc >> (8 * (2 * kk + (g >> 1)))) & 0xFFu;
+    const f16 sf = (as_h2(0x6400u | sb).x - (f16)1152.f) * p.d;
+    const half2_t S = half2_t{sf, sf};
+    const uint32_t x = h16 | (h16 << 8);
+    const uint32_t v = w.q[u][kk], t = v >> 8;
+    const uint32_t h0 = ((x << 4) & 0x00300030u) | k.mag_hi, h1 = ((x << 6) & 0x03000300u) | k.mag_lo;
+    const uint32_t h2 = (x & 0x00300030u) | k.mag_hi, h3 = ((x << 2) & 0x03000300u) | k.mag_lo;
+    return pack8(as_u32((as_h2(and_or(v, k.mlo, h0)) - h2c(1056.f)) * S),
+                 as_u32((as_h2(and_or(v, k.mhi, h1)) - h2c(96.f)) * S),
+                 as_u32((as_h2(and_or(t, k.mlo, h2)) - h2c(1056.f)) * S),
+                 as_u32((as_h2(and_or(t, k.mhi, h3)) - h2c(96.f)) * S));
   }
 };
 
-template <> struct G3<P_Q8_0> {
+// Q8_0: quants [u][h][r] 32 B (int8 + 128), block scales [u][r] 4 B = (d(2q), d(2q+1))
+template <> struct W3<P_Q8_0> {
   static constexpr int CB = chunk_bytes(P_Q8_0);
-  static constexpr int MODE = G3_RAW_LDS;
-  static constexpr int raw_bytes(int NT) { return NT * 1024 + NT * 64; }
-  __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
-    g3_segment<16>(R, 64 * NT, wave, lane, [&](int i) {
-      const int e = i >> 1, h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-      return c.chunk(T, CB) + h * 2048 + (16 * c.q + r) * 32 + 16 * (i & 1);
-    });
-    g3_segment<4>(R + NT * 1024, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 4096 + (i & 15) * 16 + 4 * c.q; });
+  static constexpr int RAW(int TW) { return TW * 1088; }
+  static constexpr int NI(int TW) { return TW + 1; }
+  static constexpr int NR(int TW) { return 3 * TW; }
+  template <int TW> struct Raw { uint32_t dd[TW]; u32x2 v[TW][2]; };
+  struct Prep { uint32_t dd; };
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+#pragma unroll
+    for (int u = 0; u < TW; ++u)   // 64 entries of 16 B per tile: (h, r, half)
+      glds<16>(c.chunk(u, CB) + (lane >> 5) * 2048 + (16 * c.q + ((lane >> 1) & 15)) * 32 + 16 * (lane & 1), R + u * 1024);
+    glds_n<4>(R + TW * 1024, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 4096 + (e & 15) * 16 + 4 * c.q; });
   }
-  template <int NS>
-  __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts&, half8_t* b) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const u32x4 a0 = *reinterpret_cast<const u32x4*>(R + e * 32 + (NS == 4 ? 0 : 16 * part));
-    const u32x4 a1 = NS == 4 ? *reinterpret_cast<const u32x4*>(R + e * 32 + 16) : a0;
-    const uint32_t dd = *reinterpret_cast<const uint32_t*>(R + NT * 1024 + (T * 16 + r) * 4);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      ds_b32(w.dd[u], R + TW * 1024 + (u * 16 + r) * 4);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ds_b64(w.v[u][kk], R + ((u * 2 + kk) * 16 + r) * 32 + 8 * g);
+    }
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>& w, int u, int, int) { return Prep{w.dd[u]}; }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep& p, int u, int kk, int, const Consts&) {
+    const u32x2 v = w.v[u][kk];
     const half2_t off = h2c(1152.f);
-    const half2_t S = h ? h2hi(as_h2(dd)) : h2lo(as_h2(dd));
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const u32x4 src = s < 2 ? a0 : a1;
-      const uint32_t lo = src[2 * (s & 1)], hi = src[2 * (s & 1) + 1];
-      b[s] = pack8(as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u)) - off) * S),
-                   as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u)) - off) * S),
-                   as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u)) - off) * S),
-                   as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u)) - off) * S));
-    }
+    const half2_t S = kk ? h2hi(as_h2(p.dd)) : h2lo(as_h2(p.dd));
+    return pack8(as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, v.x, 0x04010400u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, v.x, 0x04030402u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, v.y, 0x04010400u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, v.y, 0x04030402u)) - off) * S));
   }
 };
 
-template <> struct G3<P_Q4_0> {
+// Q4_0: quants [u][h][r] 16 B, block scales [u][r] 4 B = (d(2q), d(2q+1))
+template <> struct W3<P_Q4_0> {
   static constexpr int CB = chunk_bytes(P_Q4_0);
-  static constexpr int MODE = G3_RAW_LDS;
-  static constexpr int raw_bytes(int NT) { return NT * 512 + NT * 64; }
-  __device__ static __forceinline__ void issue(char* R, const G3Ctx& c, int NT, int wave, int lane) {
-    g3_segment<16>(R, 32 * NT, wave, lane, [&](int i) {
-      const int h = i / (16 * NT), T = (i >> 4) % NT, r = g3_perm(i & 15);
-      return c.chunk(T, CB) + h * 1024 + (16 * c.q + r) * 16;
+  static constexpr int RAW(int TW) { return TW * 576; }
+  static constexpr int NI(int) { return 2; }
+  static constexpr int NR(int TW) { return 3 * TW; }
+  template <int TW> struct Raw { uint32_t dd[TW], q[TW][2]; };
+  struct Prep { uint32_t dd; };
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+      return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    g3_segment<4>(R + NT * 512, 16 * NT, wave, lane, [&](int i) { return c.chunk(i >> 4, CB) + 2048 + (i & 15) * 16 + 4 * c.q; });
+    glds_n<4>(R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16 + 4 * c.q; });
   }
-  template <int NS>
-  __device__ static __forceinline__ void dequant(const char* R, int NT, int e, int part, int q, const Consts& k, half8_t* b) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const u32x4 w4 = *reinterpret_cast<const u32x4*>(R + e * 16);
-    const uint32_t dd = *reinterpret_cast<const uint32_t*>(R + NT * 512 + (T * 16 + r) * 4);
-    const half2_t S = h ? h2hi(as_h2(dd)) : h2lo(as_h2(dd));
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+    const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t w = g3_word<NS>(w4, part, s), t = w >> 8;
-      b[s] = pack8(as_u32((as_h2(and_or(w, k.mlo, k.mag_hi)) - h2c(1032.f)) * S),
-                   as_u32((as_h2(and_or(w, k.mhi, k.mag_lo)) - h2c(72.f)) * S),
-                   as_u32((as_h2(and_or(t, k.mlo, k.mag_hi)) - h2c(1032.f)) * S),
-                   as_u32((as_h2(and_or(t, k.mhi, k.mag_lo)) - h2c(72.f)) * S));
+    for (int u = 0; u < TW; ++u) {
+      ds_b32(w.dd[u], R + TW * 512 + (u * 16 + r) * 4);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ds_b32(w.q[u][kk], R + ((u * 2 + kk) * 16 + r) * 16 + 4 * g);
     }
   }
-};
-
-// 16-bit weights: the stage's B image is loaded directly (no raw image, no dequant)
-template <> struct G3<P_F16> {
-  static constexpr int CB = chunk_bytes(P_F16);
-  static constexpr int MODE = G3_DIRECT;
-  static constexpr int raw_bytes(int) { return 0; }
-  // B image bytes [col][128 B]: piece of 1 KB = 8 columns; lane l -> column 8 pc + (l >> 3), image
-  // chunk l & 7 = source chunk c ^ swz(col); source chunk c (k = 8c..8c+7 of the quarter) is packed
-  // element i = c (4H + s) of lane (q, r) of the T16 chunk: byte c * 1024 + (16 q + r) * 16
-  __device__ static __forceinline__ void issue_b(char* B, const G3Ctx& c, int NT, int wave, int lane) {
-    for (int pc = wave; pc < 2 * NT; pc += 8) {
-      const int col = 8 * pc + (lane >> 3);
-      const int ch = (lane & 7) ^ g3_swz(col);
-      glds<16>(c.chunk(col >> 4, CB) + ch * 1024 + (16 * c.q + (col & 15)) * 16, B + pc * 1024);
-    }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>& w, int u, int, int) { return Prep{w.dd[u]}; }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep& p, int u, int kk, int, const Consts& k) {
+    const half2_t S = kk ? h2hi(as_h2(p.dd)) : h2lo(as_h2(p.dd));
+    const uint32_t v = w.q[u][kk], t = v >> 8;
+    return pack8(as_u32((as_h2(and_or(v, k.mlo, k.mag_hi)) - h2c(1032.f)) * S),
+                 as_u32((as_h2(and_or(v, k.mhi, k.mag_lo)) - h2c(72.f)) * S),
+                 as_u32((as_h2(and_or(t, k.mlo, k.mag_hi)) - h2c(1032.f)) * S),
+                 as_u32((as_h2(and_or(t, k.mhi, k.mag_lo)) - h2c(72.f)) * S));
   }
 };
 
-// bf16 weights (F16 chunk layout, bf16 bits): entry e's chunks 4h + part NS + j of the quarter
-// (k = 8 c .. 8 c + 7 of column perm(r)) are element i = c of lane (q, r): byte c * 1024 + (16 q + r) * 16
-template <> struct G3<P_BF16> {
-  static constexpr int CB = chunk_bytes(P_BF16);
-  static constexpr int MODE = G3_REG;
-  static constexpr int raw_bytes(int) { return 0; }
-  template <int NS>
-  __device__ static __forceinline__ void load(const G3Ctx& c, int NT, int e, int part, u32x4* v) {
-    const int h = e / (16 * NT), T = (e >> 4) % NT, r = g3_perm(e & 15);
-    const uint8_t* src = c.chunk(T, CB) + (16 * c.q + r) * 16;
+// 16-bit weights (F16, or BF16 widened to f16 per fragment): the fragment bytes themselves,
+// [u][kk][lane] 16 B = element 4 kk + g of lane (q, r) of the T16 chunk
+template <int PT> struct W3_16 {
+  static constexpr int CB = chunk_bytes(PT);
+  static constexpr int RAW(int TW) { return TW * 2048; }
+  static constexpr int NI(int TW) { return 2 * TW; }
+  static constexpr int NR(int TW) { return 2 * TW; }
+  template <int TW> struct Raw { u32x4 v[TW][2]; };
+  struct Prep {};
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
 #pragma unroll
-    for (int j = 0; j < NS; ++j) v[j] = ld16_nt(src + (4 * h + NS * part + j) * 1024);
+    for (int f = 0; f < 2 * TW; ++f)
+      glds<16>(c.chunk(f >> 1, CB) + (4 * (f & 1) + (lane >> 4)) * 1024 + (16 * c.q + (lane & 15)) * 16, R + f * 1024);
   }
-  template <int NS>
-  __device__ static __forceinline__ void convert(const u32x4* v, half8_t* b) {
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
 #pragma unroll
-    for (int j = 0; j < NS; ++j) b[j] = bf8_to_h8(v[j]);
+    for (int u = 0; u < TW; ++u)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ds_b128(w.v[u][kk], R + (u * 2 + kk) * 1024 + lane * 16);
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>&, int, int, int) { return Prep{}; }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep&, int u, int kk, int, const Consts&) {
+    if constexpr (PT == P_BF16) return bf8_to_h8(w.v[u][kk]);
+    else return __builtin_bit_cast(half8_t, w.v[u][kk]);
   }
 };
+template <> struct W3<P_F16> : W3_16<P_F16> {};
+template <> struct W3<P_BF16> : W3_16<P_BF16> {};
 
-// PROBE (timing probes only, never in the engine): bit 0 skips the MFMAs (operand reads kept
-// live), bit 1 the dequant, bit 2 all global->LDS staging
-template <int PT, int EPI, int BM, int BN, int PROBE = 0>
+// PROBE & 2: some raw bits as a "fragment" (no dequant VALU)
+template <class RawT>
+__device__ __forceinline__ u32x4 raw_as_u32x4(const RawT& r, int u) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&r);
+  return u32x4{w[0], w[1], w[2], w[3 + u]};
+}
+
+template <int PT, int BM, int TW>
+struct G3Geom {
+  static constexpr int A_BYTES = BM * 128;                    // x rows of one stage
+  static constexpr int R_WAVE = W3<PT>::RAW(TW);             // one wave's raw bytes of one stage
+  static constexpr int STAGE = A_BYTES + 8 * R_WAVE;
+  static constexpr int NB = 3 * STAGE <= 160 * 1024 ? 3 : 2;  // pipeline depth (stages in LDS)
+  static constexpr int A_INSTR = BM / 64;                     // 1-KB A pieces per wave per stage
+  static constexpr int LOADS = A_INSTR + W3<PT>::NI(TW);      // LDS-DMA instructions per wave per stage
+};
+
+// PROBE (timing probes only, never in the engine): bit 0 skips the MFMAs (operands kept live),
+// bit 1 the dequant (B fragments read raw), bit 2 all global->LDS staging
+template <int PT, int EPI, int BM, int TW, int PROBE = 0>
 __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages) {
-  using Q = G3<PT>;
-  constexpr int NT = BN / 16;
-  constexpr int WN = BN == 256 ? 4 : (BM == 256 ? 2 : 4);
-  constexpr int WM = 8 / WN;
-  constexpr int FM = BM / (16 * WM), FN = BN / (16 * WN);
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, R_BYTES = Q::raw_bytes(NT);
-  constexpr int A_PER_WAVE = BM / 64;   // 1-KB pieces (8 rows) per wave per stage
-  static_assert(FM >= 1 && FN >= 1 && 16 * FM * WM == BM && 16 * FN * WN == BN, "tile");
-  __shared__ __attribute__((aligned(16))) char smem[2 * A_BYTES + 2 * B_BYTES + 2 * R_BYTES];
-  char* const As = smem;
-  char* const Bs = smem + 2 * A_BYTES;
-  char* const Rs = Bs + 2 * B_BYTES;
+  using Q = W3<PT>;
+  using G = G3Geom<PT, BM, TW>;
+  constexpr int NB = G::NB, FM = BM / 16, BN = 128 * TW;
+  __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware logical id (bijective for any grid size): blocks b = x (mod 8) share an XCD and get
-  // consecutive logical ids, i.e. the row blocks of one column group
+  // XCD-aware logical id (bijective for any grid size)
   const int nwg = gridDim.x, bx = blockIdx.x;
   const int xcd = bx & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
@@ -345,145 +450,121 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   if (s_begin >= s_end) return;   // uniform over the workgroup
   const int M = p.M;
 
-  G3Ctx ctx;
-  ctx.W = p.W; ctx.t0 = cg * NT; ctx.ntiles = p.ntiles; ctx.nsb = p.nsb;
+  W3Src src;
+  src.W = p.W; src.t0 = cg * (BN / 16) + wave * TW; src.ntiles = p.ntiles; src.nsb = p.nsb;
+  auto stage_a = [&](int b) { return smem + b * G::STAGE; };
+  auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
 
-  // A (x) stage: piece pc (8 rows) of this wave; lane -> row 8 pc + (l >> 3), image chunk l & 7
-  auto issue_a = [&](int s, int buf) {
+  // every wave issues exactly G::LOADS LDS-DMA instructions per stage (counted vmcnt below)
+  auto issue = [&](int s, int b) {
     if constexpr (PROBE & 4) return;
     const int k0 = s * 64;
 #pragma unroll
-    for (int i = 0; i < A_PER_WAVE; ++i) {
-      const int pc = wave * A_PER_WAVE + i;
+    for (int i = 0; i < G::A_INSTR; ++i) {   // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7
+      const int pc = wave * G::A_INSTR + i;
       const int row = 8 * pc + (lane >> 3);
       const int ch = (lane & 7) ^ g3_swz(row);
       const int gr = min(m0 + row, M - 1);
-      glds<16>(p.X + (size_t)gr * p.ldx + k0 + 8 * ch, As + buf * A_BYTES + pc * 1024);
+      glds<16>(p.X + (size_t)gr * p.ldx + k0 + 8 * ch, stage_a(b) + pc * 1024);
     }
-  };
-  // all 512 threads dequantize: NT = 16 one entry each; NT = 8 half an entry each, waves 2k and
-  // 2k + 1 sharing the entries of lanes 64 k .. (part = wave parity; h stays wave-uniform)
-  constexpr int DQ_NS = 32 * NT == 512 ? 4 : 2;
-  const int dq_part = DQ_NS == 4 ? 0 : (wave & 1);
-  const int dq_e = DQ_NS == 4 ? tid : (lane | ((wave >> 1) << 6));
-  const int dq_h = dq_e / (16 * NT);
-  const int dq_col = 16 * ((dq_e >> 4) % NT) + g3_perm(dq_e & 15);
-  u32x4 breg[G3<PT>::MODE == G3_REG ? DQ_NS : 1];   // G3_REG: raw of the next stage to convert
-  auto issue_b = [&](int s, int buf) {
-    if constexpr (PROBE & 4) return;
-    ctx.sb = s >> 2; ctx.q = s & 3;
-    if constexpr (Q::MODE == G3_DIRECT) Q::issue_b(Bs + buf * B_BYTES, ctx, NT, wave, lane);
-    else if constexpr (Q::MODE == G3_RAW_LDS) Q::issue(Rs + buf * R_BYTES, ctx, NT, wave, lane);
-  };
-  auto load_breg = [&](int s, u32x4* v) {
-    if constexpr (Q::MODE == G3_REG) {
-      ctx.sb = s >> 2; ctx.q = s & 3;
-      Q::template load<DQ_NS>(ctx, NT, dq_e, dq_part, v);
-    }
-  };
-  const Consts kc = make_consts();
-  auto store_b = [&](const half8_t* b, int buf) {
-    char* B = Bs + buf * B_BYTES;
-#pragma unroll
-    for (int j = 0; j < DQ_NS; ++j) *reinterpret_cast<half8_t*>(B + g3_off(dq_col, 4 * dq_h + DQ_NS * dq_part + j)) = b[j];
-  };
-  auto dequant = [&](int s, int buf) {   // raw R[buf] (registers for G3_REG) of stage s -> B[buf]
-    if constexpr (PROBE & 2) return;
-    half8_t b[DQ_NS];
-    if constexpr (Q::MODE == G3_RAW_LDS) {
-      Q::template dequant<DQ_NS>(Rs + buf * R_BYTES, NT, dq_e, dq_part, s & 3, kc, b);
-      store_b(b, buf);
-    } else if constexpr (Q::MODE == G3_REG) {
-      Q::template convert<DQ_NS>(breg, b);
-      store_b(b, buf);
-    }
+    src.sb = s >> 2; src.q = s & 3;
+    Q::template issue<TW>(stage_r(b), src, lane);
   };
 
-  f32x4 acc[FM][FN];
+  f32x4 acc[FM][TW];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < TW; ++u) acc[i][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const Consts kc = make_consts();
+  const int g = lane >> 4, rl = lane & 15;
 
-  // prologue: A(0), B/raw(0), raw(1) -> dequant(0)
-  issue_a(s_begin, 0);
-  issue_b(s_begin, 0);
-  if constexpr (Q::MODE == G3_RAW_LDS) {
-    if (s_begin + 1 < s_end) issue_b(s_begin + 1, 1);
-    __syncthreads();
-    dequant(s_begin, 0);
-  } else if constexpr (Q::MODE == G3_REG) {
-    load_breg(s_begin, breg);
-    dequant(s_begin, 0);
-    load_breg(min(s_begin + 1, s_end - 1), breg);
-  }
-  __syncthreads();
+  // prologue: NB - 1 stages in flight
+  issue(s_begin, 0);
+  if constexpr (NB == 3) issue(min(s_begin + 1, s_end - 1), 1);
+  if constexpr (NB == 3) wait_vmcnt<G::LOADS>(); else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
 
-  const int wm = wave / WN, wn = wave % WN;
-  const int rbase = wm * FM * 16 + (lane & 15), cbase = wn * FN * 16 + (lane & 15);
-  const int g = lane >> 4;
+  int b = 0;   // buffer of stage s
   for (int s = s_begin; s < s_end; ++s) {
-    const int t = s - s_begin, cur = t & 1;
-    // A(s+1) -> A[cur^1] and raw(s+2) -> R[cur] (or, 16-bit weights, B(s+1) -> B[cur^1]): both
-    // buffers were last read in iteration s-1
-    // (unconditional, stage clamped to the range: the loop body stays one basic block, so the
-    // scheduler can interleave the dequant VALU with the MFMAs; past-the-end loads re-read the last
-    // stage into buffers nobody reads, the last dequant converts stale bytes into an unread buffer)
-    const int s1 = min(s + 1, s_end - 1);
-    issue_a(s1, cur ^ 1);
-    if constexpr (Q::MODE == G3_DIRECT) issue_b(s1, cur ^ 1);
-    else issue_b(min(s + 2, s_end - 1), cur);
-    u32x4 bnext[Q::MODE == G3_REG ? DQ_NS : 1];   // G3_REG: raw(s+2), loaded while stage s computes
-    load_breg(min(s + 2, s_end - 1), bnext);
-    const char* Ab = As + cur * A_BYTES;
-    const char* Bb = Bs + cur * B_BYTES;
+    // stage s + NB - 1 (clamped: past-the-end stages re-load the last one into a buffer nobody
+    // reads, keeping the per-wave load count uniform) into the buffer stage s - 1 used
+    const int bn = b + NB - 1 >= NB ? b - 1 : b + NB - 1;
+    issue(min(s + NB - 1, s_end - 1), bn);
+    const char* A = stage_a(b);
+    const char* R = stage_r(b);
+    // raw bytes (NR LDS reads), then the first AD A fragments; the B fragments of k-half 0 once the
+    // raw reads are in, of k-half 1 a quarter into the MFMA stream; A fragment j (= kk FM + i) is
+    // waited for right before its TW MFMAs with fragment j + AD issued behind them
+    constexpr int NA = 2 * FM, AD = 8, NR = Q::NR(TW);
+    static_assert(AD < 16, "lgkmcnt range");   // (more than 15 reads in flight just stall issue)
+    typename Q::template Raw<TW> raw;
+    Q::template load<TW>(R, lane, raw);
+    u32x4 af[NA];
+    // row 16 i + rl has the swizzle of rl: fragment (kk, i) = base(kk) + 2048 i (immediate offset)
+    const uint32_t abase[2] = {lds_addr(A + g3_off(rl, g)), lds_addr(A + g3_off(rl, 4 + g))};
+    auto read_a = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      ds_b128o<(j % FM) * 2048>(af[j], abase[j / FM]);
+    };
+    static_for<AD>([&](auto jc) { read_a(jc); });
+    wait_lgkm<AD>();   // raw in
+    typename Q::Prep pr[TW];
+    half8_t bf[2][TW];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      half8_t a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const half8_t*>(Ab + g3_off(rbase + 16 * i, 4 * kk + g));
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const half8_t*>(Bb + g3_off(cbase + 16 * j, 4 * kk + g));
+    for (int u = 0; u < TW; ++u) {
+      pr[u] = Q::template prep<TW>(raw, u, s & 3, lane);
+      if constexpr (PROBE & 2) bf[0][u] = __builtin_bit_cast(half8_t, raw_as_u32x4(raw, u));
+      else bf[0][u] = Q::template frag<TW>(raw, pr[u], u, 0, lane, kc);
+    }
+    static_for<NA>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      wait_lgkm<(NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1)>();   // fragment j in
+      constexpr int kk = j / FM, i = j % FM;
       if constexpr (PROBE & 1) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(a[i]));
-#pragma unroll
-        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(b[j]));
+        asm volatile("" ::"v"(af[j]));
       } else {
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        for (int u = 0; u < TW; ++u) acc[i][u] = mfma16x16x32(__builtin_bit_cast(half8_t, af[j]), bf[kk][u], acc[i][u]);
       }
-    }
-    // dequant raw(s+1) -> B[cur^1] (landed at the end of iteration s-1).  Placed AFTER the MFMA
-    // code: its ds_writes may not move above the operand ds_reads (the compiler cannot separate the
-    // two B buffers), so written first it would serialise the whole dequant ahead of the first
-    // MFMA; written here, its VALU is free to fill the MFMA stream and only the 4 stores trail it.
-    dequant(s + 1, cur ^ 1);
-    if constexpr (Q::MODE == G3_REG) {
+      if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{});
+      if constexpr (j == FM / 2) {   // k-half 1's B fragments, behind the first MFMAs
 #pragma unroll
-      for (int j = 0; j < DQ_NS; ++j) breg[j] = bnext[j];
+        for (int u = 0; u < TW; ++u) {
+          if constexpr (PROBE & 2) bf[1][u] = __builtin_bit_cast(half8_t, raw_as_u32x4(raw, u) + 1u);
+          else bf[1][u] = Q::template frag<TW>(raw, pr[u], u, 1, lane, kc);
+        }
+      }
+    });
+    if constexpr (PROBE & 1) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int u = 0; u < TW; ++u) asm volatile("" ::"v"(bf[kk][u]));
     }
-    __syncthreads();
+    // stage s+1 landed (this wave's loads: all but the newest stage's), then every wave's: the
+    // barrier also ends every read of buffer b before the next iteration's loads overwrite it
+    if constexpr (NB == 3) wait_vmcnt<G::LOADS>(); else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    b = b + 1 == NB ? 0 : b + 1;
   }
+  wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
 
-  // epilogue: lane holds C[row 16 i + 4 g + v][col 16 j + r] of the wave tile
-  const int r = lane & 15;
-  const int row0 = m0 + wm * FM * 16 + 4 * g;
-  const int col0 = cg * BN + wn * FN * 16;
+  // epilogue: lane holds C[row 16 i + 4 g + v][col 16 u + r] of the wave's tiles
+  const int row0 = m0 + 4 * g;
+  const int col0 = cg * BN + wave * 16 * TW;
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = col0 + 16 * j + r;
+  for (int u = 0; u < TW; ++u) {
+    const int n = col0 + 16 * u + rl;
     if constexpr (EPI == EPI_SWIGLU) {
-      const int o = (n >> 4) * 8 + r;   // tile rows 0-7 gate, 8-15 up of the same 8 outputs
+      const int o = (n >> 4) * 8 + rl;   // tile rows 0-7 gate, 8-15 up of the same 8 outputs
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float other = __shfl_xor(acc[i][j][v], 8);
+          const float other = __shfl_xor(acc[i][u][v], 8);
           const int m = row0 + 16 * i + v;
-          if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(acc[i][j][v]) * other);
+          if (rl < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(acc[i][u][v]) * other);
         }
     } else {
       if (n < p.n_valid) {
@@ -495,8 +576,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
             const int m = row0 + 16 * i + v;
             if (m < M) {
               float* dst = p.Y + (size_t)blockIdx.y * p.split_stride + (size_t)m * p.ldy + n;
-              if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i][j][v] + bias);
-              else *dst = acc[i][j][v] + bias;
+              if constexpr (EPI == EPI_ATOMIC) unsafeAtomicAdd(dst, acc[i][u][v] + bias);
+              else *dst = acc[i][u][v] + bias;
             }
           }
       }
@@ -513,9 +594,14 @@ void set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) {
   g3_force_bm = bm; g3_force_bn = bn; g3_force_split = nsplit; g3_split_wg = split_wg > 0 ? split_wg : 256;
 }
 
-template <int PT, int EPI, int BM, int BN>
+template <int PT, int EPI, int BM, int TW, int PROBE>
+static void gemm3_launch(const GemvParams& p, dim3 grid, int n_mb, int per, int n_stages, hipStream_t st) {
+  hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, TW, PROBE>), grid, dim3(512), 0, st, p, n_mb, per, n_stages);
+}
+
+template <int PT, int EPI, int BM, int TW>
 static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
-  constexpr int NT = BN / 16;
+  constexpr int NT = 8 * TW;   // T16 tiles per workgroup
   const int n_cg = (p.ntiles + NT - 1) / NT;
   const int n_mb = (p.M + BM - 1) / BM;
   const int n_stages = p.nsb * 4;
@@ -528,41 +614,34 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
-  if constexpr (PT == P_Q4_K && EPI == EPI_SWIGLU && BM == 256 && BN == 256) {
+  const dim3 grid(wgs, nsplit);
+  if constexpr (PT == P_Q4_K && EPI == EPI_SWIGLU && BM == 256 && TW == 2) {
     switch (knob(KNOB_GEMM3_PROBE)) {   // timing probes (tools/gemv_bench.py --knob GEMM3_PROBE=k)
-      case 1: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 1>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
-      case 2: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 2>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
-      case 3: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 3>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
-      case 4: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 4>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
-      case 6: hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN, 6>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages); return;
+      case 1: return gemm3_launch<PT, EPI, BM, TW, 1>(p, grid, n_mb, per, n_stages, st);
+      case 2: return gemm3_launch<PT, EPI, BM, TW, 2>(p, grid, n_mb, per, n_stages, st);
+      case 3: return gemm3_launch<PT, EPI, BM, TW, 3>(p, grid, n_mb, per, n_stages, st);
+      case 4: return gemm3_launch<PT, EPI, BM, TW, 4>(p, grid, n_mb, per, n_stages, st);
+      case 6: return gemm3_launch<PT, EPI, BM, TW, 6>(p, grid, n_mb, per, n_stages, st);
       default: break;
     }
   }
-  hipLaunchKernelGGL((mpk::gemm3_kernel<PT, EPI, BM, BN>), dim3(wgs, nsplit), dim3(512), 0, st, p, n_mb, per, n_stages);
-}
-
-template <int PT, int BM, int BN>
-static constexpr bool g3_fits() {
-  return 2 * (BM * 128 + BN * 128 + mpk::G3<PT>::raw_bytes(BN / 16)) <= 160 * 1024;
+  gemm3_launch<PT, EPI, BM, TW, 0>(p, grid, n_mb, per, n_stages, st);
 }
 
 template <int PT, int EPI>
 static void gemm3_shape(GemvParams p, bool allow_split, hipStream_t st) {
-  // BM: 128 rows when one 128-row block holds M; BN: 256 columns unless that leaves fewer than
-  // half the CUs with a workgroup and the epilogue cannot split K
+  // BM: 128 rows when one 128-row block holds M; BN: 256 columns (2 tiles per wave) unless that
+  // leaves fewer than half the CUs with a workgroup and the epilogue cannot split K
   const int bm = g3_force_bm ? g3_force_bm : (p.M <= 128 ? 128 : 256);
   const int wg256 = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
   const bool splits = EPI == EPI_ATOMIC && allow_split;
   const int bn = g3_force_bn ? g3_force_bn : (!splits && wg256 < 128 ? 128 : 256);
   if (bm == 128) {
-    if (bn == 128) gemm3_go<PT, EPI, 128, 128>(p, allow_split, st);
-    else gemm3_go<PT, EPI, 128, 256>(p, allow_split, st);
+    if (bn == 128) gemm3_go<PT, EPI, 128, 1>(p, allow_split, st);
+    else gemm3_go<PT, EPI, 128, 2>(p, allow_split, st);
   } else {
-    // Q8_0's 32-B raw quants: 256 x 256 does not fit 160 KB of LDS double-buffered
-    if constexpr (g3_fits<PT, 256, 256>()) {
-      if (bn == 256) return gemm3_go<PT, EPI, 256, 256>(p, allow_split, st);
-    }
-    gemm3_go<PT, EPI, 256, 128>(p, allow_split, st);
+    if (bn == 128) gemm3_go<PT, EPI, 256, 1>(p, allow_split, st);
+    else gemm3_go<PT, EPI, 256, 2>(p, allow_split, st);
   }
 }
 
