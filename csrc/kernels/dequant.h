@@ -270,8 +270,8 @@ template <> struct Deq<P_Q4_0> {
   }
 };
 
-// bf16 pair (low, high halves of w) -> f16 pair: exact for every bf16 inside f16's normal range
-// (8 significant bits into 11); v_cvt_pkrtz rounds toward zero, so a bf16 beyond 65504 becomes
+// bf16 pair (low, high halves of w) -> f16 pair (dense unpack only: the GEMV/GEMM kernels keep bf16):
+// exact inside f16's normal range; v_cvt_pkrtz rounds toward zero, so a bf16 beyond 65504 becomes
 // +-65504 (saturation) instead of an infinity
 __device__ __forceinline__ uint32_t bf2_to_h2(uint32_t w) {
   return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__uint_as_float(w << 16), __uint_as_float(w & 0xFFFF0000u)));
@@ -311,10 +311,11 @@ template <> struct Deq<P_BF16> {
   }
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane, const Consts&) { dequant<H>(r, b, lane); }
+  // the bf16 bits themselves: every consumer runs mma<true> on them (kcommon.h)
   template <int H>
   __device__ static __forceinline__ void dequant(const Raw& r, half8_t b[4], int lane) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) b[s] = bf8_to_h8(r.v[4 * H + s]);
+    for (int s = 0; s < 4; ++s) b[s] = __builtin_bit_cast(half8_t, r.v[4 * H + s]);
   }
 };
 

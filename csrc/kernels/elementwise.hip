@@ -129,9 +129,14 @@ __device__ float deq_elem(int t, const uint8_t* row, int e) {
 
 __global__ __launch_bounds__(256) void embed_kernel(int t, const uint8_t* table, int64_t rb, int d,
                                                     const int32_t* tokens, float* x, int ldx) {
+  // one element per thread, d / 256 workgroups per token: each element is a short chain of
+  // dependent block-header loads, so the row's latency is one chain, not d / 256 of them in a row
+  // (one workgroup per token took 12.8 us for the 8B row, r5c_prof_8b_mb1.txt)
   const int m = blockIdx.x;
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  if (e >= d) return;
   const uint8_t* row = table + (int64_t)tokens[m] * rb;
-  for (int e = threadIdx.x; e < d; e += 256) x[(size_t)m * ldx + e] = deq_elem(t, row, e);
+  x[(size_t)m * ldx + e] = deq_elem(t, row, e);
 }
 
 // ---------------------------------------------------------------- RoPE (NORM, adjacent pairs) + KV append
@@ -388,7 +393,7 @@ void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f
 
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,
                   int ldx, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::embed_kernel, dim3(M), dim3(256), 0, st, t, table, rb, d, tokens, x, ldx);
+  hipLaunchKernelGGL(mpk::embed_kernel, dim3(M, (d + 255) / 256), dim3(256), 0, st, t, table, rb, d, tokens, x, ldx);
 }
 
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {

@@ -73,8 +73,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemvParams p) {
         const f16* xr = &xs[cur][(16 * ms + r) * GM_LDX + (t16_xoff(g, 4 * h) ^ x_qswap(r))];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const half8_t a = *reinterpret_cast<const half8_t*>(xr + 8 * s);
-          acc[ms] = mfma16x16x32(a, b[s], acc[ms]);
+          const half8_t a = x_op<PT == P_BF16>(*reinterpret_cast<const half8_t*>(xr + 8 * s));
+          acc[ms] = mma<PT == P_BF16>(a, b[s], acc[ms]);
         }
       }
     }

@@ -377,7 +377,7 @@ template <> struct W3<P_Q4_0> {
   }
 };
 
-// 16-bit weights (F16, or BF16 widened to f16 per fragment): the fragment bytes themselves,
+// 16-bit weights (F16, or BF16 for the bf16 MFMA: the A fragments go to bf16): the fragment bytes themselves,
 // [u][kk][lane] 16 B = element 4 kk + g of lane (q, r) of the T16 chunk
 template <int PT> struct W3_16 {
   static constexpr int CB = chunk_bytes(PT);
@@ -403,8 +403,7 @@ template <int PT> struct W3_16 {
   __device__ static __forceinline__ Prep prep(const Raw<TW>&, int, int, int) { return Prep{}; }
   template <int TW>
   __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep&, int u, int kk, int, const Consts&) {
-    if constexpr (PT == P_BF16) return bf8_to_h8(w.v[u][kk]);
-    else return __builtin_bit_cast(half8_t, w.v[u][kk]);
+    return __builtin_bit_cast(half8_t, w.v[u][kk]);
   }
 };
 template <> struct W3<P_F16> : W3_16<P_F16> {};
@@ -417,6 +416,8 @@ __device__ __forceinline__ u32x4 raw_as_u32x4(const RawT& r, int u) {
   return u32x4{w[0], w[1], w[2], w[3 + u]};
 }
 
+
+#define G3_AD(BM, TW) 8
 template <int PT, int BM, int TW>
 struct G3Geom {
   static constexpr int A_BYTES = BM * 128;                    // x rows of one stage
@@ -435,6 +436,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   using Q = W3<PT>;
   using G = G3Geom<PT, BM, TW>;
   constexpr int NB = G::NB, FM = BM / 16, BN = 128 * TW;
+  constexpr bool BF = PT == P_BF16;
   __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -455,8 +457,9 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   auto stage_a = [&](int b) { return smem + b * G::STAGE; };
   auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
 
-  // every wave issues exactly G::LOADS LDS-DMA instructions per stage (counted vmcnt below)
-  auto issue = [&](int s, int b) {
+  // every wave issues exactly G::A_INSTR (x) + Q::NI(TW) (its raw weight bytes) LDS-DMA
+  // instructions per stage (the counted vmcnt waits below rely on it; glds_n keeps lane 0 active)
+  auto issue_a = [&](int s, int b) {
     if constexpr (PROBE & 4) return;
     const int k0 = s * 64;
 #pragma unroll
@@ -467,9 +470,13 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
       const int gr = min(m0 + row, M - 1);
       glds<16>(p.X + (size_t)gr * p.ldx + k0 + 8 * ch, stage_a(b) + pc * 1024);
     }
+  };
+  auto issue_b = [&](int s, int b) {
+    if constexpr (PROBE & 4) return;
     src.sb = s >> 2; src.q = s & 3;
     Q::template issue<TW>(stage_r(b), src, lane);
   };
+  constexpr int NIB = (PROBE & 4) ? 0 : Q::NI(TW);
 
   f32x4 acc[FM][TW];
 #pragma unroll
@@ -479,61 +486,100 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   const Consts kc = make_consts();
   const int g = lane >> 4, rl = lane & 15;
 
-  // prologue: NB - 1 stages in flight
-  issue(s_begin, 0);
-  if constexpr (NB == 3) issue(min(s_begin + 1, s_end - 1), 1);
-  if constexpr (NB == 3) wait_vmcnt<G::LOADS>(); else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
-  int b = 0;   // buffer of stage s
-  for (int s = s_begin; s < s_end; ++s) {
-    // stage s + NB - 1 (clamped: past-the-end stages re-load the last one into a buffer nobody
-    // reads, keeping the per-wave load count uniform) into the buffer stage s - 1 used
-    const int bn = b + NB - 1 >= NB ? b - 1 : b + NB - 1;
-    issue(min(s + NB - 1, s_end - 1), bn);
-    const char* A = stage_a(b);
-    const char* R = stage_r(b);
-    // raw bytes (NR LDS reads), then the first AD A fragments; the B fragments of k-half 0 once the
-    // raw reads are in, of k-half 1 a quarter into the MFMA stream; A fragment j (= kk FM + i) is
-    // waited for right before its TW MFMAs with fragment j + AD issued behind them
-    constexpr int NA = 2 * FM, AD = 8, NR = Q::NR(TW);
-    static_assert(AD < 16, "lgkmcnt range");   // (more than 15 reads in flight just stall issue)
-    typename Q::template Raw<TW> raw;
-    Q::template load<TW>(R, lane, raw);
-    u32x4 af[NA];
-    // row 16 i + rl has the swizzle of rl: fragment (kk, i) = base(kk) + 2048 i (immediate offset)
-    const uint32_t abase[2] = {lds_addr(A + g3_off(rl, g)), lds_addr(A + g3_off(rl, 4 + g))};
-    auto read_a = [&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      ds_b128o<(j % FM) * 2048>(af[j], abase[j / FM]);
-    };
-    static_for<AD>([&](auto jc) { read_a(jc); });
-    wait_lgkm<AD>();   // raw in
-    typename Q::Prep pr[TW];
-    half8_t bf[2][TW];
+  // One continuous LDS-read / MFMA stream over all stages.  Iteration s runs the NA = 2 FM
+  // fragment steps j of stage s; A fragments are read AD steps ahead, across the stage boundary:
+  // the reads of stage s+1's first fragments (and its raw bytes) start at step JB, right behind the
+  // iteration's single barrier, so a stage starts with its operands already in registers and its
+  // k-half-0 B fragments already dequantized (no per-stage pipe bubble).
+  //   barrier of iteration s (after step JB's MFMAs): every wave has landed stage s+1 and has
+  //   finished iteration s-1 (so buffer (s-1) % 3 is free) -> issue stage s+2's x rows into it and
+  //   stage s+3's weight bytes into the raw slot of stage s (read, and waited for, in iteration
+  //   s-1), then read stage s+1.  The weights come from HBM: issued three stages ahead they get two
+  //   stages of latency (loads retire in order, so the wait for x(s+1) leaves only w(s+2) behind).
+  static_assert(NB == 3, "gemm3: the cross-stage stream needs 3 stage buffers");
+  constexpr int NA = 2 * FM, AD = G3_AD(BM, TW), NR = Q::NR(TW), JB = NA - AD - 1;
+  static_assert(JB > FM / 2 && NA - AD > JB, "gemm3: barrier step");
+  typename Q::template Raw<TW> raw;   // this stage's raw bytes
+  typename Q::Prep pr[TW];
+  half8_t bf[2][TW];
+  u32x4 af[NA];
+  auto abase = [&](int b, int kk) { return lds_addr(stage_a(b) + g3_off(rl, 4 * kk + g)); };
+  // row 16 i + rl has the swizzle of rl: fragment (kk, i) = base(kk) + 2048 i (immediate offset)
+  auto read_a = [&](auto jc, u32x4& dst, uint32_t base) {
+    constexpr int j = decltype(jc)::value;
+    ds_b128o<(j % FM) * 2048>(dst, base);
+  };
+  auto dequant0 = [&](const typename Q::template Raw<TW>& w, typename Q::Prep* p, int q) {
 #pragma unroll
     for (int u = 0; u < TW; ++u) {
-      pr[u] = Q::template prep<TW>(raw, u, s & 3, lane);
-      if constexpr (PROBE & 2) bf[0][u] = __builtin_bit_cast(half8_t, raw_as_u32x4(raw, u));
-      else bf[0][u] = Q::template frag<TW>(raw, pr[u], u, 0, lane, kc);
+      p[u] = Q::template prep<TW>(w, u, q, lane);
+      if constexpr (PROBE & 2) bf[0][u] = __builtin_bit_cast(half8_t, raw_as_u32x4(w, u));
+      else bf[0][u] = Q::template frag<TW>(w, p[u], u, 0, lane, kc);
     }
+  };
+
+  // prologue: stages 0, 1 (and 2's weights) in flight; stage 0's raw, first AD fragments, k-half-0 B fragments
+  issue_a(s_begin, 0);
+  issue_b(s_begin, 0);
+  issue_a(min(s_begin + 1, s_end - 1), 1);
+  issue_b(min(s_begin + 1, s_end - 1), 1);
+  issue_b(min(s_begin + 2, s_end - 1), 2);
+  wait_vmcnt<(PROBE & 4) ? 0 : G::A_INSTR + 2 * NIB>();
+  __builtin_amdgcn_s_barrier();
+  Q::template load<TW>(stage_r(0), lane, raw);
+  {
+    const uint32_t a0 = abase(0, 0);
+    static_for<AD>([&](auto jc) { read_a(jc, af[decltype(jc)::value], a0); });
+  }
+  wait_lgkm<AD>();   // raw in (the oldest reads)
+  dequant0(raw, pr, s_begin & 3);
+
+  // one stage; the loop runs it twice per trip with the (current, next) register sets swapped, so
+  // the next stage's fragments never need a register copy (their reads are still in flight at the
+  // end of the stage: a v_mov would read them early)
+  using RawT = typename Q::template Raw<TW>;
+  using PrepT = typename Q::Prep;
+  auto stage = [&](const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n,
+                   PrepT (&pr)[TW], PrepT (&pr_n)[TW]) {
+    const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;   // buffers of stages s+1, s+2 (= s-1)
+    const uint32_t a0 = abase(b, 0), a1 = abase(b, 1);
+    const uint32_t n0 = abase(b1, 0);
     static_for<NA>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      wait_lgkm<(NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1)>();   // fragment j in
       constexpr int kk = j / FM, i = j % FM;
+      // reads issued after fragment j: the rest of this stage's look-ahead, plus (from step JB on)
+      // the next stage's raw bytes and its first fragments (exact issue counts: completion is in
+      // order, so lgkmcnt(n) retires everything but the n youngest); capped at the counter's 15
+      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (j > JB ? NR + (j - JB - 1) : 0);
+      wait_lgkm<(later < 15 ? later : 15)>();
       if constexpr (PROBE & 1) {
         asm volatile("" ::"v"(af[j]));
       } else {
 #pragma unroll
-        for (int u = 0; u < TW; ++u) acc[i][u] = mfma16x16x32(__builtin_bit_cast(half8_t, af[j]), bf[kk][u], acc[i][u]);
+        for (int u = 0; u < TW; ++u) acc[i][u] = mma<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[kk][u], acc[i][u]);
       }
-      if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{});
+      if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], (j + AD) / FM ? a1 : a0);
       if constexpr (j == FM / 2) {   // k-half 1's B fragments, behind the first MFMAs
 #pragma unroll
         for (int u = 0; u < TW; ++u) {
           if constexpr (PROBE & 2) bf[1][u] = __builtin_bit_cast(half8_t, raw_as_u32x4(raw, u) + 1u);
           else bf[1][u] = Q::template frag<TW>(raw, pr[u], u, 1, lane, kc);
         }
+      }
+      if constexpr (j == JB) {
+        wait_vmcnt<NIB>();   // x(s+1) and w(s+1) in: only w(s+2) (issued after x(s+1)) may be in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue_a(min(s + 2, s_end - 1), b2);
+        issue_b(min(s + 3, s_end - 1), b);
+        Q::template load<TW>(stage_r(b1), lane, raw_n);
+      }
+      if constexpr (j > JB) {   // stage s+1's fragment j - JB - 1 (all k-half 0: AD <= FM)
+        read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], n0);
+      }
+      if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
+        wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
+        dequant0(raw_n, pr_n, (s + 1) & 3);   // (bf[0] of stage s is consumed: last use at j = FM - 1)
       }
     });
     if constexpr (PROBE & 1) {
@@ -542,13 +588,20 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
 #pragma unroll
         for (int u = 0; u < TW; ++u) asm volatile("" ::"v"(bf[kk][u]));
     }
-    // stage s+1 landed (this wave's loads: all but the newest stage's), then every wave's: the
-    // barrier also ends every read of buffer b before the next iteration's loads overwrite it
-    if constexpr (NB == 3) wait_vmcnt<G::LOADS>(); else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    b = b + 1 == NB ? 0 : b + 1;
+  };
+  u32x4 afB[NA];
+  RawT rawB;
+  PrepT prB[TW];
+  int s = s_begin, b = 0;
+  for (; s + 1 < s_end; s += 2) {
+    stage(s, b, af, afB, raw, rawB, pr, prB);
+    b = b == 2 ? 0 : b + 1;
+    stage(s + 1, b, afB, af, rawB, raw, prB, pr);
+    b = b == 2 ? 0 : b + 1;
   }
+  if (s < s_end) stage(s, b, af, afB, raw, rawB, pr, prB);
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
+  wait_lgkm<0>();
 
   // epilogue: lane holds C[row 16 i + 4 g + v][col 16 u + r] of the wave's tiles
   const int row0 = m0 + 4 * g;
@@ -601,6 +654,9 @@ static void gemm3_launch(const GemvParams& p, dim3 grid, int n_mb, int per, int 
 
 template <int PT, int EPI, int BM, int TW>
 static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
+  if constexpr (mpk::G3Geom<PT, BM, TW>::NB < 3) {   // 16-bit 256 x 256: 3 stages do not fit in LDS
+    return gemm3_go<PT, EPI, BM, 1>(p, allow_split, st);
+  } else {
   constexpr int NT = 8 * TW;   // T16 tiles per workgroup
   const int n_cg = (p.ntiles + NT - 1) / NT;
   const int n_mb = (p.M + BM - 1) / BM;
@@ -626,6 +682,7 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
     }
   }
   gemm3_launch<PT, EPI, BM, TW, 0>(p, grid, n_mb, per, n_stages, st);
+  }
 }
 
 template <int PT, int EPI>
@@ -635,7 +692,9 @@ static void gemm3_shape(GemvParams p, bool allow_split, hipStream_t st) {
   const int bm = g3_force_bm ? g3_force_bm : (p.M <= 128 ? 128 : 256);
   const int wg256 = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
   const bool splits = EPI == EPI_ATOMIC && allow_split;
-  const int bn = g3_force_bn ? g3_force_bn : (!splits && wg256 < 128 ? 128 : 256);
+  // split-K (ATOMIC) shapes: 128 columns (r6e, M = 256: 70B qkv 104 -> 77 us, o 101 -> 74, down
+  // 186 -> 161, 8B down 91 -> 65); SwiGLU / store keep 256 unless that leaves half the CUs idle
+  const int bn = g3_force_bn ? g3_force_bn : (splits || wg256 < 128 ? 128 : 256);
   if (bm == 128) {
     if (bn == 128) gemm3_go<PT, EPI, 128, 1>(p, allow_split, st);
     else gemm3_go<PT, EPI, 128, 2>(p, allow_split, st);

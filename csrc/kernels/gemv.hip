@@ -35,6 +35,7 @@ __global__ __launch_bounds__(64) void unpack_kernel(const uint8_t* W, int nsb, f
     else D::template dequant<1>(raw, b, lane);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
+      if constexpr (PT == P_BF16) b[s] = bf8_to_h8(__builtin_bit_cast(u32x4, b[s]));   // dense f16 output
       f16* o = out + (size_t)(tile * 16 + r) * ldo + sb * 256 + t16_xoff(g, 4 * h + s);
       *reinterpret_cast<half8_t*>(o) = b[s];
     }

@@ -40,6 +40,7 @@ constexpr int G2_LDX = 256 + 8;
 template <int PT, int EPI, int NW, int NSLOT, int MT, int TW, bool NORM>
 __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   using D = Deq<PT>;
+  constexpr bool BF = PT == P_BF16;
   constexpr int CB = D::CB;
   constexpr int NT = NW * 64;
   constexpr int XC = 512 * MT;   // 16 B x chunks per super-block
@@ -157,9 +158,9 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const half8_t a = *reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 8 * s);
+        const half8_t a = x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 8 * s));
 #pragma unroll
-        for (int t = 0; t < TW; ++t) acc[t][mt] = mfma16x16x32(a, b[t][s], acc[t][mt]);
+        for (int t = 0; t < TW; ++t) acc[t][mt] = mma<BF>(a, b[t][s], acc[t][mt]);
       }
 #pragma unroll
     for (int t = 0; t < TW; ++t) D::template dequant<1>(ring[sl][t], b[t], lane, kc);
@@ -167,9 +168,9 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const half8_t a = *reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 32 + 8 * s);
+        const half8_t a = x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 32 + 8 * s));
 #pragma unroll
-        for (int t = 0; t < TW; ++t) acc[t][mt] = mfma16x16x32(a, b[t][s], acc[t][mt]);
+        for (int t = 0; t < TW; ++t) acc[t][mt] = mma<BF>(a, b[t][s], acc[t][mt]);
       }
     store_x((sl + 1) % NSLOT, buf ^ 1, cur + 1 < sbB);   // x(cur + 1), loaded NSLOT - 1 steps ago
     issue(sl, cur + NSLOT);

@@ -47,6 +47,7 @@ template <int PT, int EPI, int G, bool NORM, int NSO = 0>
 __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
+  constexpr bool BF = PT == P_BF16;
   constexpr int KSW = GS_NW / G;
   constexpr int NS = NSO ? NSO : is16(PT) ? 2 : 4;   // weight super-blocks in flight per wave
   extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange]
@@ -191,15 +192,15 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       half8_t a = {};
-      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 8 * i);
-      acc = mfma16x16x32(a, b[i], acc);
+      if (xr_ok) a = x_op<BF>(*reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 8 * i));
+      acc = mma<BF>(a, b[i], acc);
     }
     D::template dequant<1>(ring[s], b, lane, kc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       half8_t a = {};
-      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 32 + 8 * i);
-      acc = mfma16x16x32(a, b[i], acc);
+      if (xr_ok) a = x_op<BF>(*reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 32 + 8 * i));
+      acc = mma<BF>(a, b[i], acc);
     }
   };
   const int n = wB - wA;

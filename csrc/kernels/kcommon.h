@@ -19,6 +19,29 @@ __device__ __forceinline__ f32x4 mfma16x16x32(half8_t a, half8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// bf16 MFMA operands travel in the same 16-byte containers as f16 ones (a half8_t holds the bits)
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ half8_t h8_to_bf8(half8_t a) {   // 8 f16 -> 8 bf16 (round to nearest even)
+  bf16x8_t r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (__bf16)(float)a[i];
+  return __builtin_bit_cast(half8_t, r);
+}
+// Weight-type MFMA.  BF: bf16 weights (P_BF16) -- their fragments are the packed bf16 bits and the
+// f16 activation fragment goes through x_op (-> bf16) first, so the product runs on the bf16 MFMA
+// with bf16's full exponent range (no narrowing of the weights to f16).  !BF: f16 MFMA.
+template <bool BF>
+__device__ __forceinline__ half8_t x_op(half8_t a) {
+  if constexpr (BF) return h8_to_bf8(a);
+  else return a;
+}
+template <bool BF>
+__device__ __forceinline__ f32x4 mma(half8_t a, half8_t b, f32x4 c) {
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ half8_t pack8(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
   u32x4 v = {w0, w1, w2, w3};
   return __builtin_bit_cast(half8_t, v);

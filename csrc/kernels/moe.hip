@@ -79,14 +79,14 @@ __global__ __launch_bounds__(64) void moe_gemv_kernel(const MoeGemvParams p) {
         if (cur < sb1) {
           half8_t a[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 8 * i);
+          for (int i = 0; i < 8; ++i) a[i] = x_op<PT == P_BF16>(*reinterpret_cast<const half8_t*>(xp + (size_t)cur * 256 + 8 * i));
           half8_t b[4];
           D::template dequant<0>(ring[sl], b, lane);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[s], b[s], acc);
+          for (int s = 0; s < 4; ++s) acc = mma<PT == P_BF16>(a[s], b[s], acc);
           D::template dequant<1>(ring[sl], b, lane);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma16x16x32(a[4 + s], b[s], acc);
+          for (int s = 0; s < 4; ++s) acc = mma<PT == P_BF16>(a[4 + s], b[s], acc);
           if (cur + NSLOT < sb1) D::load(ring[sl], wt + (size_t)(cur + NSLOT) * CB, lane);
         }
       }
@@ -125,6 +125,7 @@ template <int PT, int EPI, int NW, int NSLOT, int MT>
 __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams p) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
+  constexpr bool BF = PT == P_BF16;
   constexpr int NT = NW * 64;
   constexpr int XC = 512 * MT;
   constexpr int XCH = (XC + NT - 1) / NT;
@@ -192,13 +193,15 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        if (mt == 0 || mt < mte) acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 8 * s), b[s], acc[mt]);
+        if (mt == 0 || mt < mte)
+          acc[mt] = mma<BF>(x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 8 * s)), b[s], acc[mt]);
     D::template dequant<1>(ring[sl], b, lane);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        if (mt == 0 || mt < mte) acc[mt] = mfma16x16x32(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 32 + 8 * s), b[s], acc[mt]);
+        if (mt == 0 || mt < mte)
+          acc[mt] = mma<BF>(x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * MOE_LDX + 32 + 8 * s)), b[s], acc[mt]);
     store_x((sl + 1) % NSLOT, buf ^ 1);   // x(cur + 1), loaded NSLOT - 1 steps ago
     issue(sl, min(cur + NSLOT, last));
     __syncthreads();

@@ -1,0 +1,100 @@
+"""Failure recovery with HIP stages (VERDICT r2 "do next" 3: the failover and elastic-restart paths
+were only ever exercised with CPU stages).
+
+  * in-process failover: a 2-stage GPU pipeline (both stages on the box's one GPU) whose second
+    stage faults mid-request; the orchestrator rebuilds the engine on the surviving stage and the
+    request completes with the fault-free text.
+  * elastic restart: two torchrun ranks, one HIP stage each on GPU 0 (gloo rendezvous, TCP links:
+    RCCL refuses two ranks of one communicator on one GPU); rank 1 dies after 7 rounds, torchrun
+    restarts both, they resume from the last checkpoint and generate the uninterrupted tokens.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import REPO, make_model
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(REPO, "distributed-llm-pipeline_amd", "bin")
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_failover_hip_stages_repartitions(cuda, native, model_dir):
+    import httpx
+    path, _ = make_model(model_dir, "tiny-l3", "Q8_0")
+    assert os.path.exists(os.path.join(BIN, "orchestrator"))
+    prompt = "The pipeline sends activations"
+    base = [os.path.join(BIN, "mi-cli"), "-m", path, "-c", "256", "-ngl", "99", "--no-display-prompt"]
+    ref = subprocess.run(base + ["-p", prompt, "-n", "40"], capture_output=True, timeout=180)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    ref = ref.stdout.decode("utf-8", errors="replace").rstrip("\n")
+    port = _free_port()
+    proc = subprocess.Popen([os.path.join(BIN, "orchestrator"), "--host", "127.0.0.1", "--port", str(port),
+                             "-m", path, "-ngl", "99", "-c", "256", "--stages", "2", "--devices", "0,0",
+                             "--split", "even"],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                            env={**os.environ, "MIPIPE_FAULT": json.dumps({"stage": 1, "fail_at": 25})})
+    url = f"http://127.0.0.1:{port}"
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 90:
+            try:
+                httpx.get(url + "/health", timeout=1)
+                break
+            except Exception:   # noqa: BLE001
+                time.sleep(0.2)
+        h = httpx.get(url + "/health", timeout=30).json()
+        assert len(h["stages"]) == 2 and all(s["backend"] == "hip" for s in h["stages"]), h
+        r = httpx.post(url + "/completion", json={"prompt": prompt, "n_predict": 40}, timeout=180).json()
+        assert r["content"] == ref
+        h = httpx.get(url + "/health", timeout=30).json()
+        assert h["ok"] and h["engine_restarts"] == 1
+        assert len(h["stages"]) == 1 and h["stages"][0]["backend"] == "hip"   # re-partitioned, still on the GPU
+    finally:
+        proc.terminate()
+        proc.wait(timeout=30)
+
+
+_ELASTIC = r"""
+import json, os, sys
+sys.path.insert(0, {repo!r})
+from mipipe.parallel import generate_elastic
+import torch.distributed as dist
+out = generate_elastic({prompts!r}, {n!r}, {ckpt!r}, every=3, pp=2, gguf={path!r}, device=0, pg_backend="gloo",
+                       link="tcp", max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16, split="even", base_port={port})
+print("OUT " + json.dumps(dict(rank=int(os.environ["RANK"]), restart=os.environ.get("TORCHELASTIC_RESTART_COUNT"),
+                               out=out)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_elastic_restart_hip_stages(cuda, native, model_dir, tmp_path):
+    from mipipe.engine import Engine
+    path, _ = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts, n = [[5, 6, 7, 8], [9, 10]], 12
+    with Engine(gguf=path, max_ctx=128, n_mb=2, mb_size=1, prefill_chunk=16) as eng:
+        ref, _ = eng.generate(prompts, n)
+    ckpt = tmp_path / "ckpt"
+    script = tmp_path / "run.py"
+    script.write_text(_ELASTIC.format(repo=REPO, path=path, prompts=prompts, n=n, ckpt=str(ckpt), port=_free_port()))
+    env = dict(os.environ, MIPIPE_ELASTIC_FAIL="1,7")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2", "--max-restarts", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    outs = [json.loads(l[4:]) for l in p.stdout.splitlines() if l.startswith("OUT ")]
+    assert {o["restart"] for o in outs} == {"1"}, outs   # only the restarted attempt finished
+    assert all(o["out"] == ref for o in outs)

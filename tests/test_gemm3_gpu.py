@@ -117,3 +117,31 @@ def test_gemm3_matches_gemv_bf16(cuda, native, M):
     y = gemm(w, xh.cuda(), EPI_STORE, v=3).cpu()
     y2 = torch.cat([gemv(w, xh[r:r + 64].cuda(), EPI_STORE).cpu() for r in range(0, M, 64)])
     assert nmse(y, y2) < 1e-6
+
+
+@pytest.mark.parametrize("M", [1, 64, 128, 300])
+def test_bf16_weights_keep_their_range(cuda, native, M):
+    """BF16 weights run on the bf16 MFMA (activations rounded to bf16), never narrowed to f16: rows
+    of magnitude 1e6 (past f16's 65504) and 1e-9 (below f16's subnormals) come out right in the
+    decode GEMV (M <= 64) and in the GEMM (M > 64)."""
+    from mipipe.ops.kernels import PackedWeight, gemm, gemv, gemv_small, EPI_STORE
+    n, k = 64, 512
+    rng = np.random.default_rng(11)
+    wf = rng.standard_normal((n, k)).astype(np.float32)
+    wf[:16] *= 1e6      # beyond f16
+    wf[16:32] *= 1e-9   # below f16
+    raw = Q.quantize(wf, Q.BF16)
+    deq = torch.from_numpy(Q.dequantize(raw, Q.BF16).reshape(n, k))
+    assert deq[:16].abs().max() > 65504 and deq[16:32].abs().max() < 6e-8
+    w = PackedWeight(raw, Q.BF16, n, k)
+    g = torch.Generator().manual_seed(M)
+    xh = torch.zeros(M, w.k_pad, dtype=torch.float16)
+    xh[:, :k] = (torch.randn(M, k, generator=g) * 1e-3).half()
+    ref = xh[:, :k].bfloat16().float() @ deq.T
+    ys = [(gemv(w, xh.cuda(), EPI_STORE) if M <= 64 else gemm(w, xh.cuda(), EPI_STORE, v=3)).cpu()]
+    if M == 1:
+        ys.append(gemv_small(w, EPI_STORE, x=xh.cuda()).cpu())   # the single-stream kernel (gemvs)
+    for y in ys:
+        for rows in (slice(0, 16), slice(16, 32), slice(32, 64)):
+            assert torch.isfinite(y[:, rows]).all()
+            assert nmse(y[:, rows], ref[:, rows]) < 1e-5, rows
