@@ -139,6 +139,22 @@ __global__ __launch_bounds__(256) void embed_kernel(int t, const uint8_t* table,
   x[(size_t)m * ldx + e] = deq_elem(t, row, e);
 }
 
+// ---------------------------------------------------------------- int8 activation rows (K15 prototype)
+__global__ __launch_bounds__(256) void quant_rows_i8_kernel(const f16* X, int ldx, int K, int8_t* Q, int ldq, float* xs) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const f16* x = X + (size_t)m * ldx;
+  float mx = 0.f;
+  for (int k = tid; k < K; k += 256) mx = fmaxf(mx, fabsf((float)x[k]));
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = mx > 0.f ? mx / 127.f : 1.f, inv = 1.f / s;
+  for (int k = tid; k < K; k += 256) Q[(size_t)m * ldq + k] = (int8_t)__float2int_rn((float)x[k] * inv);
+  if (tid == 0) xs[m] = s;
+}
+
 // ---------------------------------------------------------------- RoPE (NORM, adjacent pairs) + KV append
 __global__ __launch_bounds__(256) void rope_kv_kernel(const RopeKvParams p) {
   // grid (M tokens, head groups of 4 over [q heads | k heads | v heads]); one thread per pair
@@ -394,6 +410,10 @@ void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,
                   int ldx, hipStream_t st) {
   hipLaunchKernelGGL(mpk::embed_kernel, dim3(M, (d + 255) / 256), dim3(256), 0, st, t, table, rb, d, tokens, x, ldx);
+}
+
+void launch_quant_rows_i8(const f16* X, int ldx, int M, int K, int8_t* Q, int ldq, float* xs, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::quant_rows_i8_kernel, dim3(M), dim3(256), 0, st, X, ldx, K, Q, ldq, xs);
 }
 
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {

@@ -409,6 +409,41 @@ template <int PT> struct W3_16 {
 template <> struct W3<P_F16> : W3_16<P_F16> {};
 template <> struct W3<P_BF16> : W3_16<P_BF16> {};
 
+// int8 weights (P_I8, the int8-activation prototype): 16 rows x 256 k int8 per chunk,
+// 16-B piece (st, kk, lane) at ((2 st + kk) * 64 + lane) * 16 holding row r = lane & 15,
+// k = 128 st + 64 kk + 16 (lane >> 4) + j.  Stages are 128 k (two per super-block): the A image
+// keeps its 128-byte rows (128 int8 activations), and one k-half kk is one v_mfma_i32_16x16x64_i8
+// (A and B index k the same way inside the 64, which is all a dot product needs).
+template <> struct W3<P_I8> {
+  static constexpr int CB = chunk_bytes(P_I8);
+  static constexpr int RAW(int TW) { return TW * 2048; }
+  static constexpr int NI(int TW) { return 2 * TW; }
+  static constexpr int NR(int TW) { return 2 * TW; }
+  template <int TW> struct Raw { u32x4 v[TW][2]; };
+  struct Prep {};
+  template <int TW>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+#pragma unroll
+    for (int f = 0; f < 2 * TW; ++f)
+      glds<16>(c.chunk(f >> 1, CB) + ((2 * c.q + (f & 1)) * 64 + lane) * 16, R + f * 1024);
+  }
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
+#pragma unroll
+    for (int u = 0; u < TW; ++u)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) ds_b128(w.v[u][kk], R + (u * 2 + kk) * 1024 + lane * 16);
+  }
+  template <int TW>
+  __device__ static __forceinline__ Prep prep(const Raw<TW>&, int, int, int) { return Prep{}; }
+  template <int TW>
+  __device__ static __forceinline__ half8_t frag(const Raw<TW>& w, const Prep&, int u, int kk, int, const Consts&) {
+    return __builtin_bit_cast(half8_t, w.v[u][kk]);
+  }
+};
+// stages per 256-k super-block: 64 k per stage for 16-bit activations, 128 for int8 ones
+template <int PT> constexpr int g3_spb() { return PT == P_I8 ? 2 : 4; }
+
 // PROBE & 2: some raw bits as a "fragment" (no dequant VALU)
 template <class RawT>
 __device__ __forceinline__ u32x4 raw_as_u32x4(const RawT& r, int u) {
@@ -459,21 +494,21 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
 
   // every wave issues exactly G::A_INSTR (x) + Q::NI(TW) (its raw weight bytes) LDS-DMA
   // instructions per stage (the counted vmcnt waits below rely on it; glds_n keeps lane 0 active)
+  constexpr int SPB = g3_spb<PT>(), XB = PT == P_I8 ? 1 : 2;   // stages per super-block, bytes per x element
   auto issue_a = [&](int s, int b) {
     if constexpr (PROBE & 4) return;
-    const int k0 = s * 64;
 #pragma unroll
     for (int i = 0; i < G::A_INSTR; ++i) {   // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7
       const int pc = wave * G::A_INSTR + i;
       const int row = 8 * pc + (lane >> 3);
       const int ch = (lane & 7) ^ g3_swz(row);
       const int gr = min(m0 + row, M - 1);
-      glds<16>(p.X + (size_t)gr * p.ldx + k0 + 8 * ch, stage_a(b) + pc * 1024);
+      glds<16>(reinterpret_cast<const char*>(p.X) + (size_t)gr * p.ldx * XB + s * 128 + 16 * ch, stage_a(b) + pc * 1024);
     }
   };
   auto issue_b = [&](int s, int b) {
     if constexpr (PROBE & 4) return;
-    src.sb = s >> 2; src.q = s & 3;
+    src.sb = s / SPB; src.q = s % SPB;
     Q::template issue<TW>(stage_r(b), src, lane);
   };
   constexpr int NIB = (PROBE & 4) ? 0 : Q::NI(TW);
@@ -556,7 +591,12 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
         asm volatile("" ::"v"(af[j]));
       } else {
 #pragma unroll
-        for (int u = 0; u < TW; ++u) acc[i][u] = mma<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[kk][u], acc[i][u]);
+        for (int u = 0; u < TW; ++u) {
+          if constexpr (PT == P_I8)
+            acc[i][u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                __builtin_bit_cast(i32x4, af[j]), __builtin_bit_cast(i32x4, bf[kk][u]), __builtin_bit_cast(i32x4, acc[i][u]), 0, 0, 0));
+          else acc[i][u] = mma<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[kk][u], acc[i][u]);
+        }
       }
       if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], (j + AD) / FM ? a1 : a0);
       if constexpr (j == FM / 2) {   // k-half 1's B fragments, behind the first MFMAs
@@ -606,6 +646,17 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   // epilogue: lane holds C[row 16 i + 4 g + v][col 16 u + r] of the wave's tiles
   const int row0 = m0 + 4 * g;
   const int col0 = cg * BN + wave * 16 * TW;
+  if constexpr (PT == P_I8) {   // exact int32 sums -> f32: times the x row scale and the weight row scale
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      const float ws = p.wscale[min(col0 + 16 * u + rl, p.ntiles * 16 - 1)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          acc[i][u][v] = (float)__builtin_bit_cast(int, acc[i][u][v]) * (p.xscale[min(row0 + 16 * i + v, M - 1)] * ws);
+    }
+  }
 #pragma unroll
   for (int u = 0; u < TW; ++u) {
     const int n = col0 + 16 * u + rl;
@@ -660,7 +711,7 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
   constexpr int NT = 8 * TW;   // T16 tiles per workgroup
   const int n_cg = (p.ntiles + NT - 1) / NT;
   const int n_mb = (p.M + BM - 1) / BM;
-  const int n_stages = p.nsb * 4;
+  const int n_stages = p.nsb * mpk::g3_spb<PT>();
   const int wgs = n_cg * n_mb;
   int nsplit = 1;
   if (EPI == EPI_ATOMIC && allow_split) {
@@ -722,6 +773,7 @@ void launch_gemm3(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_s
     case P_Q4_0: gemm3_pt<P_Q4_0>(epi, p, allow_split, st); break;
     case P_F16: gemm3_pt<P_F16>(epi, p, allow_split, st); break;
     case P_BF16: gemm3_pt<P_BF16>(epi, p, allow_split, st); break;
+    case P_I8: gemm3_pt<P_I8>(epi, p, allow_split, st); break;
   }
 }
 

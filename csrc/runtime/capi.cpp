@@ -182,6 +182,29 @@ int mp_op_gemm3(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
 
 void mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) { set_gemm3_tuning(bm, bn, nsplit, split_wg); }
 
+// int8-activation GEMM prototype (K15): X f16 [M][ldx] -> int8 rows Q [M][ldq] + row scales xs;
+// then Y = xs[m] ws[n] sum_k Q[m][k] W8[n][k] on v_mfma_i32_16x16x64_i8 (W: P_I8 chunks)
+int mp_op_quant_i8(const void* X, int ldx, int M, int K, void* Q, int ldq, void* xs, void* stream) {
+  API_TRY
+  launch_quant_rows_i8((const f16*)X, ldx, M, K, (int8_t*)Q, ldq, (float*)xs, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+int mp_op_gemm3_i8(int epi, const void* W, int ntiles, int nsb, const void* Q, int ldq, int M, void* Y, int ldy,
+                   void* H, int ldh, int n_valid, const void* xs, const void* ws, int allow_split, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)Q; p.ldx = ldq; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  p.xscale = (const float*)xs; p.wscale = (const float*)ws;
+  launch_gemm3(P_I8, epi, p, (hipStream_t)stream, allow_split != 0);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_set_knob(const char* name, int value) {
   API_TRY
   set_knob(name, value);

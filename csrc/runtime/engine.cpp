@@ -297,7 +297,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
-  so.prefill_gemm_v = j.get_int("prefill_gemm_v", 3);
+  so.prefill_gemm_v = j.get_int("prefill_gemm_v", 0);
   so.deterministic = j.get_bool("deterministic", false);
   so.prefill_flash = j.get_bool("prefill_flash", true);
   so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";
@@ -819,6 +819,8 @@ Json Engine::health() const {
   for (auto& w : workers_) {
     Json o = Json::object();
     o["stage"] = w->stage->spec().stage;
+    o["backend"] = w->stage->backend_name();
+    o["device"] = w->device;
     o["items_done"] = (int64_t)w->progress.load();
     if (w->out) {
       o["bytes_sent"] = (int64_t)w->out->bytes_sent;

@@ -645,10 +645,14 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // v2 GEMM (128 rows x 256 columns per workgroup, the decode GEMV's dequant + LDS-shared rows):
   // every shape, f16 weights excepted (they take the 64 x 64 GEMM)
   // v3 GEMM (gemm3.hip: 128|256 x 128|256 workgroup tiles, each weight element dequantized once
-  // per workgroup into LDS): every type, 16-bit weights included
+  // per workgroup, cross-stage MFMA stream): every type, 16-bit weights included
+  // auto (0): v3 for the SwiGLU gate/up and 16-bit weights, v2 for the split-K (ATOMIC) and STORE
+  // shapes -- measured in the 70B mb256 round (profiles/r6h_engine_gemm_v2_v3.txt): gate/up 212 (v3)
+  // vs 249 us (v2), o/down 114 vs 98, qkv 72 vs 69, Q6_K LM head 1162 vs 639
+  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v : (epi == EPI_SWIGLU || is16(m.ptype)) ? 3 : 2;
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
-  const bool v3 = opt_.prefill_gemm_v == 3;
-  const bool v2 = opt_.prefill_gemm_v == 2 && !is16(m.ptype);
+  const bool v3 = gv == 3;
+  const bool v2 = gv == 2 && !is16(m.ptype);
   if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;

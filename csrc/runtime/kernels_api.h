@@ -38,6 +38,9 @@ struct GemvParams {
   float* zero = nullptr;         // side job after the GEMV: zero_n floats cleared
   int64_t zero_n = 0;
   int m_blocks = 1;              // prompt GEMM (launch_gemm2): row blocks of 128 per weight tile group
+  // P_I8 (launch_gemm3): X holds int8 rows (ldx in bytes), y = xscale[m] * wscale[n] * sum(xq * wq)
+  const float* xscale = nullptr;
+  const float* wscale = nullptr;
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
@@ -117,6 +120,8 @@ struct RopeKvParams {
   int kv_fp8 = 0;        // caches hold e4m3 bytes (same element layout, 1 byte each)
 };
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st);
+// int8 rows for the P_I8 GEMM prototype: Q[m][k] = round(X[m][k] / xs[m]), xs[m] = max_k |X[m][k]| / 127
+void launch_quant_rows_i8(const f16* X, int ldx, int M, int K, int8_t* Q, int ldq, float* xs, hipStream_t st);
 
 struct AttnParams {
   const f16* q;          // [M][Hq][Dp]

@@ -54,9 +54,10 @@ MP_HD inline int block_bytes(int t) {
 inline size_t row_bytes(int t, int64_t n) { return (size_t)(n / block_elems(t)) * block_bytes(t); }
 
 // Packed kernel types (what the GEMV/GEMM kernels stream).  F32 weights are packed as F16; BF16
-// weights stay bf16 (P_BF16, same chunk layout as F16): no narrowing at pack time, the kernels
-// widen them on the fly.
-enum PackType : int { P_F16 = 0, P_Q8_0 = 1, P_Q4_K = 2, P_Q5_K = 3, P_Q6_K = 4, P_Q4_0 = 5, P_BF16 = 6 };
+// weights stay bf16 (P_BF16, same chunk layout as F16): no narrowing at pack time, the kernels run
+// the bf16 MFMA on them.  P_I8 is not a GGUF type: per-row int8 re-quantized weights (one f32 scale
+// per output row, kept beside the matrix) for the int8-activation GEMM prototype (gemm3.hip, K15).
+enum PackType : int { P_F16 = 0, P_Q8_0 = 1, P_Q4_K = 2, P_Q5_K = 3, P_Q6_K = 4, P_Q4_0 = 5, P_BF16 = 6, P_I8 = 7 };
 constexpr bool is16(int p) { return p == P_F16 || p == P_BF16; }
 
 inline int pack_type_of(int ggml_type) {
@@ -72,7 +73,7 @@ inline int pack_type_of(int ggml_type) {
 // bytes of one (16-row tile, 256-k super-block) chunk
 constexpr int chunk_bytes(int p) {
   return is16(p) ? 8192 : p == P_Q8_0 ? 4352 : p == P_Q4_K ? 2304 : p == P_Q5_K ? 2816
-       : p == P_Q6_K ? 3360 : p == P_Q4_0 ? 2304 : 0;
+       : p == P_Q6_K ? 3360 : p == P_Q4_0 ? 2304 : p == P_I8 ? 4096 : 0;
 }
 
 inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }

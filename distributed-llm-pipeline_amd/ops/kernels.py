@@ -14,7 +14,7 @@ from .. import _native as N
 from ..utils import quants as Q
 
 EPI_STORE, EPI_ATOMIC, EPI_SWIGLU = 0, 1, 2
-P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0, P_BF16 = 0, 1, 2, 3, 4, 5, 6
+P_F16, P_Q8_0, P_Q4_K, P_Q5_K, P_Q6_K, P_Q4_0, P_BF16, P_I8 = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 def _ptr(t: torch.Tensor | None):
@@ -131,6 +131,59 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
         y = torch.zeros(M, w.n, dtype=torch.float32, device=x.device)
     N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
                y.stride(0), None, 0, w.n if n_valid is None else n_valid, _stream()), "gemm")
+    return y
+
+
+class I8Weight:
+    """Per-row int8 re-quantization of a packed weight for the int8-activation GEMM prototype
+    (SURVEY K15): w8[n][k] = round(w[n][k] / ws[n]), ws[n] = max_k |w[n][k]| / 127, packed into P_I8
+    chunks (csrc/kernels/gemm3.hip W3<P_I8>: byte ((2 st + kk) * 64 + 16 g + r) * 16 + j of chunk
+    (tile t, super-block sb) is row 16 t + r, k = 256 sb + 128 st + 64 kk + 16 g + j)."""
+
+    ptype = P_I8
+
+    def __init__(self, w: PackedWeight):
+        dense = w.unpack().float()
+        n, k = dense.shape
+        self.n, self.k, self.n_pad, self.k_pad, self.ntiles, self.nsb = n, k, w.n_pad, w.k_pad, w.ntiles, w.nsb
+        ws = dense.abs().amax(1).clamp_min(1e-30) / 127.0
+        q = torch.zeros(self.n_pad, self.k_pad, dtype=torch.int8, device=dense.device)
+        q[:n, :k] = torch.round(dense / ws[:, None]).clamp(-127, 127).to(torch.int8)
+        self.ws = torch.ones(self.n_pad, dtype=torch.float32, device=dense.device)
+        self.ws[:n] = ws
+        self.q = q
+        v = q.view(self.ntiles, 16, self.nsb, 2, 2, 4, 16)           # t, r, sb, st, kk, g, j
+        self.dev = v.permute(0, 2, 3, 4, 5, 1, 6).contiguous().view(-1)   # t, sb, st, kk, g, r, j
+
+
+def quant_rows_i8(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """f16 [M][K] -> (int8 [M][K], f32 row scales [M]): q = round(x / s), s = max|x| / 127 per row."""
+    assert x.dtype == torch.float16 and x.is_contiguous()
+    M, K = x.shape
+    q = torch.empty(M, K, dtype=torch.int8, device=x.device)
+    xs = torch.empty(M, dtype=torch.float32, device=x.device)
+    N.check(N.lib().mp_op_quant_i8(_ptr(x), K, M, K, _ptr(q), K, _ptr(xs), _stream()), "quant_i8")
+    return q, xs
+
+
+def gemm_i8(w: I8Weight, x: torch.Tensor | None = None, epi: int = EPI_STORE, y: torch.Tensor | None = None,
+            xq: tuple[torch.Tensor, torch.Tensor] | None = None, allow_split: bool = True) -> torch.Tensor:
+    """int8-activation GEMM prototype: x f16 [M][K_pad] quantized per row (or xq = quant_rows_i8(x)
+    given), v_mfma_i32_16x16x64_i8 against I8Weight, y = xs[m] ws[n] sum_k xq wq (exact int32 sums)."""
+    q, xs = xq if xq is not None else quant_rows_i8(x)
+    assert q.shape[1] == w.k_pad
+    M = q.shape[0]
+    L = N.lib()
+    if epi == EPI_SWIGLU:
+        F = w.n // 2
+        h = torch.zeros(M, F, dtype=torch.float16, device=q.device) if y is None else y
+        N.check(L.mp_op_gemm3_i8(epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(q), w.k_pad, M, None, 0, _ptr(h), h.stride(0),
+                                 F, _ptr(xs), _ptr(w.ws), int(allow_split), _stream()), "gemm_i8")
+        return h
+    if y is None:
+        y = torch.zeros(M, w.n, dtype=torch.float32, device=q.device)
+    N.check(L.mp_op_gemm3_i8(epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(q), w.k_pad, M, _ptr(y), y.stride(0), None, 0,
+                             w.n, _ptr(xs), _ptr(w.ws), int(allow_split), _stream()), "gemm_i8")
     return y
 
 

@@ -34,7 +34,8 @@ def main():
     ap.add_argument("--epi", type=int, default=-1, help="override the epilogue (0 store, 1 atomic): timing probes")
     ap.add_argument("--copies", type=int, default=0, help="weight copies cycled (default: enough to defeat the 256 MiB MALL; 1 = hot)")
     ap.add_argument("--gemm", type=int, default=0,
-                    help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256 per-wave dequant, 3: LDS-shared dequant)")
+                    help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256 per-wave dequant, 3: LDS-shared dequant, "
+                         "8: the int8-activation prototype on per-row int8 weights, gemm3 P_I8)")
     ap.add_argument("--g3", default="0,0,0", help="v3 GEMM tuning BM,BN,nsplit (0 = auto); ';'-separated list sweeps")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=V[,V..]",
                     help="tuning knob (csrc/runtime/tuning.h) swept per shape, e.g. GEMM3_PROBE=0,1,2")
@@ -52,14 +53,22 @@ def main():
             pt = pack_type(qt)
             n_pad, k_pad, ntiles, nsb = packed_dims(qt, n, k)
             nbytes = L.mp_packed_bytes(qt, n, k)
+            if a.gemm == 8:   # int8 weights: 1 byte per element, per-row scales
+                tname, nbytes = "I8", ntiles * nsb * 4096
             copies = a.copies or max(2, min(24, (1536 << 20) // nbytes + 1))
             Ws = []
             for c in range(copies):
+                if a.gemm == 8:
+                    Ws.append(torch.randint(-127, 128, (nbytes,), dtype=torch.int8, device="cuda"))
+                    continue
                 W = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
                 L.mp_init_packed(ctypes.c_void_p(W.data_ptr()), nbytes, pt, 1.0 / k ** 0.5, 7 + c, st())
                 Ws.append(W)
+            ws = torch.full((ntiles * 16,), 1e-3, device="cuda")
             for M in [int(x) for x in a.M.split(",")]:
                 X = torch.randn(M, k_pad, device="cuda").half()
+                Xq = torch.randint(-127, 128, (M, k_pad), dtype=torch.int8, device="cuda")
+                xs = torch.full((M,), 1e-2, device="cuda")
                 Y = torch.zeros(M, n, device="cuda")
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
                 knobs = [[]]
@@ -81,6 +90,13 @@ def main():
                         splits = [int(s) for s in a.splits.split(",")]
                     for nsplit in splits:
                         def run(W):
+                            if a.gemm == 8:
+                                N.check(L.mp_op_gemm3_i8(epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
+                                                         ctypes.c_void_p(Xq.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
+                                                         n, ctypes.c_void_p(H.data_ptr()), n // 2,
+                                                         n if epi != EPI_SWIGLU else n // 2, ctypes.c_void_p(xs.data_ptr()),
+                                                         ctypes.c_void_p(ws.data_ptr()), 1, st()), "gemm3_i8")
+                                return
                             if a.gemm == 3:
                                 N.check(L.mp_op_gemm3(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
                                                       ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
@@ -111,7 +127,17 @@ def main():
                         print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
                                               GBps=round(nbytes / us / 1e3, 1),
                                               TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
-                                              g3=g3 if a.gemm == 3 else None, knobs=dict(kn) or None)), flush=True)
+                                              g3=g3 if a.gemm in (3, 8) else None, knobs=dict(kn) or None)), flush=True)
+                if a.gemm == 8:   # the per-row activation quantization the int8 GEMM needs first
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for i in range(a.iters):
+                        N.check(L.mp_op_quant_i8(ctypes.c_void_p(X.data_ptr()), k_pad, M, k_pad,
+                                                 ctypes.c_void_p(Xq.data_ptr()), k_pad, ctypes.c_void_p(xs.data_ptr()), st()), "q")
+                    e1.record()
+                    torch.cuda.synchronize()
+                    print(json.dumps(dict(shape=sname, op="quant_rows_i8", M=M, us=round(e0.elapsed_time(e1) * 1e3 / a.iters, 2))),
+                          flush=True)
             del Ws
             torch.cuda.empty_cache()
 
