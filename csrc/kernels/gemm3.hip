@@ -651,10 +651,12 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
     for (int u = 0; u < TW; ++u) {
       const float ws = p.wscale[min(col0 + 16 * u + rl, p.ntiles * 16 - 1)];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i) {
+        // whole-vector bit cast: clang's __builtin_bit_cast of one ext_vector element read element 0
+        const i32x4 iv = __builtin_bit_cast(i32x4, acc[i][u]);
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-          acc[i][u][v] = (float)__builtin_bit_cast(int, acc[i][u][v]) * (p.xscale[min(row0 + 16 * i + v, M - 1)] * ws);
+        for (int v = 0; v < 4; ++v) acc[i][u][v] = (float)iv[v] * (p.xscale[min(row0 + 16 * i + v, M - 1)] * ws);
+      }
     }
   }
 #pragma unroll

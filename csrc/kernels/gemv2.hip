@@ -123,10 +123,9 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
           const float4 a = __builtin_bit_cast(float4, xv[sl][j][0]), b = __builtin_bit_cast(float4, xv[sl][j][1]);
           const float4 ga = __builtin_bit_cast(float4, xv[sl][j][2]), gb = __builtin_bit_cast(float4, xv[sl][j][3]);
           if (count) ssn += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
-          v = __builtin_bit_cast(u32x4, half8_t{(f16)(a.x * ga.x), (f16)(a.y * ga.y), (f16)(a.z * ga.z), (f16)(a.w * ga.w),
-                                                (f16)(b.x * gb.x), (f16)(b.y * gb.y), (f16)(b.z * gb.z), (f16)(b.w * gb.w)});
+          v = x8_pack<BF>(a.x * ga.x, a.y * ga.y, a.z * ga.z, a.w * ga.w, b.x * gb.x, b.y * gb.y, b.z * gb.z, b.w * gb.w);
         } else {
-          v = xv[sl][j][0];
+          v = x8_from_h8<BF>(xv[sl][j][0]);   // bf16 weights: the x tile is staged as bf16
         }
         *reinterpret_cast<u32x4*>(&xs[buf][row * G2_LDX + (col ^ x_qswap(row))]) = v;
       }
@@ -158,7 +157,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const half8_t a = x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 8 * s));
+        const half8_t a = *reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 8 * s);
 #pragma unroll
         for (int t = 0; t < TW; ++t) acc[t][mt] = mma<BF>(a, b[t][s], acc[t][mt]);
       }
@@ -168,7 +167,7 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const half8_t a = x_op<BF>(*reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 32 + 8 * s));
+        const half8_t a = *reinterpret_cast<const half8_t*>(xr + mt * 16 * G2_LDX + 32 + 8 * s);
 #pragma unroll
         for (int t = 0; t < TW; ++t) acc[t][mt] = mma<BF>(a, b[t][s], acc[t][mt]);
       }

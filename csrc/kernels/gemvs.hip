@@ -50,7 +50,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   constexpr bool BF = PT == P_BF16;
   constexpr int KSW = GS_NW / G;
   constexpr int NS = NSO ? NSO : is16(PT) ? 2 : 4;   // weight super-blocks in flight per wave
-  extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange]
+  extern __shared__ __attribute__((aligned(16))) f16 xs[];   // [M][krange] (bf16 bits for BF16 weights)
   __shared__ float red[GS_NW][64];
   __shared__ float red_ss[GS_NW][4];
   __shared__ float rs_s[4];
@@ -106,9 +106,8 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
       for (int u = 0; u < 4; ++u) {
         const int c = tid + u * GS_NT;
         if (c < d4 && 4 * c >= k0 && 4 * c < k1) {
-          const half2_t a = {(f16)(v[u].x * sc * gm[u].x), (f16)(v[u].y * sc * gm[u].y)};
-          const half2_t b = {(f16)(v[u].z * sc * gm[u].z), (f16)(v[u].w * sc * gm[u].w)};
-          *reinterpret_cast<u32x2*>(xs + 4 * c - k0) = u32x2{as_u32(a), as_u32(b)};
+          *reinterpret_cast<u32x2*>(xs + 4 * c - k0) =
+              x4_pack<BF>(v[u].x * sc * gm[u].x, v[u].y * sc * gm[u].y, v[u].z * sc * gm[u].z, v[u].w * sc * gm[u].w);
         }
       }
     } else {
@@ -153,9 +152,8 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
           const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
           const float4 ga = *reinterpret_cast<const float4*>(p.gamma + kg), gb = *reinterpret_cast<const float4*>(p.gamma + kg + 4);
           const float sc = rs_s[m];
-          o = __builtin_bit_cast(u32x4, half8_t{(f16)(a.x * sc * ga.x), (f16)(a.y * sc * ga.y), (f16)(a.z * sc * ga.z),
-                                                (f16)(a.w * sc * ga.w), (f16)(b.x * sc * gb.x), (f16)(b.y * sc * gb.y),
-                                                (f16)(b.z * sc * gb.z), (f16)(b.w * sc * gb.w)});
+          o = x8_pack<BF>(a.x * sc * ga.x, a.y * sc * ga.y, a.z * sc * ga.z, a.w * sc * ga.w, b.x * sc * gb.x,
+                          b.y * sc * gb.y, b.z * sc * gb.z, b.w * sc * gb.w);
         }
         *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = o;
       }
@@ -175,7 +173,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + tid + u * GS_NT;
         const int m = c / k8, kl = (c - m * k8) * 8;
-        if (c < tot) *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = v[u];
+        if (c < tot) *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = x8_from_h8<BF>(v[u]);
       }
     }
   }
@@ -192,14 +190,14 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       half8_t a = {};
-      if (xr_ok) a = x_op<BF>(*reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 8 * i));
+      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 8 * i);   // bf16 already for BF
       acc = mma<BF>(a, b[i], acc);
     }
     D::template dequant<1>(ring[s], b, lane, kc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       half8_t a = {};
-      if (xr_ok) a = x_op<BF>(*reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 32 + 8 * i));
+      if (xr_ok) a = *reinterpret_cast<const half8_t*>(xrow + sbl * 256 + 32 + 8 * i);
       acc = mma<BF>(a, b[i], acc);
     }
   };

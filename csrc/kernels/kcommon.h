@@ -36,6 +36,27 @@ __device__ __forceinline__ half8_t x_op(half8_t a) {
   if constexpr (BF) return h8_to_bf8(a);
   else return a;
 }
+// activations staged once per workgroup in the MFMA's A format: f16, or bf16 for BF16 weights
+// (converted from f32 directly where the staging computes them, from f16 where it copies them)
+template <bool BF>
+__device__ __forceinline__ u32x4 x8_pack(float v0, float v1, float v2, float v3, float v4, float v5, float v6, float v7) {
+  if constexpr (BF) return __builtin_bit_cast(u32x4, bf16x8_t{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3, (__bf16)v4,
+                                                               (__bf16)v5, (__bf16)v6, (__bf16)v7});
+  else return __builtin_bit_cast(u32x4, half8_t{(f16)v0, (f16)v1, (f16)v2, (f16)v3, (f16)v4, (f16)v5, (f16)v6, (f16)v7});
+}
+template <bool BF>
+__device__ __forceinline__ u32x2 x4_pack(float v0, float v1, float v2, float v3) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+  if constexpr (BF) return __builtin_bit_cast(u32x2, bf16x4_t{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)v3});
+  else return __builtin_bit_cast(u32x2, half4_t{(f16)v0, (f16)v1, (f16)v2, (f16)v3});
+}
+template <bool BF>
+__device__ __forceinline__ u32x4 x8_from_h8(u32x4 v) {
+  if constexpr (BF) return __builtin_bit_cast(u32x4, h8_to_bf8(__builtin_bit_cast(half8_t, v)));
+  else return v;
+}
+
 template <bool BF>
 __device__ __forceinline__ f32x4 mma(half8_t a, half8_t b, f32x4 c) {
   if constexpr (BF)

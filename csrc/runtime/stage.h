@@ -25,7 +25,7 @@ struct StageOptions {
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
-  int prefill_gemm_v = 0;    // 0: auto (v3 for SwiGLU / 16-bit weights, else v2); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
+  int prefill_gemm_v = 0;    // 0: auto (v2 for quantized, v3 for 16-bit weights); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
   bool prefill_flash = true; // prompt chunks: the LDS-tiled prefill flash attention (attn_prefill.hip)
   bool kv_fp8 = false;       // kv_dtype "fp8": KV pages hold OCP e4m3 bytes
   int kv_pages = 0;          // KV pool pages per stage (64 tokens each; 0: n_slots x max_ctx / 64)

@@ -9,4 +9,5 @@ for mb in 64 256; do for kv in f16 fp8; do
 done; done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/r6g_prof -o run -- python bench.py --steps 10 --warmup 2 --no-secondary \
   --prompt-len 2040 --mb-size 256 > $O/r6g_prof_bench.log 2>&1 || { tail -5 $O/r6g_prof_bench.log; exit 1; }
-echo profiled
+python tools/prof_db_summary.py $O/r6g_prof 3 > $O/r6g_prof_summary.txt && rm -rf $O/r6g_prof   # the db exceeds the copy-back cap
+head -12 $O/r6g_prof_summary.txt

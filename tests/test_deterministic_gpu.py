@@ -24,8 +24,10 @@ def _run(syn, ftype, mb, stages=1, **kw):
         return eng.logits(rows=mb), eng.tokens()
 
 
-@pytest.mark.parametrize("mb", [1, 16, 64])
+@pytest.mark.parametrize("mb", [1, 16, 64, 128, 256])
 def test_deterministic_bitwise_runs_and_pp2(cuda, native, mb):
+    """mb > 64 runs the decode projections on the GEMMs (gemm2 / gemm3): deterministic mode turns
+    their split-K off, so every output element has one writer and a fixed k order."""
     a, ta = _run(WIDE, "Q4_K", mb, deterministic=True)
     b, tb = _run(WIDE, "Q4_K", mb, deterministic=True)
     assert np.array_equal(a, b), float(np.abs(a - b).max())

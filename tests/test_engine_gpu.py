@@ -44,6 +44,43 @@ def test_engine_matches_reference(cuda, native, model_dir, name, ftype):
             assert nmse(lg, rl) < 2e-4, (step, nmse(lg, rl))
 
 
+def test_70b_width_mb256_matches_reference(cuda, native, model_dir):
+    """The headline path at its real widths: a 2-layer Llama-3-70B-width Q4_K
+    model (d 8192, 64 / 8 heads, d_ff 28672), 256 sequences in one micro-batch, so prompt chunks and
+    every decode projection run on the MFMA GEMMs with K = 8192 / 28672 and split-K; logits of
+    sampled rows against the fp32 oracle after the prompt and after two decode rounds."""
+    import os
+    from mipipe.engine import Engine
+    from mipipe.models.config import CONFIGS
+    from mipipe.models.reference import RefLlama
+    from mipipe.models.synthetic import write_synthetic_gguf
+    cfg = CONFIGS["llama3-70b"].scaled(n_layer=2, vocab=4096, name="l70w2")
+    path = os.path.join(str(model_dir), "l70w2-Q4_K.gguf")
+    if not os.path.exists(path):
+        write_synthetic_gguf(path, cfg, "Q4_K", seed=3, fast_random_blocks=True)
+    rng = np.random.default_rng(5)
+    mb = 256
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, int(n))] for n in rng.integers(4, 24, mb)]
+    with Engine(gguf=path, max_ctx=64, n_mb=1, mb_size=mb, prefill_chunk=512) as eng:
+        eng.start(prompts)
+        lg0 = eng.logits(rows=mb)
+        eng.decode(2)
+        lg2 = eng.logits(rows=mb)
+        toks = eng.tokens()
+    ref = RefLlama.from_gguf(path, device="cuda")
+    for r in (0, 1, 77, 128, 200, 255):
+        ref.reset()
+        rl = ref.forward(prompts[r], 0)[-1].float().cpu().numpy()
+        assert nmse(lg0[r], rl) < 2e-4, (r, nmse(lg0[r], rl))
+        pos = len(prompts[r])
+        for t in toks[r][:2]:   # the engine's own tokens (a near-tie flip would only change the path)
+            rl = ref.forward([t], pos)[-1].float().cpu().numpy()
+            pos += 1
+        assert nmse(lg2[r], rl) < 2e-4, (r, nmse(lg2[r], rl))
+    del ref
+    torch.cuda.empty_cache()
+
+
 def _fp8_round(t):
     return t.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(t.dtype)
 
