@@ -9,4 +9,4 @@ for L in libold.so libmipipe.so; do
   MIPIPE_LIB=$L timeout -k 10 300 python3 $R/bench.py --model llama3-8b --mb-size 64 --prompt-len 1024 --steps 10 --warmup 3 > $O/r2r_m64_$L.log 2>&1 || { tail -5 $O/r2r_m64_$L.log; exit 1; }
   echo "8B mb64 1K $L: $(grep -o '"value": [0-9.]*' $O/r2r_m64_$L.log)"
 done
-cd /tmp && bash $R/scripts/ab_lib.sh libold.so libmipipe.so --steps 20 --warmup 5
+cd /tmp && bash $R/scripts/experiments/ab_lib.sh libold.so libmipipe.so --steps 20 --warmup 5

@@ -7,4 +7,4 @@ for G in 1 2; do
   timeout -k 10 300 python3 $R/tools/gemv_bench.py --gemm $G --shapes 70b.gateup,70b.down,70b.qkv,70b.o,8b.gateup,8b.down,8b.qkv --M 512 --iters 6 > $O/gemm_$G.log 2>&1 || { tail -5 $O/gemm_$G.log; exit 1; }
   echo "== gemm v$G"; grep -oE '"shape": "[^"]*"|"us": [0-9.]+|"TFLOPs": [0-9.]+' $O/gemm_$G.log | paste -sd' ' | sed 's/"shape": /\n/g'
 done
-bash $R/scripts/r2u_prof_mb1.sh
+bash $R/scripts/experiments/r2u_prof_mb1.sh

@@ -11,4 +11,4 @@ for T in true false; do
   timeout -k 10 300 python3 bench.py --mb-size 1 --set tail_norm=$T > $O/r3a_70b_$T.log 2>&1 || { tail -5 $O/r3a_70b_$T.log; exit 1; }
   echo "70B mb1 tail_norm=$T $(grep -o '"value": [0-9.]*' $O/r3a_70b_$T.log)"
 done
-bash $R/scripts/prof_mb.sh t8b --model llama3-8b --ftype Q4_K_M --mb-size 1 --steps 30
+bash $R/scripts/experiments/prof_mb.sh t8b --model llama3-8b --ftype Q4_K_M --mb-size 1 --steps 30

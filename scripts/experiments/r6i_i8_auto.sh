@@ -14,4 +14,4 @@ done
 timeout -k 10 400 python bench.py --steps 10 --warmup 2 > $O/r6i_bench_auto.log 2>&1 || { tail -5 $O/r6i_bench_auto.log; exit 1; }
 cat $O/r6i_bench_auto.log | grep '"metric"' | cut -c1-400
 grep -o '"secondary".*' $O/r6i_bench_auto.log
-bash scripts/r6g_long_ctx.sh
+bash scripts/experiments/r6g_long_ctx.sh
