@@ -337,8 +337,10 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restric
   if (acc == 0x9E3779B9u) out[blockIdx.x] = (float)acc;   // keeps the loads; practically never stores
 }
 
-__global__ void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
-  const int i = threadIdx.x;
+// one thread per row of the micro-batch (mb_size up to 1024: a 64-thread single block advanced only
+// rows 0-63, so wide micro-batches decoded rows >= 64 at a frozen position)
+__global__ __launch_bounds__(256) void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < M) { const int p = pos[i] + 1; pos[i] = p; kvlen[i] = p + 1; }
   if (i == 0 && step) step[0] += 1;
 }
@@ -450,7 +452,7 @@ void launch_stream_read(const void* buf, size_t bytes, float* out, hipStream_t s
 }
 
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::advance_kernel, dim3(1), dim3(64), 0, st, pos, kvlen, M, step);
+  hipLaunchKernelGGL(mpk::advance_kernel, dim3((M + 255) / 256), dim3(256), 0, st, pos, kvlen, M, step);
 }
 
 void launch_swiglu(const float* gu, int ld, int F, int M, f16* h, int ldh, hipStream_t st) {

@@ -68,7 +68,7 @@ def test_70b_width_mb256_matches_reference(cuda, native, model_dir):
         lg2 = eng.logits(rows=mb)
         toks = eng.tokens()
     ref = RefLlama.from_gguf(path, device="cuda")
-    for r in (0, 1, 77, 128, 200, 255):
+    for r in (0, 1, 63, 64, 77, 128, 200, 255):
         ref.reset()
         rl = ref.forward(prompts[r], 0)[-1].float().cpu().numpy()
         assert nmse(lg0[r], rl) < 2e-4, (r, nmse(lg0[r], rl))
@@ -222,16 +222,19 @@ def test_microbatch_invariance(cuda, native, model_dir):
 @pytest.mark.parametrize("mb_size", [24, 40, 64, 96, 200])
 def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
     """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment;
-    above 64 rows the decode projections and the LM head run on the prompt GEMM (gemm2)."""
+    above 64 rows the decode projections and the LM head run on the prompt GEMM (gemm2).  Rows on
+    both sides of every 64-row boundary and the last row are compared: a single-block 64-thread
+    position advance once froze rows >= 64 at their prompt position (found by the 70B-width test)."""
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
     rng = np.random.default_rng(mb_size)
     prompts = [[int(t) for t in rng.integers(3, cfg.vocab, size=int(rng.integers(1, 9)))] for _ in range(mb_size)]
+    rows = sorted({0, 1, 2, mb_size - 1} | {r for b in range(64, mb_size, 64) for r in (b - 1, b)})
     with Engine(gguf=path, max_ctx=128) as eng:
-        singles = [eng.generate([p], 6)[0][0] for p in prompts[:6]]
+        singles = [eng.generate([prompts[r]], 6)[0][0] for r in rows]
     with Engine(gguf=path, max_ctx=128, n_mb=1, mb_size=mb_size) as eng:
         o, _ = eng.generate(prompts, 6)
-    assert o[:6] == singles
+    assert [o[r] for r in rows] == singles
 
 
 def test_synthetic_engine_runs(cuda, native):
