@@ -2,6 +2,7 @@
 // (K5+K6 fused), argmax (K12 greedy), decode-step advance, SwiGLU (K8, unfused fallback).
 // All loads/stores of bf16/f16/f32 rows are vectorised (guide Guideline 13).
 #include "kcommon.h"
+#include <stdexcept>
 #include "../runtime/kernels_api.h"
 #include "../runtime/qtypes.h"
 
@@ -24,9 +25,12 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
 // weights, both loaded before anything else so the two reads overlap; the split-K accumulator the
 // next GEMV adds into is cleared by the same launch (16K floats per workgroup) after the loads are
 // in flight.
+// part (optional, d <= 8192 and d % 4 == 0): the residual first absorbs nsplit split-K GEMM partials
+// (part + s * pstride + row * ldp, fixed order) and is written back before the norm (gemm_splitk_store)
 __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
                                                        float eps, f16* out, int ldo, float* zero,
-                                                       int64_t zero_n, int M, const float* bias, int bias_n) {
+                                                       int64_t zero_n, int M, const float* bias, int bias_n,
+                                                       const float* part, int nsplit, int64_t pstride, int ldp) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
@@ -39,6 +43,19 @@ __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, 
       const int i = (tid + 1024 * k) * 4;
       v[k] = i < d ? *reinterpret_cast<const float4*>(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
       ww[k] = i < d ? *reinterpret_cast<const float4*>(w + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (part) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = (tid + 1024 * k) * 4;
+        if (i < d) {
+          for (int sp = 0; sp < nsplit; ++sp) {
+            const float4 a = *reinterpret_cast<const float4*>(part + (size_t)sp * pstride + (size_t)row * ldp + i);
+            v[k].x += a.x; v[k].y += a.y; v[k].z += a.z; v[k].w += a.w;
+          }
+          *reinterpret_cast<float4*>(const_cast<float*>(xr) + i) = v[k];
+        }
+      }
     }
   }
   if (zero && bias) {
@@ -318,6 +335,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   Y[(size_t)m * ldy + j] = acc;
 }
 
+// 4 consecutive columns per thread (n, ldp, ldy multiples of 4)
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ part, int nsplit, int64_t ss, int ldp,
+                                                             int n, float* __restrict__ Y, int ldy) {
+  const int m = blockIdx.y, j = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j >= n) return;
+  float4 acc = *reinterpret_cast<const float4*>(Y + (size_t)m * ldy + j);
+  for (int s = 0; s < nsplit; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)s * ss + (size_t)m * ldp + j);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  *reinterpret_cast<float4*>(Y + (size_t)m * ldy + j) = acc;
+}
+
 __global__ __launch_bounds__(256) void moe_combine_kernel(const float* __restrict__ ys, int lds, int k, int n,
                                                           float* __restrict__ Y, int ldy) {
   const int t = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
@@ -406,7 +436,17 @@ void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f
                     float* zero, int64_t zero_n, hipStream_t st, const float* bias, int bias_n) {
   const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
   hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
-                     zero_n, M, bias, bias_n);
+                     zero_n, M, bias, bias_n, nullptr, 0, 0, 0);
+}
+
+void launch_rmsnorm_acc(float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
+                        float* zero, int64_t zero_n, const float* part, int nsplit, int64_t ss, int ldp, hipStream_t st,
+                        const float* bias, int bias_n) {
+  if ((d & 3) || d > 8192 || (ldx & 3) || (ldp & 3) || (ss & 3))
+    throw std::runtime_error("launch_rmsnorm_acc: needs d <= 8192 and 4-aligned rows");
+  const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
+  hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
+                     zero_n, M, bias, bias_n, part, nsplit, ss, ldp);
 }
 
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,
@@ -438,8 +478,12 @@ void launch_argmax(const float* logits, int ld, int n, int M, int32_t* tokens, h
 
 void launch_splitk_reduce(const float* part, int nsplit, int64_t split_stride, int ldp, int M, int n, float* Y, int ldy,
                           hipStream_t st) {
-  hipLaunchKernelGGL(mpk::splitk_reduce_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, part, nsplit, split_stride,
-                     ldp, n, Y, ldy);
+  if ((n & 3) == 0 && (ldp & 3) == 0 && (ldy & 3) == 0 && (split_stride & 3) == 0)
+    hipLaunchKernelGGL(mpk::splitk_reduce4_kernel, dim3((n / 4 + 255) / 256, M), dim3(256), 0, st, part, nsplit,
+                       split_stride, ldp, n, Y, ldy);
+  else
+    hipLaunchKernelGGL(mpk::splitk_reduce_kernel, dim3((n + 255) / 256, M), dim3(256), 0, st, part, nsplit, split_stride,
+                       ldp, n, Y, ldy);
 }
 
 void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, float* Y, int ldy, hipStream_t st) {

@@ -447,6 +447,25 @@ void HipStage::alloc_runtime() {
     pf_opart_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * Dp_ * 4);
     pf_ml_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * 2 * 4);
   }
+  if (opt_.gemm_splitk_store && opt_.prefill_gemm) {
+    // split-K partials of the M > 64 GEMMs (decode micro-batches and prompt chunks wider than 64 rows)
+    size_t need = 0;
+    auto acc = [&](const PackedMat& m) {
+      if (!m.d || is16(m.ptype)) return;
+      for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
+        if (M <= 64) continue;
+        const int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
+        if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
+      }
+    };
+    for (const LayerW& L : layers_) {
+      for (const MatSeg& sg : L.qkv) acc(sg.m);
+      acc(L.wo);
+      acc(L.down);
+    }
+    if (need) sk_part_ = (float*)dmalloc(need * 4);
+    sk_part_n_ = need;
+  }
   if (opt_.deterministic) {
     // fixed-order split-K: the largest nsplit x rows x N of any ATOMIC GEMV call (<= 64 rows each)
     size_t need = 0;
@@ -660,7 +679,20 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
     if (v3) launch_gemm3(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
-    else if (v2) launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+    else if (v2) {
+      // split-K partial stores + a fixed-order reduction (gemm_splitk_store; into the residual x it
+      // is deferred to the next RMSNorm, norm_x) or float atomics into Y
+      // (fixed-order: also the deterministic mode's split-K, which otherwise runs unsplit)
+      const bool sk = opt_.gemm_splitk_store && sk_part_ && epi == EPI_ATOMIC && allow_split;
+      const bool defer = sk && Y == sk_defer_;
+      if (sk) flush_sk(st);   // the scratch is about to be overwritten
+      int ns = 0;
+      if (sk && launch_gemm2_splitk(m.ptype, p, sk_part_, sk_part_n_, st, !defer, &ns)) {
+        if (defer) sk_pend_ = SkPending{Y, M, n_valid, ldy, ns, p.ntiles * 16, (int64_t)M * p.ntiles * 16};
+      } else {
+        launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+      }
+    }
     else launch_gemm(m.ptype, epi, p, st);
     return;
   }
@@ -696,6 +728,25 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     }
     launch_gemv(m.ptype, epi, p, nsplit, st);
   }
+}
+
+void HipStage::flush_sk(hipStream_t st) {
+  if (!sk_pend_.x) return;
+  launch_splitk_reduce(sk_part_, sk_pend_.ns, sk_pend_.ss, sk_pend_.ldp, sk_pend_.M, sk_pend_.n, sk_pend_.x, sk_pend_.ldy, st);
+  sk_pend_ = SkPending{};
+}
+
+void HipStage::norm_x(float* x, const float* w, int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias,
+                      int bias_n) {
+  const int d = cfg_.d_model;
+  if (sk_pend_.x == x && sk_pend_.M == M && sk_pend_.n == d && sk_pend_.ldy == d && d <= 8192 && (d & 3) == 0) {
+    launch_rmsnorm_acc(x, d, w, d, cfg_.eps, xn_, Kd_, M, zero, zero_n, sk_part_, sk_pend_.ns, sk_pend_.ss, sk_pend_.ldp,
+                       st, bias, bias_n);
+    sk_pend_ = SkPending{};
+    return;
+  }
+  flush_sk(st);
+  launch_rmsnorm(x, d, w, d, cfg_.eps, xn_, Kd_, M, zero, zero_n, st, bias, bias_n);
 }
 
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
@@ -810,7 +861,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
       gemv(s.m, EPI_ATOMIC, nullptr, 0, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st, &e);
     }
   } else {
-    launch_rmsnorm(x, d, L.attn_norm, d, cfg_.eps, xn_, Kd_, M, qkv_, (int64_t)M * qkv_n_, st, L.qkv_bias, qkv_n_);
+    norm_x(x, L.attn_norm, M, qkv_, (int64_t)M * qkv_n_, st, L.qkv_bias, qkv_n_);
     for (const MatSeg& s : L.qkv)
       gemv(s.m, EPI_ATOMIC, xn_, Kd_, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N, true, st);
   }
@@ -820,14 +871,15 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     z.zero = ssq_; z.zero_n = 64 + (int64_t)M * qkv_n_;
     gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st, &z);
   } else {
+    sk_defer_ = x;
     gemv(L.wo, EPI_ATOMIC, attn_, Ko_, M, x, d, nullptr, 0, d, true, st);
+    sk_defer_ = nullptr;
     if (opt_.fused_norm && li + 1 == (int)layers_.size())
       HIP_OK(hipMemsetAsync(ssq_, 0, (64 + (size_t)M * qkv_n_) * 4, st));
   }
   const bool ffn_fused = small && !L.moe;
   // MoE: the same launch clears the router logits, which the router GEMV then accumulates split-K
-  if (!ffn_fused)
-    launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
+  if (!ffn_fused) norm_x(x, L.ffn_norm, M, L.moe ? moe_logits_ : nullptr, L.moe ? (int64_t)M * 64 : 0, st);
   if (L.moe) {
     moe_ffn(L, M, st, x);
     return;
@@ -844,7 +896,9 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     gemv(L.up, EPI_STORE, xin, Kd_, M, gu_ + F, 2 * F, nullptr, 0, F, false, st, fe);
     launch_swiglu(gu_, 2 * F, F, M, h_, Kff_, st);
   }
+  sk_defer_ = x;   // absorbed by the next layer's attention norm (or flushed after the last layer)
   gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
+  sk_defer_ = nullptr;
 }
 
 void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
@@ -1002,6 +1056,7 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
   segs_ = &segs;
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, T, x, pf_pos_, pf_kvlen_, pf_slot_, false, st);
+  flush_sk(st);
   segs_ = nullptr;
   if (spec_.last() && !segs.empty() && segs[0].verify) {
     // speculative verification: LM head over every row of the chunk, greedy next token per row
@@ -1047,6 +1102,7 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
     launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tok_[mb], B, x, cfg_.d_model, st);
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
+  flush_sk(st);
   if (spec_.last()) head(mb, B, x, tok_[mb], (uint64_t)mb + 1, st);
   launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
 }

@@ -135,6 +135,10 @@ class HipStage : public Stage {
                   float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st);
   size_t kv_eb() const { return opt_.kv_fp8 ? 1 : 2; }   // bytes per cached K/V element
   int det_splits(int ntiles, int nsb, int M, int epi, bool allow_split = true) const;   // RMSNorm folded into the consuming GEMVs at this row count
+  void flush_sk(hipStream_t st);
+  // RMSNorm of the residual x into xn_ (absorbing pending split-K partials of x first)
+  void norm_x(float* x, const float* w, int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias = nullptr,
+              int bias_n = 0);
   void gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, float* Y, int ldy, f16* H, int ldh,
             int n_valid, bool allow_split, hipStream_t st,
             const GemvParams* extras = nullptr);
@@ -189,6 +193,12 @@ class HipStage : public Stage {
   float* gu_ = nullptr;   // unfused gate|up f32
   float* logits_ = nullptr; int logits_ld_ = 0;
   ArgmaxScratch am_{nullptr, nullptr, 0};   // two-level argmax partials / arrival counters
+  float* sk_part_ = nullptr; size_t sk_part_n_ = 0;   // gemm_splitk_store: per-split GEMM partials
+  // split-K partials of the last o / down GEMM not yet added into the residual x: the next RMSNorm
+  // of x absorbs them (norm_x), anything else reading x first calls flush_sk
+  struct SkPending { float* x = nullptr; int M = 0, n = 0, ldy = 0, ns = 0, ldp = 0; int64_t ss = 0; };
+  SkPending sk_pend_;
+  float* sk_defer_ = nullptr;   // gemv(): ATOMIC GEMMs into this buffer defer their reduction
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
   int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
   // MoE scratch

@@ -80,6 +80,14 @@ void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
 // dequantized weight fragment, two 16-column tiles per wave, 256 columns x 128 rows per 8-wave
 // workgroup, whole K per workgroup); EPI_ATOMIC adds into Y (single writer per element)
 // (EPI_ATOMIC: split-K over workgroups when there are few output tiles, unless allow_split is false)
+// split-K factor gemm2 uses for a splittable (ATOMIC) launch of this shape
+int gemm2_splits(int ntiles, int nsb, int M);
+// gemm2 split-K through per-split partial stores + a fixed-order reduction into Y (no atomics);
+// false = not applicable (no split, 16-bit weights, scratch too small): nothing was launched
+// reduce = false: the partials are left in scratch ([nsplit][M][ntiles * 16], *nsplit_out splits)
+// for the consumer to absorb (launch_rmsnorm_acc)
+bool launch_gemm2_splitk(int ptype, GemvParams p, float* scratch, size_t scratch_n, hipStream_t st,
+                         bool reduce = true, int* nsplit_out = nullptr);
 void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
 // Prompt / wide-decode GEMM v3 (gemm3.hip): BM x BN = {128, 256} x {128, 256} workgroup tiles, each
 // weight element dequantized once per workgroup into an f16 LDS image shared by its 8 waves,
@@ -98,7 +106,11 @@ void launch_splitk_reduce(const float* part, int nsplit, int64_t split_stride, i
 // split-K accumulator of the next GEMV starts at the projection bias: Qwen2 q/k/v biases)
 void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo,
                     int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias = nullptr, int bias_n = 0);
-// same but f32 output (final norm before LM head may use f16 as well)
+// launch_rmsnorm that first adds nsplit split-K partials (part + s * ss + row * ldp) into x and
+// writes x back (gemm_splitk_store: the deferred reduction of the o / down GEMMs into the residual)
+void launch_rmsnorm_acc(float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
+                        float* zero, int64_t zero_n, const float* part, int nsplit, int64_t ss, int ldp, hipStream_t st,
+                        const float* bias = nullptr, int bias_n = 0);
 
 // embedding gather + dequant of raw GGUF rows -> x f32 [M][ldx]
 void launch_embed(int ggml_type, const uint8_t* table, int64_t row_bytes, int d, const int32_t* tokens,

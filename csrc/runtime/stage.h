@@ -25,6 +25,8 @@ struct StageOptions {
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
+  bool gemm_splitk_store = true;   // M > 64 split-K GEMMs: per-split partial stores + a fixed-order reduction
+                                   // (into the residual: absorbed by the next RMSNorm) instead of float atomics
   int prefill_gemm_v = 0;    // 0: auto (v2 for quantized, v3 for 16-bit weights); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
   bool prefill_flash = true; // prompt chunks: the LDS-tiled prefill flash attention (attn_prefill.hip)
   bool kv_fp8 = false;       // kv_dtype "fp8": KV pages hold OCP e4m3 bytes

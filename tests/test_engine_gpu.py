@@ -237,6 +237,24 @@ def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
     assert [o[r] for r in rows] == singles
 
 
+def test_wide_microbatches_pipelined_match_single(cuda, native, model_dir):
+    """The bench.py layout at PP > 1 (N + 1 micro-batches of > 64 rows circulating through the
+    ring), emulated with two stages on one GPU: rows on both sides of the 64-row boundary of both
+    micro-batches against one sequence at a time."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(144)
+    mb = 72
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, size=int(rng.integers(1, 9)))] for _ in range(2 * mb)]
+    rows = [0, 63, 64, mb - 1, mb, mb + 63, mb + 64, 2 * mb - 1]
+    with Engine(gguf=path, max_ctx=64) as eng:
+        singles = [eng.generate([prompts[r]], 5)[0][0] for r in rows]
+    with Engine(gguf=path, max_ctx=64, n_mb=2, mb_size=mb, stages=2, devices=[0, 0], link="local",
+                split="even") as eng:
+        o, _ = eng.generate(prompts, 5)
+    assert [o[r] for r in rows] == singles
+
+
 def test_synthetic_engine_runs(cuda, native):
     from mipipe.engine import Engine
     syn = dict(n_layer=2, d_model=1024, n_head=8, n_head_kv=2, d_ff=2816, vocab=4096)

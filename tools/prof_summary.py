@@ -42,6 +42,18 @@ def main():
           f"gaps {(wall - tot) / nr:.1f} us/round, {len(sel) / nr:.0f} kernels/round")
     for k, v in sorted(busy.items(), key=lambda kv: -kv[1]):
         print(f"{v / nr:9.1f} us/round  {cnt[k] // nr:4d}/round  avg {v / cnt[k]:7.2f} us  {k}")
+    # one layer's worth of the last round in dispatch order: duration and the gap before each kernel
+    last = rows[idx[-2] + 1: idx[-1] + 1]
+    n_show = int(os.environ.get("PROF_SEQ", "14"))
+    if n_show > 0:
+        print(f"\n# dispatch order, middle of the last round ({n_show} kernels): gap-before / duration us")
+        mid = max(0, len(last) // 2 - n_show // 2)
+        prev_end = int(last[mid - 1]["End_Timestamp"]) if mid > 0 else None
+        for r in last[mid: mid + n_show]:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
+            prev_end = e
+            print(f"  {gap:6.2f} {((e - s) / 1e3):8.2f}  {r['Kernel_Name'].split('(')[0][:80]}")
 
 
 if __name__ == "__main__":
