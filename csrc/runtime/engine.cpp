@@ -403,6 +403,7 @@ Engine::~Engine() {
       continue;
     }
     (void)hipSetDevice(w->device);
+    if (bcast_dev_ && w.get() == workers_[0].get()) (void)hipFree(bcast_dev_);
     for (void* p : w->wire_out) (void)hipFree(p);
     for (void* p : w->wire_in) (void)hipFree(p);
     for (auto e : w->comp_ev) (void)hipEventDestroy(e);
@@ -868,6 +869,44 @@ Json Engine::failover_config(const Json& cfg, const Json& health) {
   MP_LOGW("failover: stage %d (device %d) lost; re-partitioning over %d stage(s)", bad,
           health.get_int("failed_device", -1), S - 1);
   return c;
+}
+
+// The links are idle between run_all calls (every item's sends were matched by the peer's
+// receives, and sync_all drained the streams), so this pass cannot interleave with pipeline traffic.
+void Engine::ring_bcast_from_last(std::vector<int32_t>& v) {
+  if (mode_ != "mp" || S_ == 1 || v.empty()) return;
+  Worker& w = *workers_[0];
+  const int s = w.stage->spec().stage;
+  const size_t bytes = v.size() * 4;
+  const bool last = s == S_ - 1, fwd = s < S_ - 2;
+  if (cpu_) {
+    if (last) {
+      w.out->send(v.data(), bytes, nullptr);
+    } else {
+      w.in->recv(v.data(), bytes, nullptr);
+      if (fwd) w.out->send(v.data(), bytes, nullptr);
+    }
+    return;
+  }
+  HIP_OK(hipSetDevice(w.device));
+  if (bcast_cap_ < v.size()) {
+    if (bcast_dev_) HIP_OK(hipFree(bcast_dev_));
+    HIP_OK(hipMalloc(&bcast_dev_, bytes));
+    bcast_cap_ = v.size();
+  }
+  if (last) {
+    HIP_OK(hipMemcpy(bcast_dev_, v.data(), bytes, hipMemcpyHostToDevice));
+    w.out->send(bcast_dev_, bytes, w.send_st);
+    HIP_OK(hipStreamSynchronize(w.send_st));
+  } else {
+    w.in->recv(bcast_dev_, bytes, w.recv_st);
+    HIP_OK(hipStreamSynchronize(w.recv_st));
+    HIP_OK(hipMemcpy(v.data(), bcast_dev_, bytes, hipMemcpyDeviceToHost));
+    if (fwd) {
+      w.out->send(bcast_dev_, bytes, w.send_st);
+      HIP_OK(hipStreamSynchronize(w.send_st));
+    }
+  }
 }
 
 void Engine::sync_all() {
@@ -1445,7 +1484,11 @@ static std::vector<int32_t> lookup_draft(const std::vector<int32_t>& ctx, int k,
 // for rejected draft positions are overwritten by the next chunk (attention reads [0, kvlen)).
 Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int n_predict, int draft_max,
                            int ngram, std::vector<std::vector<int32_t>>* out) {
-  if ((int)workers_.size() != S_) throw std::runtime_error("speculative decoding needs every stage in this process");
+  // one process per stage (mode "mp"): every rank runs this same loop; the last stage's tokens
+  // reach the other ranks over the ring after each verify pass (ring_bcast_from_last), so every rank
+  // drafts, grants KV and builds the identical next verify chunk
+  const bool mp = mode_ == "mp" && S_ > 1;
+  if (!mp && (int)workers_.size() != S_) throw std::runtime_error("speculative decoding needs every stage in this process");
   if (jcfg_.get_num("temp", 0.0) > 0.0) throw std::runtime_error("speculative decoding is greedy (temp 0)");
   if (jcfg_.get_num("repeat_penalty", 1.0) != 1.0 || jcfg_.get_num("frequency_penalty", 0.0) != 0.0 ||
       jcfg_.get_num("presence_penalty", 0.0) != 0.0)
@@ -1466,6 +1509,14 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
   slot_toks_.clear();   // the verify chunks write draft rows past the accepted tokens
   const double t1 = now_ms();
   const size_t n = prompts.size();
+  if (mp) {   // the first token of every sequence is known where the last stage lives
+    std::vector<int32_t> ft(n, 0);
+    if (owns_last())
+      for (size_t i = 0; i < n; ++i) ft[i] = gen_[i][0];
+    ring_bcast_from_last(ft);
+    if (!owns_last())
+      for (size_t i = 0; i < n; ++i) gen_[i].assign(1, ft[i]);
+  }
   if (on_token)
     for (size_t i = 0; i < n; ++i) on_token((int)i, gen_[i][0]);
   std::vector<std::vector<int32_t>> ctx(n);
@@ -1493,8 +1544,10 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
         chunk[i].insert(chunk[i].end(), d.begin(), d.end());
         kv_grant(i, pos + (int)chunk[i].size());
         drafted += (long)d.size();
-        if (cpu_) std::memcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4);
-        else {
+        if (!wf) {
+        } else if (cpu_) {
+          std::memcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4);
+        } else {
           HIP_OK(hipSetDevice(wf->device));
           HIP_OK(hipMemcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4,
                            hipMemcpyHostToDevice));
@@ -1510,9 +1563,24 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
     kv_sync();
     run_all(items);
     ++rounds;
+    // the target's greedy token after every verify row, all items back to back
+    size_t n_rows = 0;
+    for (const Item& it : items) n_rows += (size_t)it.T;
+    if (vt.size() < n_rows) vt.resize(n_rows);
+    std::vector<int32_t> all(n_rows, 0);
+    if (wl) {
+      size_t off = 0;
+      for (const Item& it : items) {
+        if (!cpu_) HIP_OK(hipSetDevice(wl->device));
+        wl->stage->copy_verify_tokens(it.mb, all.data() + off, it.T);
+        off += (size_t)it.T;
+      }
+    }
+    if (mp) ring_bcast_from_last(all);
+    size_t off = 0;
     for (const Item& it : items) {
-      if (!cpu_) HIP_OK(hipSetDevice(wl->device));
-      wl->stage->copy_verify_tokens(it.mb, vt.data(), it.T);
+      std::copy(all.begin() + off, all.begin() + off + it.T, vt.begin());
+      off += (size_t)it.T;
       int row = 0;
       for (const PrefillSeg& sg : it.segs) {
         const size_t i = (size_t)it.mb * B_ + sg.b;

@@ -145,6 +145,9 @@ class Engine {
   void run_all(const std::vector<Item>& items);
   void post_ring_recv(Worker& w, int mb);
   void sync_all();
+  // multi-process pipeline: the last stage's host vector (same length on every rank) reaches every
+  // rank over the idle ring (S-1 -> 0 -> 1 -> .. -> S-2); no-op in local mode
+  void ring_bcast_from_last(std::vector<int32_t>& v);
 
   Json jcfg_;
   ModelConfig cfg_;
@@ -172,6 +175,8 @@ class Engine {
   int rounds_cap_ = 0, rounds_done_ = 0;
   bool started_ = false;
   bool resumable_ = true;   // false after spec_generate (per-sequence positions)
+  int32_t* bcast_dev_ = nullptr;   // ring_bcast_from_last device staging (RCCL / device links)
+  size_t bcast_cap_ = 0;
   // prefix cache (config "prefix_cache", default on): per slot, the tokens its KV holds; start()
   // prefills only what follows the common prefix (multi-turn chat re-sends the whole history)
   bool prefix_cache_ = true;

@@ -343,6 +343,44 @@ def test_multiprocess_pipeline_one_gpu_tcp(cuda, native, model_dir):
     assert last and json.loads(last[0][4:]) == ref_out
 
 
+_MP_SPEC_SCRIPT = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+import torch
+from mipipe.engine import Engine
+cfg = json.loads(sys.argv[1])
+with Engine(**cfg) as eng:
+    out, st = eng.spec_generate({prompts!r}, 10, draft_max=4, ngram=2)
+    print("OUT " + json.dumps(dict(out=out, stats=st)), flush=True)
+"""
+
+
+def test_spec_generate_multiprocess_hip_stages(cuda, native, model_dir):
+    """Speculative decoding with one process per HIP stage (two ranks on the box's GPU, TCP links):
+    the verify tokens cross the ring from device staging buffers; both ranks return single-process
+    greedy output."""
+    import json, socket, subprocess, sys
+    from conftest import REPO
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    prompts = [[5, 6, 7, 8, 5, 6, 7, 8, 5, 6], [9, 10, 11, 9, 10, 11, 9], [20, 21, 22, 23, 20, 21], [40, 41, 40, 41]]
+    with Engine(gguf=path, max_ctx=64, n_mb=2, mb_size=2, prefill_chunk=32) as eng:
+        ref_out, _ = eng.generate(prompts, 10)
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    script = _MP_SPEC_SCRIPT.format(repo=REPO, prompts=prompts)
+    procs = []
+    for r in range(2):
+        c = dict(gguf=path, mode="mp", world=2, rank=r, device=0, link="tcp", base_port=port,
+                 max_ctx=64, n_mb=2, mb_size=2, prefill_chunk=32, split="even")
+        procs.append(subprocess.Popen([sys.executable, "-c", script, json.dumps(c)], stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, cwd=REPO))
+    for p in procs:
+        o, _ = p.communicate(timeout=300)
+        assert p.returncode == 0, o[-3000:]
+        d = json.loads([l for l in o.splitlines() if l.startswith("OUT ")][-1][4:])
+        assert d["out"] == ref_out and d["stats"]["verify_rounds"] >= 1
+
+
 @pytest.mark.parametrize("name", ["tiny-gqa", "stories15m"])
 def test_fused_decode_attention_matches_unfused(cuda, native, model_dir, name):
     """Fused RoPE + KV append + split-K attention + last-arriver merge == the three-kernel path,

@@ -153,3 +153,49 @@ def test_elastic_checkpoint_of_another_run_is_ignored(native, model_dir, tmp_pat
     out = E.generate_elastic(prompts, 9, str(root), every=4, **kw)
     assert out == ref
     assert (root / "replica0" / "round_00000004").exists()   # another run's checkpoint is left alone
+
+
+_SPEC = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+from mipipe.parallel import init_from_torchrun
+import torch.distributed as dist
+eng = init_from_torchrun(pp={pp}, gguf={path!r}, backend="cpu", max_ctx=128, n_mb=2, mb_size=2, prefill_chunk=32,
+                         split="even", base_port={port})
+out, st = eng.spec_generate({prompts!r}, {n}, draft_max=4, ngram=2)
+eng.close()
+dist.barrier()
+print("OUT " + json.dumps(dict(rank=dist.get_rank(), out=out, stats=st)), flush=True)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("pp", [2, 3])
+def test_spec_generate_across_processes(native, model_dir, tmp_path, pp):
+    """Speculative decoding (prompt lookup) with one process per stage: after every verify pass the
+    last stage's tokens travel the ring to every rank, so all ranks draft the same next chunk; every
+    rank's output equals single-process greedy decoding (SURVEY.md D10, the design report's
+    distributed speculative decoding, PDF p.12)."""
+    from mipipe.engine import Engine
+    from test_engine_cpu import free_port
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    # repetitive prompts so lookup drafts exist (the acceptance itself depends on the model)
+    prompts = [[5, 6, 7, 8, 5, 6, 7, 8, 5, 6], [9, 10, 11, 9, 10, 11, 9], [20, 21, 22, 23, 20, 21], [40, 41, 40, 41]]
+    n = 10
+    with Engine(gguf=path, backend="cpu", max_ctx=128, n_mb=2, mb_size=2, prefill_chunk=32) as eng:
+        ref, _ = eng.generate(prompts, n)
+    script = tmp_path / "spec.py"
+    script.write_text(_SPEC.format(repo=REPO, path=path, prompts=prompts, n=n, port=free_port(), pp=pp))
+    mport = free_port()
+    procs = []
+    for r in range(pp):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(pp), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(mport), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+        d = json.loads([l for l in o.splitlines() if l.startswith("OUT ")][-1][4:])
+        assert d["out"] == ref, (d["rank"], d["out"], ref)
+        assert d["stats"]["verify_rounds"] >= 1 and d["stats"]["drafted"] >= 1
