@@ -9,10 +9,12 @@
 // (O^T = V^T P^T, A = V^T read from the transposed V page) -- no LDS round trip, no shuffles for P.
 // Online softmax in registers; 4 waves interleave chunks and are merged through LDS; splits are
 // merged by attn_combine (LSE merge).  KV pages hold 64 tokens: K [64][Dp], V^T [Dp][64].
+#include <stdexcept>
 #include <type_traits>
 #include "../runtime/tuning.h"
 
 #include "kcommon.h"
+#include "dequant.h"
 #include "../runtime/kernels_api.h"
 
 namespace mpk {
@@ -211,8 +213,11 @@ constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
 // PF: each wave loads its next chunk before the current chunk's math (short contexts: one split,
 // latency-bound); without it the kernel needs ~40 % fewer VGPRs (occupancy 3 instead of 2), which
 // the many-split long contexts need more (8B 32K mb8: 1019 vs 960 tok/s)
+// (t, kvh, z): token, kv head, KV split.  xo (LDS, one split only): the G heads' outputs of token
+// t land there, [r * hd + d], instead of p.out (the fused attention + o-projection kernel)
 template <int DP, bool F8, bool PF>
-__device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p) {
+__device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
+                                                 f16* xo = nullptr) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
   auto cvt = [](const KR& r) -> half8_t {
     if constexpr (F8) return f8x8_to_h8(r);
@@ -227,7 +232,6 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q4 = lane >> 4, col = lane & 15;
-  const int t = blockIdx.x, kvh = blockIdx.y, z = blockIdx.z;
   const int G = p.Hq / p.Hkv;
   const int g = col;
   const bool rvalid = col < G;
@@ -536,7 +540,11 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p) {
     const int hh = kvh * G + r;
     const size_t rid = (size_t)t * p.Hq + hh;
     if (n_act == 1) {
-      if (d < p.hd) p.out[(size_t)t * p.ldo + hh * p.hd + d] = (f16)(L > 0.f ? O / L : 0.f);
+      if (d < p.hd) {
+        const f16 v = (f16)(L > 0.f ? O / L : 0.f);
+        if (xo) xo[r * p.hd + d] = v;
+        else p.out[(size_t)t * p.ldo + hh * p.hd + d] = v;
+      }
     } else {
       st_sc1(p.o_part + ((size_t)z * stride + rid) * DP + d, O);
       if (d == 0) {
@@ -606,12 +614,91 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p) {
 }
 
 template <int DP, bool F8>
-__global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) { attn_decode_body<DP, F8, true>(p); }
+__global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
+  attn_decode_body<DP, F8, true>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+}
 // many-split long contexts: 3 workgroups per CU (occupancy, not per-wave latency, is what they need)
 template <int DP, bool F8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_decode_kernel_np(
     const DecodeAttnParams p) {
-  attn_decode_body<DP, F8, false>(p);
+  attn_decode_body<DP, F8, false>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// global -> LDS DMA, 16 B per active lane to (wave-uniform LDS base) + lane * 16 (gemm3.hip glds;
+// inline asm so the compiler's waitcnt pass does not drain it at the next ds_read)
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+// Fused single-stream decode attention + output projection (one launch instead of two: the o GEMV
+// of one token is bound by its launch and ramp, ~5.6 us for 9 MB at 8B, not by its bytes).
+//   workgroup (r, kvh), grid (ntiles / TPW, Hkv):
+//   1. LDS-DMA of its W_o slice: output tiles [r TPW, r TPW + TPW) x the KS super-blocks of k that
+//      kv head kvh's G query heads feed (k in [kvh G hd, (kvh + 1) G hd)); in flight during 2.
+//   2. the attention of kv head kvh for every token (one split; the R = ntiles / TPW workgroups of
+//      a head each compute it: short contexts only, the host gates on max_ctx), outputs to LDS.
+//   3. split-K GEMV of the slice on MFMA (the decode GEMV's dequant), atomics into the residual:
+//      Hkv partial sums per output (not bitwise reproducible: the deterministic mode keeps the
+//      two-kernel path).
+template <int DP, bool F8, int PT, int TPW, int KS>
+__global__ __launch_bounds__(256) void attn_o_kernel(const DecodeAttnParams p, const AttnOParams o) {
+  using D = Deq<PT>;
+  constexpr int CB = D::CB, TB = KS * CB, WB = TPW * TB;
+  static_assert(TB % 16 == 0, "attn_o: 16-B DMA pieces");
+  __shared__ __attribute__((aligned(16))) uint8_t wl[WB];
+  __shared__ __attribute__((aligned(16))) f16 xo[4][KS * 256];
+  const int r = blockIdx.x, kvh = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile0 = r * TPW, sb0 = kvh * KS;
+  constexpr int NI = (WB + 1023) / 1024;
+  for (int i = wave; i < NI; i += 4) {
+    const int off = i * 1024 + lane * 16;
+    if (off < WB) {
+      const int u = off / TB, rem = off - u * TB;
+      const int tile = min(tile0 + u, o.ntiles - 1);
+      glds16(o.W + ((size_t)tile * o.nsb + sb0) * CB + rem, wl + i * 1024);
+    }
+  }
+  const int M = p.M;
+  for (int t = 0; t < M; ++t) {
+    attn_decode_body<DP, F8, true>(p, t, kvh, 0, &xo[t][0]);
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const Consts kc = make_consts();
+  const int g = lane >> 4, m = lane & 15;
+  for (int u = wave; u < TPW; u += 4) {
+    const int tile = tile0 + u;
+    if (tile >= o.ntiles) break;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      typename D::Raw raw;
+      D::load(raw, LdsSrc{wl + (u * KS + s) * CB}, lane);
+      half8_t b[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 0) D::template dequant<0>(raw, b, lane, kc);
+        else D::template dequant<1>(raw, b, lane, kc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          half8_t a = {};
+          if (m < M) a = *reinterpret_cast<const half8_t*>(&xo[m][s * 256 + t16_xoff(g, 4 * h + i)]);
+          acc = mma<false>(a, b[i], acc);
+        }
+      }
+    }
+    // lane holds C[token 4g + v][output 16 tile + m]
+    const int n = tile * 16 + m;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int t = 4 * g + v;
+      if (t < M && n < o.n_valid) unsafeAtomicAdd(o.Y + (size_t)t * o.ldy + n, acc[v]);
+    }
+  }
 }
 
 }  // namespace mpk
@@ -645,6 +732,34 @@ static void attn_decode_go(const DecodeAttnParams& p, hipStream_t st) {
   } else {
     if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel_np<128, F8>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((mpk::attn_decode_kernel_np<64, F8>), grid, dim3(256), 0, st, p);
+  }
+}
+
+constexpr int kAttnOTpw = 8;   // output tiles per workgroup: 8B's W_o -> 32 x 8 = 256 workgroups
+
+static int attn_o_ks(const DecodeAttnParams& p) { return (p.Hq / p.Hkv) * p.hd / 256; }
+
+bool attn_o_supported(const DecodeAttnParams& p, const AttnOParams& o) {
+  const int G = p.Hq / p.Hkv;
+  if (p.M < 1 || p.M > 4 || p.Dp != 128 || p.hd != 128 || p.ssq || p.n_split != 1) return false;
+  if (G * p.hd % 256 || attn_o_ks(p) != 2 || o.ntiles % kAttnOTpw) return false;
+  if (o.ptype != P_Q4_K && o.ptype != P_Q6_K && o.ptype != P_Q8_0) return false;
+  // one round of workgroups (LDS ~100 KB: one per CU)
+  return o.ntiles / kAttnOTpw * p.Hkv <= 256;
+}
+
+template <bool F8, int PT>
+static void attn_o_go(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {
+  const dim3 grid(o.ntiles / kAttnOTpw, p.Hkv);
+  hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2>), grid, dim3(256), 0, st, p, o);
+}
+
+void launch_attn_o(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {
+  if (!attn_o_supported(p, o)) throw std::runtime_error("launch_attn_o: unsupported shape");
+  switch (o.ptype) {
+    case P_Q4_K: return p.kv_fp8 ? attn_o_go<true, P_Q4_K>(p, o, st) : attn_o_go<false, P_Q4_K>(p, o, st);
+    case P_Q6_K: return p.kv_fp8 ? attn_o_go<true, P_Q6_K>(p, o, st) : attn_o_go<false, P_Q6_K>(p, o, st);
+    case P_Q8_0: return p.kv_fp8 ? attn_o_go<true, P_Q8_0>(p, o, st) : attn_o_go<false, P_Q8_0>(p, o, st);
   }
 }
 

@@ -61,6 +61,16 @@ struct BufSrc {
   __device__ __forceinline__ u32x2 q8nt(int o) const { return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, base + o, 0, 2)); }
   __device__ __forceinline__ uint32_t q2(int o) const { return __builtin_amdgcn_raw_buffer_load_b16(r, base + o, 0, 0); }
 };
+//   LdsSrc: a chunk already copied to LDS (the fused attention + o-projection kernel)
+struct LdsSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ u32x4 q16nt(int o) const { return *reinterpret_cast<const u32x4*>(p + o); }
+  __device__ __forceinline__ u32x4 q16(int o) const { return *reinterpret_cast<const u32x4*>(p + o); }
+  __device__ __forceinline__ uint32_t q4nt(int o) const { return *reinterpret_cast<const uint32_t*>(p + o); }
+  __device__ __forceinline__ uint32_t q4(int o) const { return *reinterpret_cast<const uint32_t*>(p + o); }
+  __device__ __forceinline__ u32x2 q8nt(int o) const { return *reinterpret_cast<const u32x2*>(p + o); }
+  __device__ __forceinline__ uint32_t q2(int o) const { return *reinterpret_cast<const uint16_t*>(p + o); }
+};
 // gfx9 raw-buffer descriptor word 3 (DATA_FORMAT 32, no swizzle)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);

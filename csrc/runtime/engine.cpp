@@ -296,6 +296,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.attn_split_len = j.get_int("attn_split_len", 0);   // 0 = auto
   so.threads = j.get_int("threads", 0);
   so.fused_attn = j.get_bool("fused_attn", true);
+  so.attn_o_max_ctx = j.get_int("attn_o_max_ctx", 0);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
   so.prefill_gemm_v = j.get_int("prefill_gemm_v", 0);
   so.gemm_splitk_store = j.get_bool("gemm_splitk_store", true);

@@ -826,8 +826,10 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
         gemv_small(s.m, EPI_STORE, nullptr, 0, x, L.attn_norm, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N,
                    L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st);
     }
-    attention(li, M, pos, kvlen, slot, decode, st, false);
-    gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
+    if (!(decode && attention_o(li, M, pos, slot, x, st))) {
+      attention(li, M, pos, kvlen, slot, decode, st, false);
+      gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
+    }
     if (L.moe) {
       launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, moe_logits_, (int64_t)M * 64, st);
       moe_ffn(L, M, st, x);
@@ -899,6 +901,29 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   sk_defer_ = x;   // absorbed by the next layer's attention norm (or flushed after the last layer)
   gemv(L.down, EPI_ATOMIC, h_, Kff_, M, x, d, nullptr, 0, d, true, st);
   sk_defer_ = nullptr;
+}
+
+// single-stream decode: attention + o-projection in one launch (attention.hip attn_o_kernel) while
+// the context is short enough for every workgroup of a kv head to compute that head's attention
+// itself; false: the caller runs the two-kernel path
+bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st) {
+  const LayerW& L = layers_[li];
+  if (!opt_.fused_attn || opt_.deterministic || opt_.attn_o_max_ctx <= 0 || opt_.max_ctx > opt_.attn_o_max_ctx)
+    return false;
+  DecodeAttnParams dp{};
+  dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
+  dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
+  dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
+  dp.kv_fp8 = opt_.kv_fp8;
+  // one split over the whole context (every workgroup of a kv head runs that head's attention)
+  dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = (int)round_up(opt_.max_ctx, 128); dp.n_split = 1;
+  dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
+  AttnOParams op{};
+  op.W = L.wo.d; op.ptype = L.wo.ptype; op.ntiles = (int)L.wo.dims.ntiles; op.nsb = (int)L.wo.dims.nsb;
+  op.Y = x; op.ldy = cfg_.d_model; op.n_valid = cfg_.d_model;
+  if (!attn_o_supported(dp, op)) return false;
+  launch_attn_o(dp, op, st);
+  return true;
 }
 
 void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,

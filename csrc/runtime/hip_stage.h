@@ -127,6 +127,7 @@ class HipStage : public Stage {
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
   bool fuse_norm(int M) const;
+  bool attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st);
   void attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
                  hipStream_t st, bool qkv_deferred);
   bool small_path(int M) const { return opt_.small_gemv && M <= 4; }

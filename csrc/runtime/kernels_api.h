@@ -200,6 +200,16 @@ struct DecodeAttnParams {
   int kv_fp8 = 0;                  // caches hold e4m3 bytes (kv_dtype "fp8")
 };
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
+// Fused decode attention + output projection (single stream, M <= 4, one KV split): workgroup
+// (r, kvh) runs the attention of kv head kvh's query heads, then adds their split-K slice of W_o
+// (output tiles [r * 8, r * 8 + 8), k in the heads' dims) into Y with atomics.
+struct AttnOParams {
+  const uint8_t* W; int ptype; int ntiles, nsb;   // W_o, T16-packed
+  float* Y; int ldy; int n_valid;                 // residual [M][ldy]
+};
+// shapes the fused kernel takes (else: launch_attn_decode + the o-projection GEMV)
+bool attn_o_supported(const DecodeAttnParams& p, const AttnOParams& o);
+void launch_attn_o(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st);
 
 // greedy sampling: tokens[m] = argmax logits[m][:n] (lowest index on ties).  With scratch: a
 // two-level grid of (chunk, row) workgroups and a last-arriver reduce; without: one workgroup/row.

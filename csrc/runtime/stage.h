@@ -24,6 +24,7 @@ struct StageOptions {
   int attn_split_len = 0;   // decode flash-decoding split length (multiple of 128; 0 = auto)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
+  int attn_o_max_ctx = 0;     // single-stream decode: attention + o-projection in one launch up to this max_ctx (0 = off)
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
   bool gemm_splitk_store = true;   // M > 64 split-K GEMMs: per-split partial stores + a fixed-order reduction
                                    // (into the residual: absorbed by the next RMSNorm) instead of float atomics

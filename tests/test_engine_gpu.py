@@ -642,3 +642,36 @@ def test_gpu_device_probe(cuda, native):
     assert 2000 < d["hbm_read_gbps"] < 9000
     assert 1000 < d["gemv_gbps"] < 9000
     assert d["speed"] == d["gemv_gbps"]
+
+
+@pytest.mark.parametrize("ftype,mb", [("Q4_K_M", 1), ("Q8_0", 3), ("Q6_K", 1), ("Q4_K_M", 4)])
+def test_fused_attention_o_matches_two_kernels(cuda, native, model_dir, ftype, mb):
+    """Single-stream decode with attention + o-projection in ONE launch (attention.hip
+    attn_o_kernel: W_o slice copied to LDS by DMA during the attention, split-K by kv head with
+    atomics into the residual) against the two-kernel path (attn_o_max_ctx=0) and the fp32 oracle.
+    tiny-l3: head dim 128, 4 query heads per kv head, the Llama-3-8B attention shape."""
+    from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
+    path, cfg = make_model(model_dir, "tiny-l3", ftype)
+    rng = np.random.default_rng(mb)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, int(n))] for n in rng.integers(5, 90, mb)]
+    res = []
+    for amc in (0, 512):
+        with Engine(gguf=path, max_ctx=256, n_mb=1, mb_size=mb, attn_o_max_ctx=amc) as eng:
+            out, _ = eng.generate(prompts, 10)
+            res.append((out, eng.logits(rows=mb)))
+    assert res[0][0] == res[1][0]
+    for r in range(mb):
+        assert nmse(res[1][1][r], res[0][1][r]) < 1e-5
+    ref = RefLlama.from_gguf(path, device="cuda")
+    for r in range(mb):
+        toks = [t for t in res[1][0][r] if t >= 0]
+        if len(toks) < 10:   # stopped early (end-of-generation token): its logits are not the last step's
+            continue
+        ref.reset()
+        ref.forward(prompts[r], 0)
+        pos = len(prompts[r])
+        for t in toks[:-1]:
+            rl = ref.forward([t], pos)[-1].float().cpu().numpy()
+            pos += 1
+        assert nmse(res[1][1][r], rl) < 2e-4, (r, nmse(res[1][1][r], rl))
