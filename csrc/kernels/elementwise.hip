@@ -157,19 +157,83 @@ __global__ __launch_bounds__(256) void embed_kernel(int t, const uint8_t* table,
 }
 
 // ---------------------------------------------------------------- int8 activation rows (K15 prototype)
+// per-row int8 activations: 16-byte loads of 8 f16, a max pass and a quantize pass over the row
+// (the second from L2), 8-byte stores (the first version's per-element loads and byte stores took
+// 39 us for 256 x 8192)
 __global__ __launch_bounds__(256) void quant_rows_i8_kernel(const f16* X, int ldx, int K, int8_t* Q, int ldq, float* xs) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   const f16* x = X + (size_t)m * ldx;
+  int8_t* q = Q + (size_t)m * ldq;
+  const bool vec = (K & 7) == 0 && (ldx & 7) == 0 && (ldq & 7) == 0;
   float mx = 0.f;
-  for (int k = tid; k < K; k += 256) mx = fmaxf(mx, fabsf((float)x[k]));
+  if (vec) {
+    for (int k = tid * 8; k < K; k += 2048) {
+      const half8_t v = *reinterpret_cast<const half8_t*>(x + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf((float)v[j]));
+    }
+  } else {
+    for (int k = tid; k < K; k += 256) mx = fmaxf(mx, fabsf((float)x[k]));
+  }
   mx = wave_max(mx);
   if ((tid & 63) == 0) red[tid >> 6] = mx;
   __syncthreads();
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const float s = mx > 0.f ? mx / 127.f : 1.f, inv = 1.f / s;
-  for (int k = tid; k < K; k += 256) Q[(size_t)m * ldq + k] = (int8_t)__float2int_rn((float)x[k] * inv);
+  if (vec) {
+    for (int k = tid * 8; k < K; k += 2048) {
+      const half8_t v = *reinterpret_cast<const half8_t*>(x + k);
+      uint32_t w[2] = {0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        w[j >> 2] |= ((uint32_t)(uint8_t)(int8_t)__float2int_rn((float)v[j] * inv)) << (8 * (j & 3));
+      *reinterpret_cast<u32x2*>(q + k) = u32x2{w[0], w[1]};
+    }
+  } else {
+    for (int k = tid; k < K; k += 256) q[k] = (int8_t)__float2int_rn((float)x[k] * inv);
+  }
   if (tid == 0) xs[m] = s;
+}
+
+// per-row int8 re-quantization of a dense f16 weight [n_pad][k_pad] into the P_I8 chunk layout of
+// gemm3.hip (byte ((2 st + kk) * 64 + 16 g + r) * 16 + j of chunk (tile t, super-block sb) holds row
+// 16 t + r, k = 256 sb + 128 st + 64 kk + 16 g + j): one workgroup per row, one 16-k group per
+// thread step (two 16-byte loads, one 16-byte store); rows >= n get zeros and scale 1
+__global__ __launch_bounds__(256) void requant_i8_kernel(const f16* W, int ldw, int n, int nsb, uint8_t* out, float* ws) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int K = nsb * 256;
+  const f16* w = W + (size_t)row * ldw;
+  float mx = 0.f;
+  if (row < n)
+    for (int k = tid * 8; k < K; k += 2048) {
+      const half8_t v = *reinterpret_cast<const half8_t*>(w + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf((float)v[j]));
+    }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = mx > 0.f ? mx / 127.f : 1.f, inv = 1.f / s;
+  const int t = row >> 4, r = row & 15;
+  for (int k0 = tid * 16; k0 < K; k0 += 4096) {
+    const int sb = k0 >> 8, st = (k0 >> 7) & 1, kk = (k0 >> 6) & 1, g = (k0 >> 4) & 3;
+    uint32_t q[4] = {0u, 0u, 0u, 0u};
+    if (row < n) {
+      const half8_t a = *reinterpret_cast<const half8_t*>(w + k0), b = *reinterpret_cast<const half8_t*>(w + k0 + 8);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float v = j < 8 ? (float)a[j] : (float)b[j - 8];
+        const int qi = max(-127, min(127, __float2int_rn(v * inv)));
+        q[j >> 2] |= ((uint32_t)(uint8_t)(int8_t)qi) << (8 * (j & 3));
+      }
+    }
+    uint8_t* dst = out + ((size_t)t * nsb + sb) * 4096 + (size_t)(((2 * st + kk) * 64 + 16 * g + r) * 16);
+    *reinterpret_cast<u32x4*>(dst) = u32x4{q[0], q[1], q[2], q[3]};
+  }
+  if (tid == 0) ws[row] = row < n ? s : 1.f;
 }
 
 // ---------------------------------------------------------------- RoPE (NORM, adjacent pairs) + KV append
@@ -456,6 +520,10 @@ void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t*
 
 void launch_quant_rows_i8(const f16* X, int ldx, int M, int K, int8_t* Q, int ldq, float* xs, hipStream_t st) {
   hipLaunchKernelGGL(mpk::quant_rows_i8_kernel, dim3(M), dim3(256), 0, st, X, ldx, K, Q, ldq, xs);
+}
+
+void launch_requant_i8(const f16* W, int ldw, int n, int n_pad, int nsb, uint8_t* out, float* ws, hipStream_t st) {
+  hipLaunchKernelGGL(mpk::requant_i8_kernel, dim3(n_pad), dim3(256), 0, st, W, ldw, n, nsb, out, ws);
 }
 
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st) {

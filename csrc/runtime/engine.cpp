@@ -300,6 +300,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
   so.prefill_gemm_v = j.get_int("prefill_gemm_v", 0);
   so.gemm_splitk_store = j.get_bool("gemm_splitk_store", true);
+  so.int8_gemm = j.get_bool("int8_gemm", false);
   so.deterministic = j.get_bool("deterministic", false);
   so.prefill_flash = j.get_bool("prefill_flash", true);
   so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";

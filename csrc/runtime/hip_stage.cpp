@@ -1,4 +1,6 @@
 #include "hip_stage.h"
+
+#include <functional>
 #include "tuning.h"
 
 #include <chrono>
@@ -384,8 +386,45 @@ void HipStage::init_synthetic(const std::string& ftype, uint64_t seed) {
   HIP_OK(hipStreamSynchronize(stream_));
 }
 
+// int8_gemm: an int8 copy of every quantized projection (K15; the wide GEMMs then run gemm3<P_I8>):
+// each matrix is unpacked to dense f16 in a temporary buffer and re-quantized per row
+void HipStage::build_i8_copies() {
+  auto each = [&](const std::function<void(PackedMat&)>& f) {
+    for (LayerW& L : layers_) {
+      if (L.moe) continue;
+      for (MatSeg& sg : L.qkv) f(sg.m);
+      f(L.wo);
+      if (L.fused_gateup) f(L.gateup);
+      else { f(L.gate); f(L.up); }
+      f(L.down);
+    }
+  };
+  size_t maxe = 0;
+  each([&](PackedMat& m) {
+    if (m.d && !is16(m.ptype)) maxe = std::max(maxe, (size_t)m.dims.ntiles * 16 * m.dims.nsb * 256);
+  });
+  if (!maxe) return;
+  f16* tmp = nullptr;
+  HIP_OK(hipMalloc(&tmp, maxe * 2));
+  size_t bytes = 0;
+  each([&](PackedMat& m) {
+    if (!m.d || is16(m.ptype)) return;
+    const int nt = (int)m.dims.ntiles, nsb = (int)m.dims.nsb;
+    launch_unpack(m.ptype, m.d, nt, nsb, tmp, nsb * 256, stream_);
+    m.i8 = (uint8_t*)dmalloc((size_t)nt * nsb * 4096);
+    m.i8_ws = (float*)dmalloc((size_t)nt * 16 * 4);
+    launch_requant_i8(tmp, nsb * 256, (int)m.dims.N, nt * 16, nsb, m.i8, m.i8_ws, stream_);
+    bytes += (size_t)nt * nsb * 4096;
+  });
+  HIP_OK(hipStreamSynchronize(stream_));
+  HIP_OK(hipFree(tmp));
+  weight_bytes_ += bytes;
+  MP_LOGI("stage %d: int8_gemm: %.2f GiB of per-row int8 weight copies", spec_.stage, bytes / 1073741824.0);
+}
+
 void HipStage::alloc_runtime() {
   HIP_OK(hipSetDevice(spec_.device));
+  if (opt_.int8_gemm && opt_.prefill_gemm) build_i8_copies();
   const int B = opt_.mb_size, NM = opt_.n_mb;
   const int d = cfg_.d_model, Hq = cfg_.n_head, Hkv = cfg_.n_head_kv;
   scratch_rows_ = std::max(B, opt_.prefill_chunk);
@@ -396,6 +435,11 @@ void HipStage::alloc_runtime() {
     return p;
   };
   xn_ = (f16*)zalloc((size_t)scratch_rows_ * Kd_ * 2);
+  if (opt_.int8_gemm && opt_.prefill_gemm && std::max(B, opt_.prefill_chunk) > 64) {
+    xq_ld_ = std::max({Kd_, Ko_, Kff_});
+    xq_ = (int8_t*)zalloc((size_t)scratch_rows_ * xq_ld_);
+    xqs_ = (float*)zalloc((size_t)scratch_rows_ * 4);
+  }
   attn_ = (f16*)zalloc((size_t)scratch_rows_ * Ko_ * 2);
   h_ = (f16*)zalloc((size_t)scratch_rows_ * Kff_ * 2);
   // [64 floats: per-row sum of squares of the deferred qkv RMSNorm][rows][q|k|v] f32 split-K
@@ -674,6 +718,17 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
   const bool v3 = gv == 3;
   const bool v2 = gv == 2 && !is16(m.ptype);
+  if (M > 64 && opt_.prefill_gemm && m.i8 && xq_ && X) {
+    // int8_gemm: x rows quantized per row, int8 MFMA against the re-quantized copy (gemm3<P_I8>)
+    const int K = (int)m.dims.nsb * 256;
+    launch_quant_rows_i8(X, ldx, M, K, xq_, xq_ld_, xqs_, st);
+    GemvParams p{};
+    p.W = m.i8; p.X = reinterpret_cast<const f16*>(xq_); p.ldx = xq_ld_; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
+    p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
+    p.xscale = xqs_; p.wscale = m.i8_ws;
+    launch_gemm3(P_I8, epi, p, st, allow_split && !opt_.deterministic);
+    return;
+  }
   if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;

@@ -38,6 +38,8 @@ struct PackedMat {
   uint8_t* d = nullptr;
   int ptype = -1;
   PackedDims dims{};
+  uint8_t* i8 = nullptr;    // int8_gemm: per-row int8 re-quantized copy (P_I8 chunks) ...
+  float* i8_ws = nullptr;   // ... and its row scales
   size_t bytes() const { return dims.bytes; }
 };
 
@@ -127,6 +129,8 @@ class HipStage : public Stage {
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
   void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
   bool fuse_norm(int M) const;
+  void build_i8_copies();
+  int8_t* xq_ = nullptr; float* xqs_ = nullptr; int xq_ld_ = 0;   // int8_gemm: quantized activation rows
   bool attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st);
   void attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
                  hipStream_t st, bool qkv_deferred);

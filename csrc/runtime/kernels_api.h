@@ -134,6 +134,9 @@ struct RopeKvParams {
 void launch_rope_kv(const RopeKvParams& p, hipStream_t st);
 // int8 rows for the P_I8 GEMM prototype: Q[m][k] = round(X[m][k] / xs[m]), xs[m] = max_k |X[m][k]| / 127
 void launch_quant_rows_i8(const f16* X, int ldx, int M, int K, int8_t* Q, int ldq, float* xs, hipStream_t st);
+// per-row int8 re-quantization of a dense f16 weight [n_pad][nsb * 256] (launch_unpack output) into
+// P_I8 chunks (4096 B per 16 rows x 256 k) + per-row scales ws[n_pad]
+void launch_requant_i8(const f16* W, int ldw, int n, int n_pad, int nsb, uint8_t* out, float* ws, hipStream_t st);
 
 struct AttnParams {
   const f16* q;          // [M][Hq][Dp]

@@ -26,6 +26,8 @@ struct StageOptions {
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   int attn_o_max_ctx = 0;     // single-stream decode: attention + o-projection in one launch up to this max_ctx (0 = off)
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
+  bool int8_gemm = false;   // M > 64 GEMMs on v_mfma_i32_16x16x64_i8: per-row int8 activations x per-row int8
+                            // re-quantized weights (+1 B/weight of HBM; reduced precision, opt-in)
   bool gemm_splitk_store = true;   // M > 64 split-K GEMMs: per-split partial stores + a fixed-order reduction
                                    // (into the residual: absorbed by the next RMSNorm) instead of float atomics
   int prefill_gemm_v = 0;    // 0: auto (v2 for quantized, v3 for 16-bit weights); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
