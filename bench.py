@@ -19,7 +19,8 @@ token per round), bracketed by barrier + torch.cuda.synchronize() on both sides;
 ranks is reported.
 
 At N = 1 the same run also measures, with the same bracket, the other named BASELINE config
-(Llama-3-8B Q4_K_M PP=1, single stream) and the round-1 like-for-like point (70B, 64 sequences):
+(Llama-3-8B Q4_K_M PP=1, single stream), the round-1 like-for-like point (70B, 64 sequences) and
+the headline shape in the opt-in int8 compute mode (reduced precision; reported only there):
 "secondary" in the JSON line (--no-secondary skips them).  For N > 1 the line reports the data
 plane the engine built ("link": transport kind, RCCL communicator sizes as ncclCommCount returns
 them, bf16 wire bytes per token per boundary).
@@ -48,9 +49,13 @@ MODELS = {
                       vocab=32000, rope_base=10000.0),
 }
 
-# (label, model, ftype, mb_size): the other BASELINE config and the round-1 like-for-like point
-SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1),
-             ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64)]
+# (label, model, ftype, mb_size, extra engine options): the other BASELINE config, the round-1
+# like-for-like point, and the headline shape in the opt-in int8 mode (per-row int8
+# activations x per-row int8 re-quantized weights on the i8 MFMA -- reduced precision, so never the
+# headline value)
+SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1, {}),
+             ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64, {}),
+             ("llama3-70b Q4_K pp1 mb256 int8_gemm (reduced precision)", "llama3-70b", "Q4_K", 256, {"int8_gemm": True})]
 
 
 def parse_set(items):
@@ -136,11 +141,12 @@ def main():
     tr_kw = dict(device=0, pg_backend="gloo") if args.same_device else {}
     pg_cpu = args.same_device
 
-    def factory(model, ftype, mb_size, n_mb):
+    def factory(model, ftype, mb_size, n_mb, extra=None):
         max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
         cfg = dict(synthetic=MODELS[model], ftype=ftype, n_mb=n_mb, mb_size=mb_size, max_ctx=max_ctx,
                    prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
         cfg.update(parse_set(args.set))
+        cfg.update(extra or {})
         # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
         # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
         return lambda: init_from_torchrun(pp=pp, link=link, **tr_kw, **cfg)
@@ -153,10 +159,10 @@ def main():
 
     secondary = {}
     if world == 1 and not args.no_secondary:
-        for label, model, ftype, mb in SECONDARY:
-            if model == args.model and ftype == args.ftype and mb == args.mb_size:
+        for label, model, ftype, mb, extra in SECONDARY:
+            if model == args.model and ftype == args.ftype and mb == args.mb_size and not extra:
                 continue
-            sms, sp50, _ = run(factory(model, ftype, mb, 1), MODELS[model]["vocab"], mb, args.prompt_len,
+            sms, sp50, _ = run(factory(model, ftype, mb, 1, extra), MODELS[model]["vocab"], mb, args.prompt_len,
                                args.steps, args.warmup, world, pg_cpu)
             secondary[label] = dict(tok_s=round(args.steps * mb / (sms / 1e3), 2), ms_per_round=round(sms / args.steps, 4),
                                     p50_token_ms=round(sp50, 4))
