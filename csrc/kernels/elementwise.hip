@@ -30,8 +30,9 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
 __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, const float* w, int d,
                                                        float eps, f16* out, int ldo, float* zero,
                                                        int64_t zero_n, int M, const float* bias, int bias_n,
-                                                       const float* part, int nsplit, int64_t pstride, int ldp) {
-  __shared__ float red[16];
+                                                       const float* part, int nsplit, int64_t pstride, int ldp,
+                                                       int8_t* q8, int ldq8, float* q8s) {
+  __shared__ float red[16], red2[16];
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
   const bool fast = (d & 3) == 0 && d <= 8192;
@@ -85,15 +86,40 @@ __global__ __launch_bounds__(1024) void rmsnorm_kernel(const float* x, int ldx, 
   for (int i = 0; i < 16; ++i) tot += red[i];
   const float sc = rsqrtf(tot / (float)d + eps);
   if (fast) {
+    float qm = 0.f;
+    half2_t hv[2][2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int i = (tid + 1024 * k) * 4;
+      hv[k][0] = half2_t{(f16)(v[k].x * sc * ww[k].x), (f16)(v[k].y * sc * ww[k].y)};
+      hv[k][1] = half2_t{(f16)(v[k].z * sc * ww[k].z), (f16)(v[k].w * sc * ww[k].w)};
       if (i < d) {
-        half2_t a = {(f16)(v[k].x * sc * ww[k].x), (f16)(v[k].y * sc * ww[k].y)};
-        half2_t b = {(f16)(v[k].z * sc * ww[k].z), (f16)(v[k].w * sc * ww[k].w)};
-        u32x2 pk = {as_u32(a), as_u32(b)};
+        u32x2 pk = {as_u32(hv[k][0]), as_u32(hv[k][1])};
         *reinterpret_cast<u32x2*>(o + i) = pk;
+        qm = fmaxf(qm, fmaxf(fmaxf(fabsf((float)hv[k][0].x), fabsf((float)hv[k][0].y)),
+                             fmaxf(fabsf((float)hv[k][1].x), fabsf((float)hv[k][1].y))));
       }
+    }
+    if (q8) {   // int8_gemm: the same f16 row quantized per row (quant_rows_i8_kernel's rounding)
+      qm = wave_max(qm);
+      if ((tid & 63) == 0) red2[tid >> 6] = qm;
+      __syncthreads();
+      qm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) qm = fmaxf(qm, red2[i]);
+      const float s = qm > 0.f ? qm / 127.f : 1.f, inv = 1.f / s;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = (tid + 1024 * k) * 4;
+        if (i < d) {
+          const float e[4] = {(float)hv[k][0].x, (float)hv[k][0].y, (float)hv[k][1].x, (float)hv[k][1].y};
+          uint32_t w = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w |= ((uint32_t)(uint8_t)(int8_t)__float2int_rn(e[j] * inv)) << (8 * j);
+          *reinterpret_cast<uint32_t*>(q8 + (size_t)row * ldq8 + i) = w;
+        }
+      }
+      if (tid == 0) q8s[row] = s;
     }
   } else {
     for (int i = tid; i < d; i += 1024) o[i] = (f16)(xr[i] * sc * w[i]);
@@ -500,17 +526,17 @@ void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f
                     float* zero, int64_t zero_n, hipStream_t st, const float* bias, int bias_n) {
   const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
   hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
-                     zero_n, M, bias, bias_n, nullptr, 0, 0, 0);
+                     zero_n, M, bias, bias_n, nullptr, 0, 0, 0, nullptr, 0, nullptr);
 }
 
 void launch_rmsnorm_acc(float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
                         float* zero, int64_t zero_n, const float* part, int nsplit, int64_t ss, int ldp, hipStream_t st,
-                        const float* bias, int bias_n) {
-  if ((d & 3) || d > 8192 || (ldx & 3) || (ldp & 3) || (ss & 3))
+                        const float* bias, int bias_n, int8_t* q8, int ldq8, float* q8s) {
+  if ((d & 3) || d > 8192 || (ldx & 3) || (part && ((ldp & 3) || (ss & 3))) || (q8 && (ldq8 & 3)))
     throw std::runtime_error("launch_rmsnorm_acc: needs d <= 8192 and 4-aligned rows");
   const int zb = zero ? (int)((zero_n + 16383) / 16384) : 0;
   hipLaunchKernelGGL(mpk::rmsnorm_kernel, dim3(M > zb ? M : zb), dim3(1024), 0, st, x, ldx, w, d, eps, out, ldo, zero,
-                     zero_n, M, bias, bias_n, part, nsplit, ss, ldp);
+                     zero_n, M, bias, bias_n, part, part ? nsplit : 0, ss, ldp, q8, ldq8, q8s);
 }
 
 void launch_embed(int t, const uint8_t* table, int64_t rb, int d, const int32_t* tokens, int M, float* x,

@@ -721,7 +721,11 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   if (M > 64 && opt_.prefill_gemm && m.i8 && xq_ && X) {
     // int8_gemm: x rows quantized per row, int8 MFMA against the re-quantized copy (gemm3<P_I8>)
     const int K = (int)m.dims.nsb * 256;
-    launch_quant_rows_i8(X, ldx, M, K, xq_, xq_ld_, xqs_, st);
+    if (X != xq_src_ || M != xq_rows_) {   // not already quantized by norm_x / the previous GEMM on X
+      launch_quant_rows_i8(X, ldx, M, K, xq_, xq_ld_, xqs_, st);
+      xq_src_ = X;
+      xq_rows_ = M;
+    }
     GemvParams p{};
     p.W = m.i8; p.X = reinterpret_cast<const f16*>(xq_); p.ldx = xq_ld_; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
@@ -794,14 +798,20 @@ void HipStage::flush_sk(hipStream_t st) {
 void HipStage::norm_x(float* x, const float* w, int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias,
                       int bias_n) {
   const int d = cfg_.d_model;
-  if (sk_pend_.x == x && sk_pend_.M == M && sk_pend_.n == d && sk_pend_.ldy == d && d <= 8192 && (d & 3) == 0) {
-    launch_rmsnorm_acc(x, d, w, d, cfg_.eps, xn_, Kd_, M, zero, zero_n, sk_part_, sk_pend_.ns, sk_pend_.ss, sk_pend_.ldp,
-                       st, bias, bias_n);
-    sk_pend_ = SkPending{};
+  const bool pend = sk_pend_.x == x && sk_pend_.M == M && sk_pend_.n == d && sk_pend_.ldy == d;
+  // int8_gemm: the wide GEMMs reading xn_ take its int8 rows from this launch (no separate quant)
+  const bool q8 = xq_ && M > 64 && M <= scratch_rows_;
+  if ((pend || q8) && d <= 8192 && (d & 3) == 0) {
+    launch_rmsnorm_acc(x, d, w, d, cfg_.eps, xn_, Kd_, M, zero, zero_n, pend ? sk_part_ : nullptr, sk_pend_.ns,
+                       sk_pend_.ss, sk_pend_.ldp, st, bias, bias_n, q8 ? xq_ : nullptr, xq_ld_, q8 ? xqs_ : nullptr);
+    if (pend) sk_pend_ = SkPending{};
+    xq_src_ = q8 ? (const void*)xn_ : nullptr;
+    xq_rows_ = M;
     return;
   }
   flush_sk(st);
   launch_rmsnorm(x, d, w, d, cfg_.eps, xn_, Kd_, M, zero, zero_n, st, bias, bias_n);
+  xq_src_ = nullptr;
 }
 
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
@@ -887,6 +897,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     }
     if (L.moe) {
       launch_rmsnorm(x, d, L.ffn_norm, d, cfg_.eps, xn_, Kd_, M, moe_logits_, (int64_t)M * 64, st);
+      xq_src_ = nullptr;
       moe_ffn(L, M, st, x);
       return;
     }
@@ -1097,6 +1108,7 @@ void HipStage::head(int mb, int M, const float* x, int32_t* tok_out, uint64_t sa
     gemv_small(out_, EPI_STORE, nullptr, 0, x, out_norm_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, nullptr, st);
   } else {
     launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, M, nullptr, 0, st);
+    xq_src_ = nullptr;
     gemv(out_, EPI_STORE, xn_, Kd_, M, logits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
   }
   const bool pen = penalties_on() && hist_;
@@ -1145,6 +1157,7 @@ void HipStage::prefill(int mb, const std::vector<PrefillSeg>& segs, hipStream_t 
       vtok_ = (int32_t*)dmalloc((size_t)opt_.n_mb * opt_.prefill_chunk * 4);
     }
     launch_rmsnorm(x, d, out_norm_, d, cfg_.eps, xn_, Kd_, T, nullptr, 0, st);
+    xq_src_ = nullptr;
     gemv(out_, EPI_STORE, xn_, Kd_, T, vlogits_, logits_ld_, nullptr, 0, cfg_.vocab, false, st);
     launch_argmax(vlogits_, logits_ld_, cfg_.vocab, T, vtok_ + (size_t)mb * opt_.prefill_chunk, st, &am_);
   } else if (spec_.last()) {

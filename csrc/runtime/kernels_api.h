@@ -108,9 +108,12 @@ void launch_rmsnorm(const float* x, int ldx, const float* w, int d, float eps, f
                     int M, float* zero, int64_t zero_n, hipStream_t st, const float* bias = nullptr, int bias_n = 0);
 // launch_rmsnorm that first adds nsplit split-K partials (part + s * ss + row * ldp) into x and
 // writes x back (gemm_splitk_store: the deferred reduction of the o / down GEMMs into the residual)
+// part may be null (nothing to absorb); q8 (optional): the normalised f16 row also quantized to int8
+// per row (q8 + row * ldq8, scale q8s[row]) for the int8_gemm consumer
 void launch_rmsnorm_acc(float* x, int ldx, const float* w, int d, float eps, f16* out, int ldo, int M,
                         float* zero, int64_t zero_n, const float* part, int nsplit, int64_t ss, int ldp, hipStream_t st,
-                        const float* bias = nullptr, int bias_n = 0);
+                        const float* bias = nullptr, int bias_n = 0, int8_t* q8 = nullptr, int ldq8 = 0,
+                        float* q8s = nullptr);
 
 // embedding gather + dequant of raw GGUF rows -> x f32 [M][ldx]
 void launch_embed(int ggml_type, const uint8_t* table, int64_t row_bytes, int d, const int32_t* tokens,
