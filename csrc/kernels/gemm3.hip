@@ -718,7 +718,9 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
   int nsplit = 1;
   if (EPI == EPI_ATOMIC && allow_split) {
     if (g3_force_split > 0) nsplit = g3_force_split;
-    else if (wgs < g3_split_wg) nsplit = std::max(1, std::min(g3_split_wg / wgs, n_stages / 16));
+    // >= 1024 k per split (16 f16 stages of 64 k, 8 int8 stages of 128 k): the 8B o / qkv at M = 256
+    // in int8 otherwise ran 64 workgroups (2 splits of K 4096 at 16 int8 stages each)
+    else if (wgs < g3_split_wg) nsplit = std::max(1, std::min(g3_split_wg / wgs, n_stages / (PT == P_I8 ? 8 : 16)));
   }
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
