@@ -9,4 +9,4 @@ for i8 in false true false true; do
   timeout -k 10 300 python bench.py --steps 15 --warmup 3 --no-secondary --set int8_gemm=$i8 > $O/b.log 2>&1 || { tail -5 $O/b.log; exit 1; }
   echo "int8_gemm=$i8 $(grep -o '"value": [0-9.]*' $O/b.log)"
 done
-bash scripts/r7m_i8_tiles.sh
+bash scripts/experiments/r7m_i8_tiles.sh
