@@ -100,8 +100,11 @@ from mipipe.parallel import generate_elastic
 import torch.distributed as dist
 out = generate_elastic({prompts!r}, {n!r}, {ckpt!r}, every=3, pp=2, gguf={path!r}, backend="cpu", max_ctx=128,
                        n_mb=2, mb_size=1, prefill_chunk=16, split="even", base_port={port})
-print("OUT " + json.dumps(dict(rank=int(os.environ["RANK"]), restart=os.environ.get("TORCHELASTIC_RESTART_COUNT"),
-                               out=out)), flush=True)
+# one file per (rank, attempt): torchrun merges the ranks' stdout, and two lines written at once can
+# interleave mid-line
+res = dict(rank=int(os.environ["RANK"]), restart=os.environ.get("TORCHELASTIC_RESTART_COUNT"), out=out)
+with open(os.path.join({ckpt!r}, "..", "out_%d_%s.json" % (res["rank"], res["restart"])), "w") as f:
+    json.dump(res, f)
 dist.destroy_process_group()
 """
 
@@ -124,7 +127,8 @@ def test_elastic_rank_restart_resumes_from_checkpoint(native, model_dir, tmp_pat
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(script)]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
-    outs = [json.loads(l[4:]) for l in p.stdout.splitlines() if l.startswith("OUT ")]
+    outs = [json.loads(f.read_text()) for f in sorted(tmp_path.glob("out_*.json"))]
+    assert len(outs) == 2, (outs, p.stdout[-2000:])
     assert {o["restart"] for o in outs} == {"1"}, outs       # only the restarted attempt finished
     assert all(o["out"] == ref for o in outs)
     assert not list((ckpt / "replica0").glob("round_*"))   # a finished run removes its checkpoints
