@@ -393,7 +393,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
         o = f8x2_lo(q);
       } else {
         o = half2_t{(f16)r0, (f16)r1};
-        *reinterpret_cast<half2_t*>(p.k_cache + koff + 2 * j) = o;
+        if (!(p.probe & 2)) *reinterpret_cast<half2_t*>(p.k_cache + koff + 2 * j) = o;
       }
       *reinterpret_cast<half2_t*>(sm_kn + 2 * j) = o;
     }
@@ -406,7 +406,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
         v = f8x2_lo(q).x;
       } else {
         v = (f16)vv;
-        p.v_cache[voff + (size_t)j * 64] = v;
+        if (!(p.probe & 1)) p.v_cache[voff + (size_t)j * 64] = v;
       }
       sm_vn[j] = v;
     }

@@ -204,6 +204,8 @@ struct DecodeAttnParams {
   // * qkv + bias (bias optional, [q|k|v])
   const float* ssq = nullptr; float eps = 0.f; int d_model = 0; const float* bias = nullptr;
   int kv_fp8 = 0;                  // caches hold e4m3 bytes (kv_dtype "fp8")
+  int probe = 0;                   // timing probes only (knob ATTN_PROBE): bit 0 skips the global V append,
+                                   // bit 1 the K append (results wrong; never in production runs)
 };
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
 // Fused decode attention + output projection (single stream, M <= 4, one KV split): workgroup

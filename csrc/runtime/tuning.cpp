@@ -37,6 +37,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
     {"GEMM3_PROBE", 0, 0, 7, nullptr},
+    {"ATTN_PROBE", 0, 0, 3, nullptr},
 };
 
 std::atomic<int> g_vals[KNOB_COUNT];

@@ -23,6 +23,7 @@ enum Knob : int {
   KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
   KNOB_GEMM3_PROBE,         // gemm3 timing probes (Q4_K SwiGLU 256x256 only; 0 = the real kernel)
+  KNOB_ATTN_PROBE,          // decode attention timing probes (1: no V append, 2: no K append; 0 = real)
   KNOB_COUNT
 };
 
