@@ -90,6 +90,8 @@ inline void print_common_usage(FILE* f) {
           "  --link local|rccl|tcp     stage transport;  --prefill-chunk N;  --no-graphs;  --threads N\n"
           "  --no-prefix-cache         prefill every request in full (no KV reuse of a common prefix)\n"
           "  --kv-pool TOKENS          paged KV pool per stage;  --kv-dtype f16|fp8 (-ctk/-ctv) KV cache element type\n"
+          "  --int8-gemm               batches > 64 rows on the int8 MFMA (per-row int8 activations and weights:\n"
+          "                            faster, reduced precision);  --deterministic  bitwise-reproducible logits\n"
           "  --world N --rank R        one process per stage (multi-process / multi-host)\n"
           "  --next HOST --master HOST --base-port P   TCP ring neighbours (prima.cpp style)\n"
           "  --gpu-mem GiB [--force]   per-GPU memory budget (caps auto KV; fail if a stage exceeds it)\n"
@@ -154,6 +156,8 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--kv-dtype" || a == "-ctk" || a == "--cache-type-k" || a == "-ctv" || a == "--cache-type-v")
       e["kv_dtype"] = val();                                                     // f16 | fp8 (K and V together)
     else if (a == "--force") e["force"] = true;
+    else if (a == "--int8-gemm") e["int8_gemm"] = true;
+    else if (a == "--deterministic") e["deterministic"] = true;
     else if (a == "--base-port") e["base_port"] = std::atoi(val().c_str());
     else if (a == "--rpc") rpc = val();
     else if (a == "--device") e["device"] = std::atoi(val().c_str());
