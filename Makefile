@@ -8,6 +8,11 @@ BINDIR    := $(PKG)/bin
 BUILD     := build
 CXXFLAGS  := -std=c++17 -O3 -fPIC -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-result \
              -I$(ROCM)/include -Icsrc/runtime
+# `make PROBES=1 BUILD=build_probes LIBDIR=...`: a separate library with the timing-probe knobs
+# (GEMM3_PROBE, ATTN_PROBE), which skip work and give wrong results; the default build has none
+ifeq ($(PROBES),1)
+CXXFLAGS  += -DMIPIPE_TIMING_PROBES
+endif
 HIPFLAGS  := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
 LDFLAGS   := -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
 

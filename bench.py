@@ -4,15 +4,23 @@ pipeline engine on Llama-3-70B Q4_K, PP = number of GPUs (BASELINE.json: "decode
 node) + p50/token, Llama-3-70B PP=8 and 8B PP=1"; reference headline 2-3 tok/s for 70B, PDF p.12).
 
     python bench.py --gpus 1 --steps 20 --warmup 5                  # PP=1 on one MI355X
+    python bench.py --gpus 8 --steps 20 ...                          # PP=8 in ONE process (no launcher)
     torchrun --nproc-per-node 8 bench.py --gpus 8 --steps 20 ...     # PP=8, one rank per GPU
 
 Weights are random-init directly in HBM with the exact Llama-3-70B architecture and Q4_K block
-format (no network, no checkpoint).  Each rank owns one pipeline stage (contiguous layer range,
-cost-balanced split with the LM head on the last stage); activations move stage to stage with
-RCCL send/recv over xGMI (bf16 wire); N + 1 micro-batches (N > 1) of `--mb-size` sequences
-circulate through the piped ring.  Default 256 sequences per micro-batch, sized for 288 GB of
-HBM: above 64 rows the decode projections run on the dequant MFMA GEMM v3 (gemm3.hip: weights
-dequantized once per workgroup into LDS, 256 x 256 tiles).  Weak scaling: per-GPU work is fixed
+format (no network, no checkpoint).  Every stage owns one GPU (contiguous layer range,
+cost-balanced split with the LM head on the last stage); activations move stage to stage over
+xGMI as bf16; N + 1 micro-batches (N > 1) of `--mb-size` sequences circulate through the piped
+ring.  Two launches, the same engine:
+  * under torchrun (WORLD_SIZE set): one process per GPU, engine mode "mp", RCCL send/recv on a
+    2-rank communicator per link direction (ids exchanged over torch.distributed);
+  * without a launcher (`--gpus N`, no WORLD_SIZE): one process, engine mode "local", one host
+    thread per GPU, links from ncclCommInitAll (`--link auto`/`rccl`) or, if RCCL refuses, peer-copy
+    LocalLinks (one device copy per boundary, receiver-side xGMI read); `--same-device` puts every
+    stage on GPU 0 (the 1-GPU rehearsal of the N-stage path).
+Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the Q4_K decode
+projections run on the 128-row dequant MFMA GEMM (gemm2 in gemv2.hip; hip_stage.cpp picks it for
+quantized weights, gemm3 for 16-bit ones).  Weak scaling: per-GPU work is fixed
 (every stage streams its own weights once per micro-batch per round), global batch =
 n_mb * mb_size sequences.  The timed region is exactly K decode rounds (every sequence emits one
 token per round), bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over
@@ -66,7 +74,7 @@ def parse_set(items):
     return out
 
 
-def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu):
+def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, devices=(0,)):
     """Start n_seq synthetic prompts, warm up, time exactly `steps` decode rounds; returns
     (ms, p50 ms, engine info) with ms and p50 the MAX over ranks."""
     eng = eng_factory()
@@ -80,7 +88,9 @@ def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu):
         def bracket():
             if world > 1:
                 dist.barrier()
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                for d in devices:   # in-process PP: every GPU of the pipeline
+                    torch.cuda.synchronize(d)
 
         bracket()
         t0 = time.perf_counter()
@@ -89,7 +99,7 @@ def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu):
         ms = (time.perf_counter() - t0) * 1e3
         tms = sorted(st.get("token_ms", []))
         p50 = tms[len(tms) // 2] if tms else 0.0
-        vals = torch.tensor([ms, p50], dtype=torch.float64, device="cpu" if pg_cpu else "cuda")
+        vals = torch.tensor([ms, p50], dtype=torch.float64, device="cpu" if (pg_cpu or world == 1) else "cuda")
         if world > 1:
             dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
         from mipipe import _native as N
@@ -115,10 +125,14 @@ def main():
                     help="pipeline depth (default: = #GPUs); --pp P < N runs N/P data-parallel pipeline replicas")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--link", default="rccl", choices=["rccl", "tcp"], help="stage-to-stage transport (N > 1)")
+    ap.add_argument("--link", default="auto", choices=["auto", "rccl", "local", "tcp"],
+                    help="stage-to-stage transport (N > 1). torchrun: rccl (auto) or tcp. In-process: rccl pairs "
+                         "from ncclCommInitAll, falling back to peer-copy local links if RCCL refuses (auto: rccl "
+                         "when every stage has its own GPU)")
     ap.add_argument("--same-device", action="store_true",
-                    help="every rank on GPU 0 with a gloo process group and TCP links: rehearses the N > 1 path on a "
-                         "1-GPU box (RCCL refuses two ranks of a communicator on one GPU)")
+                    help="every stage on GPU 0: rehearses the N > 1 path on a 1-GPU box (in-process: local links; "
+                         "torchrun: a gloo process group and TCP links, RCCL refuses two ranks of a communicator "
+                         "on one GPU)")
     ap.add_argument("--no-secondary", action="store_true", help="N = 1: skip the secondary configs")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra engine option (A/B runs), e.g. --set fused_norm=false")
@@ -126,20 +140,34 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus > 1 must be launched with torchrun (one rank per GPU)", file=sys.stderr)
-            sys.exit(2)
+    # no launcher and --gpus N > 1: the whole N-stage pipeline in this process (engine mode "local",
+    # one host thread per GPU); under torchrun every rank owns one stage (engine mode "mp")
+    inproc = world == 1 and args.gpus > 1
+    if world > 1 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    from mipipe.engine import Engine
     from mipipe.parallel import init_from_torchrun
 
-    pp = args.pp or world
-    if world % pp:
-        print(f"bench.py: --pp {pp} does not divide {world} GPUs", file=sys.stderr)
+    n_gpus = args.gpus if inproc else world
+    pp = args.pp or n_gpus
+    if n_gpus % pp or (inproc and pp != n_gpus):
+        print(f"bench.py: --pp {pp} with {n_gpus} GPUs: {'in-process runs one pipeline over all GPUs (use torchrun for replicas)' if inproc else 'must divide the GPU count'}",
+              file=sys.stderr)
         sys.exit(2)
-    replicas = world // pp
-    link = "tcp" if args.same_device else args.link
-    tr_kw = dict(device=0, pg_backend="gloo") if args.same_device else {}
-    pg_cpu = args.same_device
+    replicas = n_gpus // pp
+    if inproc:
+        devices = [0] * n_gpus if args.same_device else list(range(n_gpus))
+        if not args.same_device and torch.cuda.device_count() < n_gpus:
+            print(f"bench.py: --gpus {n_gpus} but {torch.cuda.device_count()} visible GPU(s) (--same-device rehearses "
+                  "the pipeline on GPU 0)", file=sys.stderr)
+            sys.exit(2)
+        link = args.link if args.link != "tcp" else "auto"
+    else:
+        devices = [0]
+        link = "tcp" if args.same_device else ("rccl" if args.link in ("auto", "local") else args.link)
+    tr_kw = dict(device=0, pg_backend="gloo") if args.same_device and not inproc else {}
+    pg_cpu = args.same_device and not inproc
 
     def factory(model, ftype, mb_size, n_mb, extra=None):
         max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
@@ -147,18 +175,22 @@ def main():
                    prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
         cfg.update(parse_set(args.set))
         cfg.update(extra or {})
+        if inproc:
+            # every stage in this process: stage s on devices[s], one host thread per stage
+            return lambda: Engine(mode="local", stages=pp, devices=devices, link=link, **cfg)
         # one stage per rank (mipipe.parallel.init_from_torchrun): link r = stage r -> stage (r+1) % N,
         # its sender (rank r) creates the RCCL unique id, exchanged over torch.distributed (RCCL)
         return lambda: init_from_torchrun(pp=pp, link=link, **tr_kw, **cfg)
 
     n_mb = args.n_mb or (pp + 1 if pp > 1 else 1)
     ms, p50, info = run(factory(args.model, args.ftype, args.mb_size, n_mb), MODELS[args.model]["vocab"],
-                        n_mb * args.mb_size, args.prompt_len, args.steps, args.warmup, world, pg_cpu)
+                        n_mb * args.mb_size, args.prompt_len, args.steps, args.warmup, world, pg_cpu,
+                        sorted(set(devices)))
     n_tok = args.steps * n_mb * args.mb_size * replicas
     value = n_tok / (ms / 1e3)
 
     secondary = {}
-    if world == 1 and not args.no_secondary:
+    if n_gpus == 1 and not args.no_secondary:
         for label, model, ftype, mb, extra in SECONDARY:
             if model == args.model and ftype == args.ftype and mb == args.mb_size and not extra:
                 continue
@@ -168,13 +200,17 @@ def main():
                                     p50_token_ms=round(sp50, 4))
 
     link_info = None
-    if world > 1:
+    if n_gpus > 1:
         links = info.get("links", [])
         link_info = dict(kind=sorted({l["kind"] for l in links}), comm_nranks=sorted({l["comm_nranks"] for l in links}),
                          links_per_rank=len(links), act_dtype=info.get("act_dtype"),
                          wire_bytes_per_token=info.get("wire_bytes_per_token"),
-                         torch_pg_world=dist.get_world_size(), torch_pg_backend=dist.get_backend(),
-                         same_device=args.same_device)
+                         launcher="in-process" if inproc else "torchrun", engine_mode=info.get("mode"),
+                         devices=sorted({s["device"] for s in info["stages"]}), same_device=args.same_device)
+        if info.get("link_fallback"):
+            link_info["fallback"] = info["link_fallback"]
+        if world > 1:
+            link_info.update(torch_pg_world=dist.get_world_size(), torch_pg_backend=dist.get_backend())
 
     if rank == 0:
         m = MODELS[args.model]
@@ -182,7 +218,7 @@ def main():
             "metric": "decode tokens/sec (whole node) + p50/token",
             "value": round(value, 2),
             "unit": "tokens/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms / args.steps, 4),

@@ -695,10 +695,8 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
 
 namespace mp {
 
-static int g3_force_bm = 0, g3_force_bn = 0, g3_force_split = 0, g3_split_wg = 256;
-void set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) {
-  g3_force_bm = bm; g3_force_bn = bn; g3_force_split = nsplit; g3_split_wg = split_wg > 0 ? split_wg : 256;
-}
+// A/B overrides come from the knob registry (tuning.h: atomic, validated); the split target is
+// gemm2's GEMM2_SPLIT_WG, so the two GEMMs fill the grid by the same rule
 
 template <int PT, int EPI, int BM, int TW, int PROBE>
 static void gemm3_launch(const GemvParams& p, dim3 grid, int n_mb, int per, int n_stages, hipStream_t st) {
@@ -716,16 +714,18 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
   const int n_stages = p.nsb * mpk::g3_spb<PT>();
   const int wgs = n_cg * n_mb;
   int nsplit = 1;
+  const int split_wg = knob(KNOB_GEMM2_SPLIT_WG);
   if (EPI == EPI_ATOMIC && allow_split) {
-    if (g3_force_split > 0) nsplit = g3_force_split;
+    if (knob(KNOB_GEMM3_SPLIT) > 0) nsplit = knob(KNOB_GEMM3_SPLIT);
     // >= 1024 k per split (16 f16 stages of 64 k, 8 int8 stages of 128 k): the 8B o / qkv at M = 256
     // in int8 otherwise ran 64 workgroups (2 splits of K 4096 at 16 int8 stages each)
-    else if (wgs < g3_split_wg) nsplit = std::max(1, std::min(g3_split_wg / wgs, n_stages / (PT == P_I8 ? 8 : 16)));
+    else if (wgs < split_wg) nsplit = std::max(1, std::min(split_wg / wgs, n_stages / (PT == P_I8 ? 8 : 16)));
   }
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
   const dim3 grid(wgs, nsplit);
+#ifdef MIPIPE_TIMING_PROBES
   if constexpr (PT == P_Q4_K && EPI == EPI_SWIGLU && BM == 256 && TW == 2) {
     switch (knob(KNOB_GEMM3_PROBE)) {   // timing probes (tools/gemv_bench.py --knob GEMM3_PROBE=k)
       case 1: return gemm3_launch<PT, EPI, BM, TW, 1>(p, grid, n_mb, per, n_stages, st);
@@ -736,6 +736,7 @@ static void gemm3_go(GemvParams p, bool allow_split, hipStream_t st) {
       default: break;
     }
   }
+#endif
   gemm3_launch<PT, EPI, BM, TW, 0>(p, grid, n_mb, per, n_stages, st);
   }
 }
@@ -744,12 +745,12 @@ template <int PT, int EPI>
 static void gemm3_shape(GemvParams p, bool allow_split, hipStream_t st) {
   // BM: 128 rows when one 128-row block holds M; BN: 256 columns (2 tiles per wave) unless that
   // leaves fewer than half the CUs with a workgroup and the epilogue cannot split K
-  const int bm = g3_force_bm ? g3_force_bm : (p.M <= 128 ? 128 : 256);
+  const int bm = knob(KNOB_GEMM3_BM) ? knob(KNOB_GEMM3_BM) : (p.M <= 128 ? 128 : 256);
   const int wg256 = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
   const bool splits = EPI == EPI_ATOMIC && allow_split;
   // split-K (ATOMIC) shapes: 128 columns (r6e, M = 256: 70B qkv 104 -> 77 us, o 101 -> 74, down
   // 186 -> 161, 8B down 91 -> 65); SwiGLU / store keep 256 unless that leaves half the CUs idle
-  const int bn = g3_force_bn ? g3_force_bn : (splits || wg256 < 128 ? 128 : 256);
+  const int bn = knob(KNOB_GEMM3_BN) ? knob(KNOB_GEMM3_BN) : (splits || wg256 < 128 ? 128 : 256);
   if (bm == 128) {
     if (bn == 128) gemm3_go<PT, EPI, 128, 1>(p, allow_split, st);
     else gemm3_go<PT, EPI, 128, 2>(p, allow_split, st);

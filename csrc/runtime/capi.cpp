@@ -196,7 +196,17 @@ int mp_op_gemm3(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   API_CATCH(-1)
 }
 
-void mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) { set_gemm3_tuning(bm, bn, nsplit, split_wg); }
+// A/B overrides of gemm3 through the knob registry (0 = auto; split_wg 0 = the default 256 of the
+// GEMM2_SPLIT_WG knob both GEMMs share)
+int mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) {
+  API_TRY
+  set_knob("GEMM3_BM", bm);
+  set_knob("GEMM3_BN", bn);
+  set_knob("GEMM3_SPLIT", nsplit);
+  set_knob("GEMM2_SPLIT_WG", split_wg > 0 ? split_wg : 256);
+  return 0;
+  API_CATCH(-1)
+}
 
 // int8-activation GEMM prototype (K15): X f16 [M][ldx] -> int8 rows Q [M][ldq] + row scales xs;
 // then Y = xs[m] ws[n] sum_k Q[m][k] W8[n][k] on v_mfma_i32_16x16x64_i8 (W: P_I8 chunks)

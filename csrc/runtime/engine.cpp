@@ -72,6 +72,34 @@ double synth_layer_bytes(const ModelConfig& c, const std::string& ftype, int li)
   return b(t.q, q, d) + b(t.k, kv, d) + b(t.v, kv, d) + b(t.o, d, q) + ffn * std::max(1, c.n_expert);
 }
 
+// int8_gemm (HipStage::build_i8_copies): an int8 copy of every quantized non-MoE projection, one
+// byte per weight of the 16-row x 256-k padded packing plus a float row scale.  These bytes live
+// next to the weights, so the KV budget and the --gpu-mem check must see them.
+double i8_copy_bytes(int t, int64_t n, int64_t k) {
+  if (t == T_F32 || t == T_F16 || t == T_BF16) return 0;
+  const double np = (double)((n + 15) / 16 * 16), kp = (double)((k + 255) / 256 * 256);
+  return np * kp + np * 4;
+}
+
+double synth_layer_i8_bytes(const ModelConfig& c, const std::string& ftype, int li) {
+  if (c.n_expert > 0) return 0;   // MoE experts keep their own kernels (no copy)
+  const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, li, c.n_layer);
+  const int64_t d = c.d_model, q = c.q_dim(), kv = c.kv_dim(), f = c.d_ff;
+  return i8_copy_bytes(t.q, q, d) + i8_copy_bytes(t.k, kv, d) + i8_copy_bytes(t.v, kv, d) + i8_copy_bytes(t.o, d, q) +
+         i8_copy_bytes(t.gate, f, d) + i8_copy_bytes(t.up, f, d) + i8_copy_bytes(t.down, d, f);
+}
+
+double gguf_layer_i8_bytes(const GgufFile& g, int li) {
+  double b = 0;
+  const std::string p = "blk." + std::to_string(li) + ".";
+  if (g.tensor(p + "ffn_gate_inp.weight")) return 0;   // MoE layer: build_i8_copies skips it whole
+  for (const char* nm : {"attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down"}) {
+    const GgufTensor* t = g.tensor(p + nm + ".weight");
+    if (t && t->ne.size() >= 2) b += i8_copy_bytes(t->type, t->ne[1], t->ne[0]);
+  }
+  return b;
+}
+
 }  // namespace
 
 Engine::Engine(const Json& j) : jcfg_(j) {
@@ -98,6 +126,9 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   const uint64_t seed = (uint64_t)j.get_num("seed", 1234);
 
   std::vector<double> layer_cost;
+  std::vector<double> layer_extra;   // HBM bytes per layer beyond its weights (int8_gemm copies)
+  const bool i8_copies = j.get_bool("int8_gemm", false) && j.get_bool("prefill_gemm", true) &&
+                         j.get_str("backend", "hip") != "cpu";
   double head_cost = 0, embd_cost = 0;
   if (j.has("gguf")) {
     gguf_.reset(new GgufFile(j.get_str("gguf", "")));
@@ -108,12 +139,16 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       for (auto& t : gguf_->tensors())
         if (t.name.compare(0, p.size(), p) == 0) bytes += (double)t.nbytes;
       layer_cost.push_back(bytes);
+      layer_extra.push_back(i8_copies ? gguf_layer_i8_bytes(*gguf_, li) : 0.0);
     }
     const GgufTensor* out = gguf_->tensor("output.weight");
     head_cost = (double)(out ? out->nbytes : gguf_->tensor("token_embd.weight")->nbytes);
   } else if (j.has("synthetic")) {
     cfg_ = config_from_json(j["synthetic"]);
-    for (int li = 0; li < cfg_.n_layer; ++li) layer_cost.push_back(synth_layer_bytes(cfg_, ftype, li));
+    for (int li = 0; li < cfg_.n_layer; ++li) {
+      layer_cost.push_back(synth_layer_bytes(cfg_, ftype, li));
+      layer_extra.push_back(i8_copies ? synth_layer_i8_bytes(cfg_, ftype, li) : 0.0);
+    }
     const SyntheticTypes t = SyntheticTypes::from_ftype(ftype, 0, cfg_.n_layer);
     head_cost = (double)cfg_.vocab * cfg_.d_model * block_bytes(t.out) / block_elems(t.out);
   } else {
@@ -195,7 +230,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     std::map<int, int> dev_l, dev_n;
     for (auto& sp : specs_) {
       double w = 0;
-      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li];
+      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li] + layer_extra[li];
       if (sp.first()) w += embd_bytes;
       if (sp.last()) w += head_cost;
       const int key = mode_ == "mp" ? sp.stage : devices[sp.stage];
@@ -243,7 +278,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     for (auto& sp : specs_) {
       if (mode_ == "mp" && sp.stage != rank_) continue;
       double w = 0;
-      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li];
+      for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li] + layer_extra[li];
       if (sp.first()) w += embd_b;
       if (sp.last()) w += head_cost;
       const double kv = (double)(sp.layer_end - sp.layer_begin) * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() *
@@ -346,13 +381,16 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   build_links(j);
   for (auto& l : links_) l->set_timeout(j.get_num("link_timeout_s", 600.0));
   // Stage-boundary wire format: the residual stream is f32 inside a stage; between
-  // GPUs it travels as bf16 by default over RCCL (half the xGMI bytes: 16 KiB per 70B token), f32
-  // elsewhere (LocalLink emulation and TCP keep PP=S bitwise equal to PP=1).  Every rank derives
-  // the same choice from the shared config.
+  // GPUs it travels as bf16 by default (half the xGMI bytes: 16 KiB per 70B token) over RCCL and
+  // over peer-copy LocalLinks, f32 elsewhere (same-GPU LocalLink emulation and TCP keep PP=S
+  // bitwise equal to PP=1).  Every rank derives the same choice from the shared config.
   {
     const std::string ad = j.get_str("act_dtype", "auto");
     const std::string lk = S_ > 1 ? std::string(links_.empty() ? "none" : links_.front()->kind()) : "none";
-    if (ad == "auto") act_dtype_ = (!cpu_ && lk == "rccl") ? ACT_BF16 : ACT_F32;
+    bool cross_gpu = false;
+    for (auto& l : links_)
+      if (auto* ll = dynamic_cast<LocalLink*>(l.get())) cross_gpu = cross_gpu || ll->peer();
+    if (ad == "auto") act_dtype_ = (!cpu_ && (lk == "rccl" || cross_gpu)) ? ACT_BF16 : ACT_F32;
     else if (ad == "f32") act_dtype_ = ACT_F32;
     else if (ad == "f16") act_dtype_ = ACT_F16;
     else if (ad == "bf16") act_dtype_ = ACT_BF16;
@@ -432,29 +470,61 @@ bool Engine::owns_first() const {
 void Engine::build_links(const Json& j) {
   if (S_ == 1) return;
   // link i: stage i -> stage (i+1) % S (link S-1 is the token ring back to stage 0)
-  const size_t act_bytes = (size_t)std::max(chunk_, B_) * cfg_.d_model * 4;
   if (mode_ == "local") {
-    const std::string kind = cpu_ ? "host" : j.get_str("link", "local");
+    // "rccl": one 2-rank communicator per link direction from ncclCommInitAll (in-process, one host
+    // thread per GPU).  RCCL refuses a communicator with two ranks on one GPU, and may be unusable
+    // on a box; then the link falls back to the peer-copy LocalLink and says so (info()["links"]).
+    // "auto": rccl when every stage has its own GPU, local otherwise.
+    std::string kind = cpu_ ? "host" : j.get_str("link", "local");
+    if (kind == "auto") {
+      std::vector<int> d;
+      for (auto& sp : specs_) d.push_back(sp.device);
+      std::sort(d.begin(), d.end());
+      kind = std::unique(d.begin(), d.end()) == d.end() ? "rccl" : "local";
+    }
     for (int i = 0; i < S_; ++i) {
       const int a = i, b = (i + 1) % S_;
       if (cpu_) {
         links_.emplace_back(new HostLink(std::max(4, M_ + 2)));
         workers_[a]->out = links_.back().get();
         workers_[b]->in = links_.back().get();
-      } else if (kind == "rccl") {
-        void *ca, *cb;
-        rccl_make_pair(specs_[a].device, specs_[b].device, &ca, &cb);
-        links_.emplace_back(new RcclLink(ca, 0, 1, specs_[a].device));   // sender end (rank 0 -> 1)
-        Link* snd = links_.back().get();
-        links_.emplace_back(new RcclLink(cb, 1, 0, specs_[b].device));   // receiver end
-        Link* rcv = links_.back().get();
-        workers_[a]->out = snd;
-        workers_[b]->in = rcv;
-      } else {
-        links_.emplace_back(new LocalLink(specs_[a].device, specs_[b].device, act_bytes, std::max(4, M_ + 2)));
-        workers_[a]->out = links_.back().get();
-        workers_[b]->in = links_.back().get();
+        continue;
       }
+      if (kind == "rccl") {
+        void *ca = nullptr, *cb = nullptr;
+        try {
+          rccl_make_pair(specs_[a].device, specs_[b].device, &ca, &cb);
+        } catch (const std::exception& e) {
+          link_fallback_ = std::string("rccl -> local: ") + e.what();
+          MP_LOGW("link %d (GPU %d -> GPU %d): %s", i, specs_[a].device, specs_[b].device, link_fallback_.c_str());
+          kind = "local";
+        }
+        if (kind == "rccl") {
+          links_.emplace_back(new RcclLink(ca, 0, 1, specs_[a].device));   // sender end (rank 0 -> 1)
+          Link* snd = links_.back().get();
+          links_.emplace_back(new RcclLink(cb, 1, 0, specs_[b].device));   // receiver end
+          Link* rcv = links_.back().get();
+          workers_[a]->out = snd;
+          workers_[b]->in = rcv;
+          continue;
+        }
+      }
+      links_.emplace_back(new LocalLink(specs_[a].device, specs_[b].device));
+      workers_[a]->out = links_.back().get();
+      workers_[b]->in = links_.back().get();
+    }
+    if (kind == "local" && !link_fallback_.empty()) {
+      // a partial RCCL ring mixed with local links would be valid, but keep one transport per ring
+      for (int i = 0; i < S_; ++i) {
+        Link* o = workers_[i]->out;
+        if (std::string(o->kind()) != "rccl") continue;
+        links_.emplace_back(new LocalLink(specs_[i].device, specs_[(i + 1) % S_].device));
+        workers_[i]->out = workers_[(i + 1) % S_]->in = links_.back().get();
+      }
+      std::vector<std::unique_ptr<Link>> keep;
+      for (auto& l : links_)
+        if (std::string(l->kind()) != "rccl") keep.push_back(std::move(l));
+      links_ = std::move(keep);
     }
     MP_LOGI("links: %d x %s (token ring %d B per sequence)", S_, kind.c_str(), 4);
   } else if (cpu_ || j.get_str("link", "rccl") == "tcp") {
@@ -1718,6 +1788,7 @@ Json Engine::info() const {
     }
   }
   j["links"] = ls;
+  if (!link_fallback_.empty()) j["link_fallback"] = link_fallback_;
   const int ab = act_dtype_ == ACT_F32 ? 4 : 2;
   j["act_dtype"] = act_dtype_ == ACT_F32 ? "f32" : act_dtype_ == ACT_F16 ? "f16" : "bf16";
   j["wire_bytes_per_token"] = S_ > 1 ? (int64_t)cfg_.d_model * ab : 0;   // per stage boundary

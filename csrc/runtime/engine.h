@@ -169,6 +169,7 @@ class Engine {
   bool trace_ = false, failed_ = false;
   bool packed_prefill_ = true;   // several sequences per prefill chunk (config "packed_prefill")
   int act_dtype_ = 0;            // stage-boundary activation wire format (ActDtype; config "act_dtype")
+  std::string link_fallback_;    // why local mode's requested RCCL links became LocalLinks (empty: none)
   double trace_t0_ = 0, watchdog_s_ = 600;
   std::vector<std::string> trace_events_;
   Json fault_;

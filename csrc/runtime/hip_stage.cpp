@@ -1006,7 +1006,9 @@ void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen
     dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
     dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
     if (qkv_deferred) { dp.ssq = ssq_; dp.eps = cfg_.eps; dp.d_model = d; dp.bias = L.qkv_bias; }
+#ifdef MIPIPE_TIMING_PROBES
     dp.probe = knob(KNOB_ATTN_PROBE);
+#endif
     launch_attn_decode(dp, st);
   } else {
     RopeKvParams rp{};

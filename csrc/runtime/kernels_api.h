@@ -92,9 +92,8 @@ void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_s
 // Prompt / wide-decode GEMM v3 (gemm3.hip): BM x BN = {128, 256} x {128, 256} workgroup tiles, each
 // weight element dequantized once per workgroup into an f16 LDS image shared by its 8 waves,
 // X and the raw quants staged by global_load_lds, 16x16x32 f16 MFMA; EPI_ATOMIC splits K over
-// blockIdx.y (allow_split).  set_gemm3_tuning: force BM / BN / split (0 = auto) for A/B runs.
+// blockIdx.y (allow_split).  A/B overrides: knobs GEMM3_BM / GEMM3_BN / GEMM3_SPLIT (tuning.h).
 void launch_gemm3(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
-void set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg);
 
 // Y[m][n] += sum_{s < nsplit} part[s][m][n], s ascending: the fixed-order split-K reduction of the
 // deterministic mode (part rows of ldp floats, splits split_stride floats apart)

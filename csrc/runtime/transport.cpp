@@ -26,11 +26,11 @@ namespace mp {
   } while (0)
 
 // ---------------------------------------------------------------- LocalLink
-LocalLink::LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_slots)
-    : src_dev_(src_device), dst_dev_(dst_device), slot_bytes_(slot_bytes) {
+LocalLink::LocalLink(int src_device, int dst_device) : src_dev_(src_device), dst_dev_(dst_device) {
   int cur = 0;
   HIP_OK(hipGetDevice(&cur));
   if (src_dev_ != dst_dev_) {
+    // the receiver's copy reads the sender's HBM directly (xGMI peer read, one hop)
     (void)hipSetDevice(src_dev_);
     (void)hipDeviceEnablePeerAccess(dst_dev_, 0);
     (void)hipGetLastError();
@@ -38,27 +38,16 @@ LocalLink::LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_sl
     (void)hipDeviceEnablePeerAccess(src_dev_, 0);
     (void)hipGetLastError();
   }
-  slots_.resize(n_slots);
-  ready_.resize(n_slots);
-  freed_.resize(n_slots);
-  freed_valid_.assign(n_slots, false);
-  HIP_OK(hipSetDevice(dst_dev_));
-  for (int i = 0; i < n_slots; ++i) {
-    HIP_OK(hipMalloc(&slots_[i], slot_bytes_));
-    HIP_OK(hipEventCreateWithFlags(&freed_[i], hipEventDisableTiming));
-    free_.push_back(i);
-  }
   HIP_OK(hipSetDevice(src_dev_));
-  for (int i = 0; i < n_slots; ++i) HIP_OK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  HIP_OK(hipSetDevice(dst_dev_));
+  HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   HIP_OK(hipSetDevice(cur));
 }
 
 LocalLink::~LocalLink() {
-  for (size_t i = 0; i < slots_.size(); ++i) {
-    (void)hipFree(slots_[i]);
-    (void)hipEventDestroy(ready_[i]);
-    (void)hipEventDestroy(freed_[i]);
-  }
+  (void)hipEventDestroy(ready_);
+  (void)hipEventDestroy(done_);
 }
 
 void LocalLink::abort() {
@@ -68,49 +57,35 @@ void LocalLink::abort() {
 }
 
 void LocalLink::send(const void* buf, size_t bytes, hipStream_t st) {
-  if (bytes > slot_bytes_) throw std::runtime_error("LocalLink: message larger than slot");
-  int slot;
-  bool wait_freed;
-  {
-    std::unique_lock<std::mutex> l(mu_);
-    if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !free_.empty(); }))
-      throw std::runtime_error("LocalLink: send timed out (peer stalled)");
-    if (aborted_) throw std::runtime_error("LocalLink: aborted");
-    slot = free_.front();
-    free_.pop_front();
-    wait_freed = freed_valid_[slot];
-  }
-  if (wait_freed) HIP_OK(hipStreamWaitEvent(st, freed_[slot], 0));
-  HIP_OK(hipMemcpyAsync(slots_[slot], buf, bytes, hipMemcpyDefault, st));
-  HIP_OK(hipEventRecord(ready_[slot], st));
-  {
-    std::lock_guard<std::mutex> l(mu_);
-    q_.push_back({slot, bytes});
-    bytes_sent += bytes;
-    ++msgs_sent;
-  }
+  const auto to = std::chrono::milliseconds((long)(timeout_s * 1000));
+  std::unique_lock<std::mutex> l(mu_);
+  if (aborted_) throw std::runtime_error("LocalLink: aborted");
+  HIP_OK(hipEventRecord(ready_, st));
+  src_ = buf;
+  bytes_ = bytes;
+  const uint64_t me = ++posted_;
   cv_.notify_all();
+  // the receiver enqueues its copy of THIS message (taken_ == me) before the sender goes on
+  if (!cv_.wait_for(l, to, [&] { return aborted_ || taken_ >= me; }))
+    throw std::runtime_error("LocalLink: send timed out (peer stalled)");
+  if (aborted_) throw std::runtime_error("LocalLink: aborted");
+  // the sender's stream (and so its sent_ev) orders after the copy: the buffer is reusable
+  HIP_OK(hipStreamWaitEvent(st, done_, 0));
+  bytes_sent += bytes;
+  ++msgs_sent;
 }
 
 void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
-  Msg m;
-  {
-    std::unique_lock<std::mutex> l(mu_);
-    if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !q_.empty(); }))
-      throw std::runtime_error("LocalLink: recv timed out (peer stalled)");
-    if (aborted_) throw std::runtime_error("LocalLink: aborted");
-    m = q_.front();
-    q_.pop_front();
-  }
-  if (m.bytes != bytes) throw std::runtime_error("LocalLink: message size mismatch");
-  HIP_OK(hipStreamWaitEvent(st, ready_[m.slot], 0));
-  HIP_OK(hipMemcpyAsync(buf, slots_[m.slot], bytes, hipMemcpyDefault, st));
-  HIP_OK(hipEventRecord(freed_[m.slot], st));
-  {
-    std::lock_guard<std::mutex> l(mu_);
-    freed_valid_[m.slot] = true;
-    free_.push_back(m.slot);
-  }
+  std::unique_lock<std::mutex> l(mu_);
+  if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)),
+                    [&] { return aborted_ || posted_ > taken_; }))
+    throw std::runtime_error("LocalLink: recv timed out (peer stalled)");
+  if (aborted_) throw std::runtime_error("LocalLink: aborted");
+  if (bytes_ != bytes) throw std::runtime_error("LocalLink: message size mismatch");
+  HIP_OK(hipStreamWaitEvent(st, ready_, 0));
+  HIP_OK(hipMemcpyAsync(buf, src_, bytes, hipMemcpyDefault, st));
+  HIP_OK(hipEventRecord(done_, st));
+  ++taken_;
   cv_.notify_all();
 }
 

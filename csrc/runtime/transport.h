@@ -3,8 +3,9 @@
 // one DIRECTION between two stages; every op is stream-ordered (enqueued, not blocking the GPU
 // of the caller), so comm overlaps the compute of other micro-batches.
 //   - RcclLink:  ncclSend/ncclRecv on a 2-rank communicator per link (xGMI peer-to-peer).
-//   - LocalLink: same-process hand-off through a ring of device slots + HIP events (1-GPU
-//                emulation of PP=S, or in-process multi-GPU without RCCL).
+//   - LocalLink: same-process hand-off, ONE device copy per message: the receiver's stream
+//                copies straight out of the sender's buffer (peer read over xGMI when the two
+//                stages sit on different GPUs; 1-GPU emulation of PP=S when they share one).
 //   - TcpLink:   host sockets (cross-host parity with the reference's worker-over-TCP mode).
 // One communicator per direction and one stream per side make every link FIFO-consistent, so
 // the piped ring (activations forward, sampled tokens last -> first) is deadlock-free.
@@ -38,25 +39,29 @@ class Link {
 };
 
 // ---------------------------------------------------------------- LocalLink
+// A rendezvous: send() publishes (buffer, ready event) and blocks the sending HOST thread until
+// the receiver has enqueued its copy; it then makes the sender's stream wait for that copy, so
+// the engine's sent_ev (recorded after send) keeps the buffer alive exactly as long as needed.
+// Host threads only meet at enqueue points (the GPU work stays asynchronous), and every stage
+// issues its link operations in the global (round, micro-batch) order, so the ring cannot
+// deadlock on the rendezvous.  Both ends may be on the same device.
 class LocalLink : public Link {
  public:
-  // slots live on `dst_device`; both sides may be on the same device.
-  LocalLink(int src_device, int dst_device, size_t slot_bytes, int n_slots);
+  LocalLink(int src_device, int dst_device);
   ~LocalLink() override;
   void send(const void* buf, size_t bytes, hipStream_t st) override;
   void recv(void* buf, size_t bytes, hipStream_t st) override;
   const char* kind() const override { return "local"; }
   void abort() override;
+  bool peer() const { return src_dev_ != dst_dev_; }
 
  private:
-  struct Msg { int slot; size_t bytes; };
   int src_dev_, dst_dev_;
-  size_t slot_bytes_;
-  std::vector<void*> slots_;
-  std::vector<hipEvent_t> ready_, freed_;   // per slot
-  std::vector<bool> freed_valid_;
-  std::deque<int> free_;
-  std::deque<Msg> q_;
+  hipEvent_t ready_ = nullptr;   // on the sender's device: the message's bytes are final
+  hipEvent_t done_ = nullptr;    // on the receiver's device: the copy has completed
+  const void* src_ = nullptr;
+  size_t bytes_ = 0;
+  uint64_t posted_ = 0, taken_ = 0;   // message counters (posted_ - taken_ <= 1)
   std::mutex mu_;
   std::condition_variable cv_;
   bool aborted_ = false;

@@ -21,6 +21,7 @@ struct KnobDef {
 bool ns_ok(int v) { return v == 2 || v == 3 || v == 4; }
 bool nw_ok(int v) { return v == 4 || v == 8; }
 bool g_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; }
+bool bm_ok(int v) { return v == 0 || v == 128 || v == 256; }
 
 const KnobDef kDefs[KNOB_COUNT] = {
     {"ATTN_PF_MAXWG", 512, 0, 1 << 30, nullptr},   // r7v: mb256 np 61.3 vs PF 65.3 us/layer
@@ -36,8 +37,12 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"MOE_V", 2, 1, 2, nullptr},
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
-    {"GEMM3_PROBE", 0, 0, 7, nullptr},
-    {"ATTN_PROBE", 0, 0, 3, nullptr},
+    {"GEMM3_BM", 0, 0, 256, bm_ok},
+    {"GEMM3_BN", 0, 0, 256, bm_ok},
+    {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
+#ifdef MIPIPE_TIMING_PROBES
+#include "timing_probes.inc"
+#endif
 };
 
 std::atomic<int> g_vals[KNOB_COUNT];

@@ -22,8 +22,15 @@ enum Knob : int {
   KNOB_MOE_V,               // MoE GEMV version (1 | 2)
   KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
+  KNOB_GEMM3_BM,            // gemm3: force rows per workgroup (0 auto, 128, 256); A/B runs only
+  KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
+  KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
+#ifdef MIPIPE_TIMING_PROBES
+  // timing probes that skip work (wrong results): only in a `make PROBES=1` build, never in the
+  // default library, so no environment variable can corrupt a serving or bench run
   KNOB_GEMM3_PROBE,         // gemm3 timing probes (Q4_K SwiGLU 256x256 only; 0 = the real kernel)
   KNOB_ATTN_PROBE,          // decode attention timing probes (1: no V append, 2: no K append; 0 = real)
+#endif
   KNOB_COUNT
 };
 

@@ -190,7 +190,7 @@ def gemm_i8(w: I8Weight, x: torch.Tensor | None = None, epi: int = EPI_STORE, y:
 def set_gemm3_tuning(bm: int = 0, bn: int = 0, nsplit: int = 0, split_wg: int = 0) -> None:
     """Force the v3 GEMM's tile rows / columns (128 | 256) and ATOMIC split-K factor (0 = auto);
     split_wg: workgroup target of the automatic split (default 256)."""
-    N.lib().mp_set_gemm3_tuning(bm, bn, nsplit, split_wg)
+    N.check(N.lib().mp_set_gemm3_tuning(bm, bn, nsplit, split_wg), "set_gemm3_tuning")
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, k_pad: int | None = None) -> torch.Tensor:

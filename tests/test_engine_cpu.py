@@ -122,6 +122,32 @@ def test_cpu_synthetic_bench(native):
     assert r["decode_tok_s"] > 0 and r["p50_ms"] > 0
 
 
+def test_bench_py_inprocess_pipeline_cpu():
+    """`python bench.py --gpus 2` with no launcher (no WORLD_SIZE) runs a 2-stage pipeline in ONE
+    process (engine mode "local"), here on the CPU backend: one JSON line with 2 stages, N + 1
+    micro-batches, and the data plane the engine reports."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--same-device", "--model", "tinyllama",
+           "--ftype", "Q4_K_M", "--steps", "1", "--warmup", "0", "--mb-size", "1", "--prompt-len", "4",
+           "--set", "backend=cpu", "--set", "threads=4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "pp2"
+    assert d["config"]["micro_batches"] == 3 and len(d["config"]["stages"]) == 2
+    assert d["link"]["launcher"] == "in-process" and d["link"]["engine_mode"] == "local"
+    assert d["link"]["kind"] == ["host"] and d["link"]["links_per_rank"] == 4
+
+
+def test_bench_py_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=120, cwd=REPO, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
 _MP_SCRIPT = r"""
 import json, sys
 sys.path.insert(0, {repo!r})
@@ -464,6 +490,38 @@ def test_cpu_gpu_mem_sums_stages_sharing_a_device(native, model_dir):
     assert budget_mib < total
     assert need([0, 1], budget_mib / 1024) is None      # each GPU fits alone
     assert need([0, 0], budget_mib / 1024)[0] == "0,1"  # together they do not
+
+
+@pytest.mark.parametrize("source", ["synthetic", "gguf"])
+def test_int8_gemm_copies_count_in_memory_budget(native, model_dir, source):
+    """int8_gemm keeps an int8 copy of every quantized non-MoE projection (1 B per padded
+    weight + a float row scale); --gpu-mem (and the max_ctx auto KV budget, same accounting) must
+    see those bytes.  The check runs before any stage is built, so it is testable without a GPU."""
+    import re
+    from mipipe.engine import Engine
+    if source == "gguf":
+        path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+        kw = dict(gguf=path)
+        n_layer, d, f, hq, hkv = cfg.n_layer, cfg.d_model, cfg.d_ff, cfg.n_head, cfg.n_head_kv
+        hd = d // hq
+    else:
+        syn = dict(n_layer=3, d_model=512, n_head=8, n_head_kv=2, d_ff=1536, vocab=2048)
+        kw = dict(synthetic=syn, ftype="Q4_K")
+        n_layer, d, f, hq, hkv, hd = 3, 512, 1536, 8, 2, 64
+
+    def weights_mib(**extra):
+        with pytest.raises(RuntimeError) as ei:
+            Engine(max_ctx=128, gpu_mem_gib=1e-9, **kw, **extra)
+        m = re.search(r"weights ([\d.]+) \+ KV", str(ei.value))
+        assert m, str(ei.value)
+        return float(m.group(1))
+
+    pad = lambda n: (n + 15) // 16 * 16
+    padk = lambda k: (k + 255) // 256 * 256
+    mats = [(hq * hd, d), (hkv * hd, d), (hkv * hd, d), (d, hq * hd), (f, d), (f, d), (d, f)]
+    expect = n_layer * sum(pad(n) * padk(k) + pad(n) * 4 for n, k in mats) / 1048576.0
+    extra = weights_mib(int8_gemm=True) - weights_mib()
+    assert abs(extra - expect) < 0.01, (extra, expect)
 
 
 def test_cpu_device_speed_probe_partition(native, model_dir):

@@ -606,6 +606,53 @@ def test_bench_two_ranks_torchrun(cuda, native):
     assert d["link"]["kind"] == ["tcp"] and d["link"]["torch_pg_world"] == 2 and d["link"]["links_per_rank"] == 2
 
 
+@pytest.mark.parametrize("gpus,link", [(2, "auto"), (3, "rccl")])
+def test_bench_inprocess_same_device(cuda, native, gpus, link):
+    """`python bench.py --gpus N` WITHOUT a launcher runs PP=N in one process (engine mode "local",
+    one host thread per stage).  --same-device puts every stage on GPU 0: link auto picks the
+    peer-copy LocalLink; link rccl asks ncclCommInitAll for the pairs, RCCL refuses a duplicate GPU,
+    and the engine falls back to LocalLinks and says so in link.fallback."""
+    import json as _json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(gpus), "--same-device", "--link", link,
+           "--model", "tinyllama", "--ftype", "Q4_K_M", "--steps", "3", "--warmup", "1", "--mb-size", "4",
+           "--prompt-len", "16"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = _json.loads(lines[0])
+    assert d["n_gpus"] == gpus and d["value"] > 0 and "secondary" not in d
+    assert d["config"]["parallelism"] == f"pp{gpus}" and d["config"]["micro_batches"] == gpus + 1
+    assert len(d["config"]["stages"]) == gpus
+    L = d["link"]
+    assert L["launcher"] == "in-process" and L["engine_mode"] == "local" and L["devices"] == [0]
+    assert L["kind"] == ["local"] and L["comm_nranks"] == [0] and L["links_per_rank"] == 2 * gpus
+    assert L["act_dtype"] == "f32" and L["wire_bytes_per_token"] == 2048 * 4   # same GPU: f32 boundary
+    assert ("fallback" in L) == (link == "rccl")
+
+
+def test_local_link_single_copy_cross_stage(cuda, native, model_dir):
+    """The rendezvous LocalLink (one device copy per message, receiver reads the sender's buffer):
+    PP=3 on one GPU with 3 micro-batches and ring tokens generates what PP=1 generates."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    rng = np.random.default_rng(21)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (9, 3, 17, 5, 11, 2)]
+    with Engine(gguf=path, max_ctx=128, n_mb=3, mb_size=2, prefill_chunk=16) as eng:
+        ref, _ = eng.generate(prompts, 9)
+    with Engine(gguf=path, max_ctx=128, n_mb=3, mb_size=2, prefill_chunk=16, stages=3, devices=[0, 0, 0],
+                link="local", split="even") as eng:
+        out, _ = eng.generate(prompts, 9)
+        h = eng.health()
+    assert out == ref
+    assert all(s["link"] == "local" and s["msgs_sent"] > 0 for s in h["stages"])
+
+
 @pytest.mark.parametrize("stages", [1, 2])
 def test_continuous_batching(cuda, native, model_dir, stages):
     """HIP stages: sequences admitted between decode rounds (row-selective head, ring tokens,
