@@ -215,51 +215,21 @@ constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
 // the many-split long contexts need more (8B 32K mb8: 1019 vs 960 tok/s)
 // (t, kvh, z): token, kv head, KV split.  xo (LDS, one split only): the G heads' outputs of token
 // t land there, [r * hd + d], instead of p.out (the fused attention + o-projection kernel)
-template <int DP, bool F8, bool PF>
-__device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
-                                                 f16* xo = nullptr) {
-  using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
-  auto cvt = [](const KR& r) -> half8_t {
-    if constexpr (F8) return f8x8_to_h8(r);
-    else return r;
-  };
-  constexpr int KK = DP / 32;
-  constexpr int DT = DP / 16;
-  __shared__ float sm_m[4][16], sm_l[4][16];
-  __shared__ float sm_o[4][16][DP];
-  __shared__ float sm_mz[16][ATTN_MAX_SPLITS], sm_lz[16][ATTN_MAX_SPLITS];   // split merge
-  __shared__ int sm_last;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int q4 = lane >> 4, col = lane & 15;
-  const int G = p.Hq / p.Hkv;
+// q fragments of the G query heads of kv head kvh for token t with RoPE applied in registers:
+// lane (q4, col) holds q[h = kvh G + col][d = 32kk + 8q4 + j] (zero for col >= G).  Used by the
+// fused decode attention bodies (workgroup- and wave-level).
+template <int KK>
+__device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const float* row, const float2* cs, float nrs,
+                                               int kvh, int G, int q4, int col, half8_t (&qf)[KK]) {
   const int g = col;
   const bool rvalid = col < G;
-  const int pos = p.pos[t];
-  const int kvlen = pos + 1;
-  const int slot = p.slot[t];
   const int h = kvh * G + g;
-  const int hd2 = p.hd / 2;
-  const float* row = p.qkv + (size_t)t * p.ldqkv;
-  const float2* cs = p.rope_cs + (size_t)pos * hd2;
-  const int32_t* bt = p.block_table + (size_t)slot * p.max_pages;
-  // deferred RMSNorm of the projection GEMV: value i of q|k|v = nrs * row[i] + bias[i]
-  const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
   auto qkv_at = [&](int i) { return p.bias ? fmaf(nrs, row[i], p.bias[i]) : nrs * row[i]; };
-
-  const int start = z * p.split_len;
-  const int end = min(start + p.split_len, kvlen);
-  // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
-  // single active split writes the output directly, so short contexts pay no merge round trip
-  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
-  if (z >= n_act) return;
-
-  // 1. q fragments with RoPE applied in registers: lane holds q[h][d = 32kk + 8q4 + j].  Built
+  // q fragments with RoPE applied in registers: lane holds q[h][d = 32kk + 8q4 + j].  Built
   // before the append so its loads overlap the append's, and (head_dim % 8 == 0) from
   // unconditional 16-byte loads issued together: written as guarded scalar reads (qkv_at per
   // element) the compiler serialised ~32 dependent load round trips here, ~10 us of fixed cost per
   // call whatever the context (measured: 12.7 us at 20 keys, mb64).
-  half8_t qf[KK];
   if ((p.hd & 7) == 0) {
     const int hs = rvalid ? h : kvh * G;          // idle MFMA columns read a valid head, then zero
     // bias / no-bias as two straight-line bodies: a bias branch inside the loop split the loads
@@ -333,6 +303,50 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       qf[kk] = v;
     }
   }
+
+}
+
+template <int DP, bool F8, bool PF>
+__device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
+                                                 f16* xo = nullptr) {
+  using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
+  auto cvt = [](const KR& r) -> half8_t {
+    if constexpr (F8) return f8x8_to_h8(r);
+    else return r;
+  };
+  constexpr int KK = DP / 32;
+  constexpr int DT = DP / 16;
+  __shared__ float sm_m[4][16], sm_l[4][16];
+  __shared__ float sm_o[4][16][DP];
+  __shared__ float sm_mz[16][ATTN_MAX_SPLITS], sm_lz[16][ATTN_MAX_SPLITS];   // split merge
+  __shared__ int sm_last;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q4 = lane >> 4, col = lane & 15;
+  const int G = p.Hq / p.Hkv;
+  const int g = col;
+  const bool rvalid = col < G;
+  const int pos = p.pos[t];
+  const int kvlen = pos + 1;
+  const int slot = p.slot[t];
+  const int h = kvh * G + g;
+  const int hd2 = p.hd / 2;
+  const float* row = p.qkv + (size_t)t * p.ldqkv;
+  const float2* cs = p.rope_cs + (size_t)pos * hd2;
+  const int32_t* bt = p.block_table + (size_t)slot * p.max_pages;
+  // deferred RMSNorm of the projection GEMV: value i of q|k|v = nrs * row[i] + bias[i]
+  const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
+
+  const int start = z * p.split_len;
+  const int end = min(start + p.split_len, kvlen);
+  // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
+  // single active split writes the output directly, so short contexts pay no merge round trip
+  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
+  if (z >= n_act) return;
+
+  // 1. q fragments with RoPE applied in registers (decode_q_frags)
+  half8_t qf[KK];
+  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
 
   // 2. append the new token's K (rotated) and V to the cache.  The split that reads the new token
   // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
@@ -624,6 +638,273 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
   attn_decode_body<DP, F8, false>(p, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
+// ---------------------------------------------------------------- wave-level decode attention
+// Wide micro-batches (many (token, kv head) pairs): ONE WAVE per (token, kv head, split) streams its
+// keys chunk after chunk with the next chunk's K / V in flight, and owns the whole softmax state, so
+// there is no cross-wave LDS merge and no workgroup barrier; the 4 waves of a workgroup are 4
+// independent items (consecutive kv heads of a token: they share the position, block-table and q
+// row loads in L2).  The workgroup kernel above spends most of a 128-key context on fixed costs
+// (profiles/r7u: 2048 workgroups, waves 55 % of their life waiting on memory, the 4-wave merge);
+// here every wave has 32 KB of K / V in flight from its first chunk on.
+// Splits (few pairs, long contexts): partials + the last-arriving wave of the (token, kv head)
+// merges, with the same sc1 publish / counter / sc1 load hand-off as attn_decode_body.
+template <int DP, bool F8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_wave_kernel(const DecodeAttnParams p) {
+  using KR = std::conditional_t<F8, u32x2, half8_t>;
+  constexpr int KK = DP / 32, DT = DP / 16, EB = F8 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) f16 sm_kn[4][DP];
+  __shared__ f16 sm_vn[4][DP];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q4 = lane >> 4, col = lane & 15;
+  const int item = blockIdx.x * 4 + wv;
+  const int per_t = p.Hkv * p.n_split;
+  const int t = item / per_t;
+  if (t >= p.M) return;   // wave-uniform; no workgroup barrier anywhere below
+  const int kvh = (item - t * per_t) / p.n_split, z = item % p.n_split;
+  const int G = p.Hq / p.Hkv;
+  const int pos = p.pos[t];
+  const int kvlen = pos + 1;
+  const int start = z * p.split_len;
+  const int end = min(start + p.split_len, kvlen);
+  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
+  if (z >= n_act) return;
+  const int hd2 = p.hd / 2;
+  const float* row = p.qkv + (size_t)t * p.ldqkv;
+  const float2* cs = p.rope_cs + (size_t)pos * hd2;
+  const int32_t* bt = p.block_table + (size_t)p.slot[t] * p.max_pages;
+  const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
+  const int nch = (end - start + 31) / 32;
+  const int krow0 = 8 * (col >> 2) + (col & 3);
+
+  auto load = [&](int ci, KR (&kf)[2][KK], KR (&vf)[DT]) {
+    const int P0 = start + ci * 32;
+    const int page = bt[P0 >> 6];
+    const int in_page = P0 & 63;
+    const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
+    const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        kf[c][kk] = *reinterpret_cast<const KR*>(kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
+  };
+  KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
+  load(0, kA, vA);   // in flight during the q build and the append
+  if (nch > 1) load(1, kB, vB);
+
+  half8_t qf[KK];
+  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+
+  // the split holding the new position appends its K (rotated) / V and keeps them in this wave's
+  // LDS slice to patch the chunk that holds it (the chunk's loads may predate the append)
+  const bool owns = start <= pos && pos < end;
+  f16* kn = sm_kn[wv];
+  f16* vn = sm_vn[wv];
+  if (owns) {
+    const int page = bt[pos >> 6], idx = pos & 63;
+    const int kr = p.Hq * p.hd + kvh * p.hd;
+    const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
+    const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
+    const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
+#pragma unroll
+    for (int jj = 0; jj < DP / 128; ++jj) {   // K: one pair per lane per 128 dims
+      const int j = lane + 64 * jj;
+      const bool kin = j < hd2;
+      float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
+      if (kin) {
+        kx = *reinterpret_cast<const float2*>(row + kr + 2 * j);
+        c = cs[j];
+        if (p.bias) kb = *reinterpret_cast<const float2*>(p.bias + kr + 2 * j);
+      }
+      const float x0 = fmaf(nrs, kx.x, kb.x), x1 = fmaf(nrs, kx.y, kb.y);
+      const float r0 = kin ? x0 * c.x - x1 * c.y : 0.f, r1 = kin ? x0 * c.y + x1 * c.x : 0.f;
+      half2_t o;
+      if constexpr (F8) {
+        const uint32_t q = f8x2_pack(r0, r1);
+        *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(p.k_cache) + koff + 2 * j) = (uint16_t)q;
+        o = f8x2_lo(q);
+      } else {
+        o = half2_t{(f16)r0, (f16)r1};
+        *reinterpret_cast<half2_t*>(p.k_cache + koff + 2 * j) = o;
+      }
+      *reinterpret_cast<half2_t*>(kn + 2 * j) = o;
+    }
+#pragma unroll
+    for (int jj = 0; jj < DP / 64; ++jj) {    // V: one element per lane per 64 dims
+      const int j = lane + 64 * jj;
+      const bool vin = j < p.hd;
+      const float vv = vin ? fmaf(nrs, row[vr + j], p.bias ? p.bias[vr + j] : 0.f) : 0.f;
+      f16 v;
+      if constexpr (F8) {
+        const uint32_t q = f8x2_pack(vv, 0.f);
+        reinterpret_cast<uint8_t*>(p.v_cache)[voff + (size_t)j * 64] = (uint8_t)q;
+        v = f8x2_lo(q).x;
+      } else {
+        v = (f16)vv;
+        p.v_cache[voff + (size_t)j * 64] = v;
+      }
+      vn[j] = v;
+    }
+  }
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto step_h = [&](int ci, half8_t (&kf)[2][KK], half8_t (&vf)[DT]) {
+    const int P0 = start + ci * 32;
+    if (owns && pos >= P0 && pos < P0 + 32) {   // wave-uniform
+      const int r = pos - P0;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (krow0 + 4 * c == r) {
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) kf[c][kk] = *reinterpret_cast<const half8_t*>(kn + 32 * kk + 8 * q4);
+        }
+      if ((r >> 3) == q4) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const f16 v = vn[16 * dt + col];
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (e == (r & 7)) vf[dt][e] = v;
+        }
+      }
+    }
+    f32x4 sc[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) a = mfma16x16x32(kf[c][kk], qf[kk], a);
+      sc[c] = a;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kpos = P0 + 8 * q4 + 4 * c + i;
+        const float v = kpos < end ? sc[c][i] : -INFINITY;
+        sc[c][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
+    float pv[2][4];
+    float psum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = (m_new == -INFINITY) ? 0.f : __expf(sc[c][i] - m_new);
+        pv[c][i] = e;
+        psum += e;
+      }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+    half8_t pf = {(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
+                  (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+  };
+  // f16 pages: the loaded registers are used (and patched) in place; e4m3: converted at use
+  auto step = [&](int ci, KR (&kraw)[2][KK], KR (&vraw)[DT]) {
+    if constexpr (F8) {
+      half8_t kf[2][KK], vf[DT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) kf[c][kk] = f8x8_to_h8(kraw[c][kk]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) vf[dt] = f8x8_to_h8(vraw[dt]);
+      step_h(ci, kf, vf);
+    } else {
+      step_h(ci, kraw, vraw);
+    }
+  };
+  // two chunks in flight: chunk ci + 2 is loaded into the registers chunk ci frees
+  for (int ci = 0; ci < nch;) {
+    step(ci, kA, vA);
+    if (ci + 2 < nch) load(ci + 2, kA, vA);
+    if (++ci >= nch) break;
+    step(ci, kB, vB);
+    if (ci + 2 < nch) load(ci + 2, kB, vB);
+    ++ci;
+  }
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+  // lane (q4, col) holds O^T[d = 16 dt + 4 q4 + i][head col]
+  const int h = kvh * G + col;
+  const size_t rid = (size_t)t * p.Hq + h;
+  if (n_act == 1) {
+    if (col < G) {
+      const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int d = 16 * dt + 4 * q4;
+        if (d < p.hd) {
+          typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+          const half4_t v = {(f16)(o[dt][0] * inv), (f16)(o[dt][1] * inv), (f16)(o[dt][2] * inv), (f16)(o[dt][3] * inv)};
+          *reinterpret_cast<half4_t*>(p.out + (size_t)t * p.ldo + h * p.hd + d) = v;
+        }
+      }
+    }
+    return;
+  }
+  // publish this split's partials (sc1 write-through), then one counter add per wave
+  const size_t stride = (size_t)p.M * p.Hq;
+  if (col < G) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st_sc1(p.o_part + ((size_t)z * stride + rid) * DP + 16 * dt + 4 * q4 + i, o[dt][i]);
+    if (q4 == 0) {
+      st_sc1(p.ml_part + ((size_t)z * stride + rid) * 2, m_run);
+      st_sc1(p.ml_part + ((size_t)z * stride + rid) * 2 + 1, l_run);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0)
+    old = __hip_atomic_fetch_add(p.counters + (size_t)t * p.Hkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0);
+  if (old != n_act - 1) return;
+  // last arriver: lane (q4, col) merges head col's dims 16 dt + 4 q4 + i over the splits
+  if (col < G) {
+    float M = -INFINITY;
+    for (int zz = 0; zz < n_act; ++zz) M = fmaxf(M, ld_sc1(p.ml_part + (zz * stride + rid) * 2));
+    float L = 0.f;
+    f32x4 acc[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int zz = 0; zz < n_act; ++zz) {
+      const float mz = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
+      const float f = mz == -INFINITY ? 0.f : __expf(mz - M);
+      L += ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1) * f;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[dt][i] += f * ld_sc1(p.o_part + (zz * stride + rid) * DP + 16 * dt + 4 * q4 + i);
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = 16 * dt + 4 * q4 + i;
+        if (d < p.hd) p.out[(size_t)t * p.ldo + h * p.hd + d] = (f16)(acc[dt][i] * inv);
+      }
+  }
+  if (lane == 0)
+    __hip_atomic_store(p.counters + (size_t)t * p.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // global -> LDS DMA, 16 B per active lane to (wave-uniform LDS base) + lane * 16 (gemm3.hip glds;
 // inline asm so the compiler's waitcnt pass does not drain it at the next ds_read)
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
@@ -763,7 +1044,26 @@ void launch_attn_o(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t 
   }
 }
 
+bool attn_decode_wave_selected(const DecodeAttnParams& p) {
+  const int mode = knob(KNOB_ATTN_WAVE);   // 0 off, 1 on, 2 auto
+  if (mode == 0) return false;
+  if (mode == 1) return true;
+  return (int64_t)p.M * p.Hkv * p.n_split >= knob(KNOB_ATTN_WAVE_MIN);
+}
+
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
+  if (attn_decode_wave_selected(p)) {
+    const int items = p.M * p.Hkv * p.n_split;
+    const dim3 grid((items + 3) / 4);
+    if (p.Dp == 128) {
+      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
+    } else {
+      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, false>), grid, dim3(256), 0, st, p);
+    }
+    return;
+  }
   // the next-chunk prefetch variant (2 workgroups per CU) for a single split per (token, kv head)
   // while the grid is small; many workgroups (long contexts, or wide micro-batches: M * Hkv above
   // MIPIPE_ATTN_PF_MAXWG) need occupancy more than per-wave latency: the 3-per-CU variant

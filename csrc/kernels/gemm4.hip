@@ -1,0 +1,561 @@
+// Dequant GEMM v4: gemm3's LDS-DMA pipeline on the 32x32x16 MFMA (M > 64: wide decode micro-batches
+// and prompt chunks).
+//
+// Y[M][N] (+)= X[M][K] W[N][K]^T with W in the T16 packed quant layout (csrc/runtime/qtypes.h).
+// Workgroup tile BM (128 | 256) rows x 256 columns, 8 waves; every wave OWNS 32 columns (two T16
+// tiles) for all BM rows and runs v_mfma_f32_32x32x16_f16 on them: per 64-k stage BM/32 x 4
+// MFMAs, each fed by ONE A-fragment ds_read_b128 and one register B fragment.
+//
+// Why 32x32x16 (gemm3 runs 16x16x32, the same FLOP per A byte): an MFMA of this shape occupies its
+// SIMD for 32 cycles and blocks vector issue for 8 of them (MI355X_MICROARCH.md, issue-cost row),
+// so per FLOP there are 1.5x the free issue cycles of the 16x16x32 form, and half the MFMA, wait and
+// A-read instructions.  gemm3's PMC (profiles/r6b) shows the wave stream issue-bound (39 % of wave
+// cycles waiting on issue, MFMA busy 46 %) with the Q4_K dequant and the A reads competing for the
+// 8 free cycles of every 16-cycle MFMA.
+//
+// Lane mapping of the 32x32x16 operands (lane l, h = l >> 5, c = l & 31):
+//   A (x):        row c of the 32-row fragment, k = 64 q + 32 kk + 16 h + 8 e + j  (t = 2 kk + e)
+//   B (weights):  column c = tile (c >> 4), row (c & 15) of that tile, the same k: dword 2 h + e of
+//                 the T16 piece (kk, row) -- so one ds_read_b64 fetches both MFMAs' quants of a kk
+//   C:            column c, row 8 (v >> 2) + 4 h + (v & 3) of the 16 accumulators v
+// The k permutation inside a 32-k half (A and B index it the same way) is all a dot product needs,
+// and the sub-block scale of MFMA t (k-half kk) is uniform over the lanes.
+//
+// The x image, the raw weight images and the 3-stage counted-vmcnt / counted-lgkmcnt stream are
+// gemm3's (gemm_lds.h); see gemm3.hip for the pipeline's invariants.
+#include "gemm_lds.h"
+#include "../runtime/tuning.h"
+
+#include <algorithm>
+
+namespace mpk {
+using namespace mp;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <bool BF>
+__device__ __forceinline__ f32x16 mma32(half8_t a, half8_t b, f32x16 c) {
+  if constexpr (BF)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// Per-type reads of one wave's raw stage image (W3<PT>::issue layout, TW = 2) in the 32x32 mapping.
+template <int PT> struct W4;
+
+template <> struct W4<P_Q4_K> {
+  static constexpr int NR = 3;   // LDS reads per stage per lane
+  struct Raw { u32x4 hdr; u32x2 q[2]; };
+  struct Prep { half2_t S2, M2; };
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
+    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+    ds_b128(w.hdr, R + 2 * 512 + (u * 16 + r) * 16);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
+  }
+  __device__ static __forceinline__ Prep prep(const Raw& w, int q) {
+    Prep p;
+    kq_scales(w.hdr, (uint32_t)q, p.S2, p.M2);
+    return p;
+  }
+  __device__ static __forceinline__ half8_t frag(const Raw& w, const Prep& p, int t, int, const Consts& k) {
+    const int kk = t >> 1, e = t & 1;
+    return nib8(w.q[kk][e], kk ? h2hi(p.S2) : h2lo(p.S2), kk ? h2hi(p.M2) : h2lo(p.M2), k);
+  }
+};
+
+// Q6_K: quants [u][h][r] 16 B (dwords 2h, 2h+1 = one b64), high bits [u][kk][r] 8 B (the 2-bit
+// pairs of dword g live in its 16-bit half g & 1... of dword g >> 1: one b32 per kk), int8 scales
+// [u][r] (dword q), d [u][r]
+template <> struct W4<P_Q6_K> {
+  static constexpr int NR = 6;
+  struct Raw { uint32_t sc, d; u32x2 q[2]; uint32_t qd[2]; };
+  struct Prep { uint32_t sc; f16 d; };
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
+    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+    ds_b32(w.sc, R + 2 * 768 + (u * 16 + r) * 4);
+    ds_u16(w.d, R + 2 * 832 + (u * 16 + r) * 2);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
+      // high bits of dwords g = 2h, 2h+1: the 16-bit halves 0, 1 of dword (g >> 1) = h
+      ds_b32(w.qd[kk], R + 2 * 512 + ((u * 2 + kk) * 16 + r) * 8 + 4 * h);
+    }
+  }
+  __device__ static __forceinline__ Prep prep(const Raw& w, int) {
+    return Prep{w.sc ^ 0x80808080u, __builtin_bit_cast(f16, (uint16_t)w.d)};
+  }
+  __device__ static __forceinline__ half8_t frag(const Raw& w, const Prep& p, int t, int h, const Consts& k) {
+    const int kk = t >> 1, e = t & 1;   // dword g = 2h + e: high bits in half e of qd[kk]
+    const uint32_t h16 = (w.qd[kk] >> (16 * e)) & 0xFFFFu;
+    // int8 scale of sub-block 4q + 2kk + (g >> 1) = 4q + 2kk + h: byte 2kk + h of the dword
+    const uint32_t sb = (p.sc >> (8 * (2 * kk + h))) & 0xFFu;
+    const f16 sf = (as_h2(0x6400u | sb).x - (f16)1152.f) * p.d;
+    const half2_t S = half2_t{sf, sf};
+    const uint32_t x = h16 | (h16 << 8);
+    const uint32_t v = w.q[kk][e], tt = v >> 8;
+    const uint32_t h0 = ((x << 4) & 0x00300030u) | k.mag_hi, h1 = ((x << 6) & 0x03000300u) | k.mag_lo;
+    const uint32_t h2 = (x & 0x00300030u) | k.mag_hi, h3 = ((x << 2) & 0x03000300u) | k.mag_lo;
+    return pack8(as_u32((as_h2(and_or(v, k.mlo, h0)) - h2c(1056.f)) * S),
+                 as_u32((as_h2(and_or(v, k.mhi, h1)) - h2c(96.f)) * S),
+                 as_u32((as_h2(and_or(tt, k.mlo, h2)) - h2c(1056.f)) * S),
+                 as_u32((as_h2(and_or(tt, k.mhi, h3)) - h2c(96.f)) * S));
+  }
+};
+
+// Q5_K: quants as Q4_K, high-bit dword [u][kk][r] (byte g = dword g's 8 high bits), header [u][r]
+template <> struct W4<P_Q5_K> {
+  static constexpr int NR = 5;
+  struct Raw { u32x4 hdr; u32x2 q[2]; uint32_t qh[2]; };
+  struct Prep { half2_t S2, M2; };
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
+    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+    ds_b128(w.hdr, R + 2 * 640 + (u * 16 + r) * 16);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
+      ds_b32(w.qh[kk], R + 2 * 512 + ((u * 2 + kk) * 16 + r) * 4);
+    }
+  }
+  __device__ static __forceinline__ Prep prep(const Raw& w, int q) {
+    Prep p;
+    kq_scales(w.hdr, (uint32_t)q, p.S2, p.M2);
+    return p;
+  }
+  __device__ static __forceinline__ half8_t frag(const Raw& w, const Prep& p, int t, int h, const Consts& k) {
+    const int kk = t >> 1, e = t & 1, g = 2 * h + e;
+    const uint32_t hb = (w.qh[kk] >> (8 * g)) & 0xFFu;
+    const uint32_t x = hb | (hb << 12);
+    const half2_t S = kk ? h2hi(p.S2) : h2lo(p.S2), M = kk ? h2hi(p.M2) : h2lo(p.M2);
+    const uint32_t v = w.q[kk][e], tt = v >> 8;
+    const uint32_t h0 = ((x << 4) & 0x00100010u) | k.mag_hi, h1 = ((x << 7) & 0x01000100u) | k.mag_lo;
+    const uint32_t h2 = ((x << 2) & 0x00100010u) | k.mag_hi, h3 = ((x << 5) & 0x01000100u) | k.mag_lo;
+    return pack8(as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mlo, h0)) - h2c(1024.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mhi, h1)) - h2c(64.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(tt, k.mlo, h2)) - h2c(1024.f), S, M)),
+                 as_u32(__builtin_elementwise_fma(as_h2(and_or(tt, k.mhi, h3)) - h2c(64.f), S, M)));
+  }
+};
+
+// Q8_0: piece (u, kk, r) = 32 int8 (+128) at R + ((u*2 + kk)*16 + r)*32; bytes 16h .. 16h+15 hold
+// dwords g = 2h, 2h+1 of the 16x16 map (one b128 per kk); block scales [u][r] = (d(2q), d(2q+1))
+template <> struct W4<P_Q8_0> {
+  static constexpr int NR = 3;
+  struct Raw { uint32_t dd; u32x4 v[2]; };
+  struct Prep { uint32_t dd; };
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
+    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+    ds_b32(w.dd, R + 2 * 1024 + (u * 16 + r) * 4);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) ds_b128(w.v[kk], R + ((u * 2 + kk) * 16 + r) * 32 + 16 * h);
+  }
+  __device__ static __forceinline__ Prep prep(const Raw& w, int) { return Prep{w.dd}; }
+  __device__ static __forceinline__ half8_t frag(const Raw& w, const Prep& p, int t, int, const Consts&) {
+    const int kk = t >> 1, e = t & 1;
+    const uint32_t lo = e ? w.v[kk].z : w.v[kk].x, hi = e ? w.v[kk].w : w.v[kk].y;
+    const half2_t off = h2c(1152.f);
+    const half2_t S = kk ? h2hi(as_h2(p.dd)) : h2lo(as_h2(p.dd));
+    return pack8(as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u)) - off) * S),
+                 as_u32((as_h2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u)) - off) * S));
+  }
+};
+
+// 16-bit weights: the raw image holds [u][kk][lane16] 16-B fragment pieces of the 16x16 mapping
+// (element 4 kk + g of lane (q, r)): piece g of (u, kk, r) = k 32 kk + 8 g + j -- the 32x32 lane
+// (h, c) of MFMA t needs piece g = 2h + e of (u, kk, r)
+template <int PT> struct W4_16 {
+  static constexpr int NR = 4;
+  struct Raw { u32x4 v[4]; };
+  struct Prep {};
+  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
+    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kk = t >> 1, g = 2 * h + (t & 1);
+      ds_b128(w.v[t], R + (u * 2 + kk) * 1024 + (16 * g + r) * 16);
+    }
+  }
+  __device__ static __forceinline__ Prep prep(const Raw&, int) { return Prep{}; }
+  __device__ static __forceinline__ half8_t frag(const Raw& w, const Prep&, int t, int, const Consts&) {
+    return __builtin_bit_cast(half8_t, w.v[t]);
+  }
+};
+template <> struct W4<P_F16> : W4_16<P_F16> {};
+template <> struct W4<P_BF16> : W4_16<P_BF16> {};
+
+template <int PT> constexpr bool g4_supported() {
+  return PT == P_Q4_K || PT == P_Q5_K || PT == P_Q6_K || PT == P_Q8_0 || PT == P_F16 || PT == P_BF16;
+}
+
+// MoE mode (grouped GEMM over the routed experts): blockIdx.z = expert e, whose rows are
+// the token slots the router listed for it (lists[e][0 .. counts[e])); row blocks past counts[e]
+// exit at once.  The A staging gathers those rows (LDS-DMA addresses are per lane, so the gather
+// costs nothing), the weights are expert e's, and the epilogues scatter by slot: SwiGLU into
+// H[slot], down weighted by the router weight into Y[token] (atomics; per-slot rows in the
+// deterministic mode, combined in slot order by launch_moe_combine).
+struct G4Moe {
+  const int32_t* counts = nullptr;
+  const int32_t* lists = nullptr;
+  int list_cap = 0;
+  size_t estride = 0;
+  int k = 1, x_per_slot = 0;
+  const float* weights = nullptr;
+  float* Yslot = nullptr;
+};
+
+template <int PT, int EPI, int BM, bool MOE>
+__global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
+                                                    const int n_stages, const G4Moe mo) {
+  constexpr int TW = 2;
+  using Q3 = W3<PT>;
+  using Q = W4<PT>;
+  using G = G3Geom<PT, BM, TW>;
+  constexpr int NB = G::NB, FR = BM / 32, BN = 256;
+  constexpr bool BF = PT == P_BF16;
+  static_assert(NB == 3, "gemm4: the cross-stage stream needs 3 stage buffers");
+  __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware logical id (bijective for any grid size): consecutive ids (the row blocks of one
+  // column group) share an XCD and its L2
+  const int nwg = gridDim.x, bx = blockIdx.x;
+  const int xcd = bx & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
+  const int cg = lid / n_mb, mb = lid - cg * n_mb;
+  const int m0 = mb * BM;
+  const int s_begin = blockIdx.y * st_per_split;
+  const int s_end = min(s_begin + st_per_split, n_stages);
+  if (s_begin >= s_end) return;   // uniform over the workgroup
+  int M = p.M;
+  const int32_t* list = nullptr;
+  const uint8_t* Wbase = p.W;
+  if constexpr (MOE) {
+    const int e = blockIdx.z;
+    M = mo.counts[e];
+    if (m0 >= M) return;   // uniform: this expert has fewer routed rows
+    list = mo.lists + (size_t)e * mo.list_cap;
+    Wbase += (size_t)e * mo.estride;
+  }
+
+  W3Src src;
+  src.W = Wbase; src.t0 = cg * (BN / 16) + wave * TW; src.ntiles = p.ntiles; src.nsb = p.nsb;
+  auto stage_a = [&](int b) { return smem + b * G::STAGE; };
+  auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
+  // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7 (swizzled on the source side):
+  // each lane's source row pointers are fixed for the whole K loop (MoE: the gathered rows)
+  const char* xsrc[G::A_INSTR];
+#pragma unroll
+  for (int i = 0; i < G::A_INSTR; ++i) {
+    const int row = 8 * (wave * G::A_INSTR + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ g3_swz(row);
+    int gr = min(m0 + row, M - 1);
+    if constexpr (MOE) {
+      const int slot = list[gr];
+      gr = mo.x_per_slot ? slot : slot / mo.k;
+    }
+    xsrc[i] = reinterpret_cast<const char*>(p.X) + (size_t)gr * p.ldx * 2 + 16 * ch;
+  }
+  auto issue_a = [&](int s, int b) {
+#pragma unroll
+    for (int i = 0; i < G::A_INSTR; ++i) glds<16>(xsrc[i] + s * 128, stage_a(b) + (wave * G::A_INSTR + i) * 1024);
+  };
+  auto issue_b = [&](int s, int b) {
+    src.sb = s / 4; src.q = s % 4;
+    Q3::template issue<TW>(stage_r(b), src, lane);
+  };
+  constexpr int NIB = Q3::NI(TW);
+
+  f32x16 acc[FR];
+#pragma unroll
+  for (int i = 0; i < FR; ++i)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+  const Consts kc = make_consts();
+  const int h = lane >> 5, cl = lane & 31;
+  // per-lane byte offset of A fragment (t, row cl) inside a stage image; row 32 i + cl adds 4096 i
+  uint32_t aoff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) aoff[t] = (uint32_t)g3_off(cl, 4 * (t >> 1) + 2 * h + (t & 1));
+
+  constexpr int NA = 4 * FR, AD = 8, NR = Q::NR, JB = NA - AD - 1;
+  static_assert(JB > FR / 2 && NA - AD > JB, "gemm4: barrier step");
+  typename Q::Raw raw;
+  typename Q::Prep pr;
+  half8_t bf[4];
+  u32x4 af[NA];
+  auto read_a = [&](auto jc, u32x4& dst, int b) {
+    constexpr int j = decltype(jc)::value;
+    ds_b128o<(j % FR) * 4096>(dst, lds_addr(stage_a(b)) + aoff[j / FR]);
+  };
+
+  // prologue: stages 0, 1 (and 2's weights) in flight; stage 0's raw, first AD fragments, frag 0
+  issue_a(s_begin, 0);
+  issue_b(s_begin, 0);
+  issue_a(min(s_begin + 1, s_end - 1), 1);
+  issue_b(min(s_begin + 1, s_end - 1), 1);
+  issue_b(min(s_begin + 2, s_end - 1), 2);
+  wait_vmcnt<G::A_INSTR + 2 * NIB>();
+  __builtin_amdgcn_s_barrier();
+  Q::load(stage_r(0), lane, raw);
+  static_for<AD>([&](auto jc) { read_a(jc, af[decltype(jc)::value], 0); });
+  wait_lgkm<AD>();   // raw in (the oldest reads)
+  pr = Q::prep(raw, s_begin & 3);
+  bf[0] = Q::frag(raw, pr, 0, h, kc);
+
+  using RawT = typename Q::Raw;
+  using PrepT = typename Q::Prep;
+  auto stage = [&](const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n, PrepT& pr,
+                   PrepT& pr_n) {
+    const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;   // buffers of stages s+1, s+2 (= s-1)
+    static_for<NA>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int t = j / FR, i = j % FR;
+      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (j > JB ? NR + (j - JB - 1) : 0);
+      wait_lgkm<(later < 15 ? later : 15)>();
+      acc[i] = mma32<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[t], acc[i]);
+      if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], b);
+      // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
+      // stage's value was FR steps ago)
+      if constexpr (i == FR / 2 && t < 3) bf[t + 1] = Q::frag(raw, pr, t + 1, h, kc);
+      if constexpr (j == JB) {
+        wait_vmcnt<NIB>();   // x(s+1) and w(s+1) in: only w(s+2) (issued after x(s+1)) may be in flight
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue_a(min(s + 2, s_end - 1), b2);
+        issue_b(min(s + 3, s_end - 1), b);
+        Q::load(stage_r(b1), lane, raw_n);
+      }
+      if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
+      if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
+        wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
+        pr_n = Q::prep(raw_n, (s + 1) & 3);
+        bf[0] = Q::frag(raw_n, pr_n, 0, h, kc);   // (bf[0] of stage s: last use at j = FR - 1)
+      }
+    });
+  };
+  u32x4 afB[NA];
+  RawT rawB;
+  PrepT prB;
+  int s = s_begin, b = 0;
+  for (; s + 1 < s_end; s += 2) {
+    stage(s, b, af, afB, raw, rawB, pr, prB);
+    b = b == 2 ? 0 : b + 1;
+    stage(s + 1, b, afB, af, rawB, raw, prB, pr);
+    b = b == 2 ? 0 : b + 1;
+  }
+  if (s < s_end) stage(s, b, af, afB, raw, rawB, pr, prB);
+  wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
+  wait_lgkm<0>();
+
+  // epilogue: lane holds C[row 32 i + 8 (v >> 2) + 4 h + (v & 3)][col cl] of the wave's 32 columns
+  const int n = cg * BN + wave * 32 + cl;
+  const int rowb = m0 + 4 * h;
+  if constexpr (EPI == EPI_SWIGLU) {
+    const int o = (n >> 4) * 8 + (cl & 15);   // tile rows 0-7 gate, 8-15 up of the same 8 outputs
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float other = __shfl_xor(acc[i][v], 8);
+        const int m = rowb + 32 * i + 8 * (v >> 2) + (v & 3);
+        if ((cl & 8) == 0 && m < M && o < p.n_valid) {
+          const int hr = MOE ? list[m] : m;   // MoE: the slot's row of H
+          p.H[(size_t)hr * p.ldh + o] = sat_f16(silu(acc[i][v]) * other);
+        }
+      }
+  } else {
+    if (n < p.n_valid) {
+      const float bias = (p.bias && blockIdx.y == 0) ? p.bias[n] : 0.f;
+      float* Y = p.Y + (size_t)blockIdx.y * p.split_stride + n;
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int m = rowb + 32 * i + 8 * (v >> 2) + (v & 3);
+          if (m < M) {
+            if constexpr (MOE) {   // down projection: weighted into the slot's token (or its own row)
+              const int slot = list[m];
+              const float wv = mo.weights[slot] * acc[i][v];
+              if (mo.Yslot) mo.Yslot[(size_t)slot * p.ldy + n] = wv;
+              else unsafeAtomicAdd(p.Y + (size_t)(slot / mo.k) * p.ldy + n, wv);
+            } else if constexpr (EPI == EPI_ATOMIC) {
+              unsafeAtomicAdd(Y + (size_t)m * p.ldy, acc[i][v] + bias);
+            } else {
+              Y[(size_t)m * p.ldy] = acc[i][v] + bias;
+            }
+          }
+        }
+    }
+  }
+}
+
+}  // namespace mpk
+
+namespace mp {
+
+bool gemm4_supported(int ptype);
+
+// K splits of a gemm4 launch: enough workgroups for one round over the 256 CUs (one 8-wave
+// workgroup per CU: the 3-stage LDS ring takes ~130 KB), >= 16 stages (1024 k) per split
+static int g4_splits(int wgs, int n_stages) {
+  const int target = knob(KNOB_GEMM2_SPLIT_WG);
+  if (wgs >= target) return 1;
+  return std::max(1, std::min(target / wgs, n_stages / 16));
+}
+
+template <int PT, int EPI, int BM, bool MOE = false>
+static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe& mo = mpk::G4Moe{}, int E = 1) {
+  const int n_cg = (p.ntiles + 15) / 16;
+  const int n_mb = (p.M + BM - 1) / BM;   // MoE: p.M = the most rows one expert can get
+  const int n_stages = p.nsb * 4;
+  nsplit = std::max(1, std::min(nsplit, n_stages));
+  const int per = (n_stages + nsplit - 1) / nsplit;
+  nsplit = (n_stages + per - 1) / per;
+  hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE>), dim3(n_cg * n_mb, nsplit, E), dim3(512), 0, st, p, n_mb,
+                     per, n_stages, mo);
+}
+
+// rows per workgroup: 256 unless one 128-row block holds M (16-bit weights: always 128, their raw
+// stage images leave no room for three 256-row x images in LDS)
+static int g4_bm(int ptype, int M) {
+  if (is16(ptype)) return 128;
+  return knob(KNOB_GEMM3_BM) ? knob(KNOB_GEMM3_BM) : (M <= 128 ? 128 : 256);
+}
+
+template <int PT, int EPI>
+static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
+  if constexpr (is16(PT)) gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  else if (g4_bm(PT, p.M) == 128) gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  else gemm4_go<PT, EPI, 256>(p, nsplit, st);
+}
+
+template <int PT>
+static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, float* scratch, size_t scratch_n,
+                     int* nsplit_out) {
+  if constexpr (!mpk::g4_supported<PT>()) {
+    return false;
+  } else {
+    const int bm = g4_bm(PT, p.M);
+    const int wgs = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
+    const int n_stages = p.nsb * 4;
+    int ns = 1;
+    if (scratch) {   // split-K partial stores: split s writes scratch + s * M * ldp
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+      const int per = (n_stages + ns - 1) / ns;
+      ns = (n_stages + per - 1) / per;
+      const int ldp = p.ntiles * 16;
+      if (ns < 2 || (size_t)ns * p.M * ldp > scratch_n) return false;
+      p.Y = scratch; p.ldy = ldp; p.split_stride = (int64_t)p.M * ldp;
+      *nsplit_out = ns;
+      gemm4_bm<PT, EPI_STORE>(p, ns, st);
+      return true;
+    }
+    if (epi == EPI_ATOMIC && allow_split) ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+    switch (epi) {
+      case EPI_STORE: gemm4_bm<PT, EPI_STORE>(p, 1, st); break;
+      case EPI_ATOMIC: gemm4_bm<PT, EPI_ATOMIC>(p, ns, st); break;
+      case EPI_SWIGLU: gemm4_bm<PT, EPI_SWIGLU>(p, 1, st); break;
+    }
+    return true;
+  }
+}
+
+static bool gemm4_dispatch(int ptype, int epi, const GemvParams& p, bool allow_split, hipStream_t st, float* scratch,
+                           size_t scratch_n, int* ns) {
+  switch (ptype) {
+    case P_Q4_K: return gemm4_pt<P_Q4_K>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    case P_Q5_K: return gemm4_pt<P_Q5_K>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    case P_Q8_0: return gemm4_pt<P_Q8_0>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    case P_Q6_K: return gemm4_pt<P_Q6_K>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    case P_F16: return gemm4_pt<P_F16>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    case P_BF16: return gemm4_pt<P_BF16>(epi, p, allow_split, st, scratch, scratch_n, ns);
+    default: return false;
+  }
+}
+
+int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
+  if (!gemm4_supported(ptype)) return 1;
+  const int bm = g4_bm(ptype, M);
+  const int wgs = (ntiles + 15) / 16 * ((M + bm - 1) / bm);
+  const int n_stages = nsb * 4;
+  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+  ns = std::max(1, std::min(ns, n_stages));
+  const int per = (n_stages + ns - 1) / ns;
+  return (n_stages + per - 1) / per;
+}
+
+bool gemm4_supported(int ptype) {
+  return ptype == P_Q4_K || ptype == P_Q5_K || ptype == P_Q6_K || ptype == P_Q8_0 || ptype == P_F16 || ptype == P_BF16;
+}
+
+bool launch_gemm4(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split) {
+  int ns = 0;
+  return gemm4_dispatch(ptype, epi, p, allow_split, st, nullptr, 0, &ns);
+}
+
+// Grouped MoE GEMM (K13): p.M = tokens of the call (the most rows one expert can receive)
+template <int PT, int EPI>
+static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
+  GemvParams p{};
+  p.W = q.W; p.X = q.X; p.ldx = q.ldx; p.M = q.M; p.Y = q.Y; p.ldy = q.ldy; p.H = q.H; p.ldh = q.ldh;
+  p.ntiles = q.ntiles; p.nsb = q.nsb; p.n_valid = q.n_valid;
+  mpk::G4Moe mo;
+  mo.counts = q.counts; mo.lists = q.lists; mo.list_cap = q.list_cap; mo.estride = q.estride; mo.k = q.k;
+  mo.x_per_slot = q.x_per_slot; mo.weights = q.weights; mo.Yslot = q.Yslot;
+  // row tile from the mean rows per expert (M k / E); split-K (down, atomics only) for the grid the
+  // ACTIVE row blocks form
+  const int avg = std::max(1, q.M * q.k / std::max(1, q.E));
+  const int n_cg = (q.ntiles + 15) / 16;
+  if constexpr (is16(PT)) {
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
+    gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
+  } else if (avg <= 128) {
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
+    gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
+  } else {
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 255) / 256), q.nsb * 4) : 1;
+    gemm4_go<PT, EPI, 256, true>(p, ns, st, mo, q.E);
+  }
+}
+
+template <int PT>
+static bool moe4_pt(int epi, const MoeGemvParams& q, hipStream_t st) {
+  if constexpr (!mpk::g4_supported<PT>()) {
+    return false;
+  } else {
+    if (epi == EPI_SWIGLU) moe4_go<PT, EPI_SWIGLU>(q, st);
+    else if (epi == EPI_ATOMIC) moe4_go<PT, EPI_ATOMIC>(q, st);
+    else return false;
+    return true;
+  }
+}
+
+bool launch_moe_gemm4(int ptype, int epi, const MoeGemvParams& q, hipStream_t st) {
+  switch (ptype) {
+    case P_Q4_K: return moe4_pt<P_Q4_K>(epi, q, st);
+    case P_Q5_K: return moe4_pt<P_Q5_K>(epi, q, st);
+    case P_Q8_0: return moe4_pt<P_Q8_0>(epi, q, st);
+    case P_Q6_K: return moe4_pt<P_Q6_K>(epi, q, st);
+    case P_F16: return moe4_pt<P_F16>(epi, q, st);
+    case P_BF16: return moe4_pt<P_BF16>(epi, q, st);
+    default: return false;
+  }
+}
+
+bool launch_gemm4_splitk(int ptype, GemvParams p, float* scratch, size_t scratch_n, hipStream_t st, bool reduce,
+                         int* nsplit_out) {
+  if (p.bias) return false;
+  float* Y = p.Y;
+  const int ldy = p.ldy;
+  int ns = 0;
+  if (!gemm4_dispatch(ptype, EPI_STORE, p, false, st, scratch, scratch_n, &ns)) return false;
+  if (nsplit_out) *nsplit_out = ns;
+  const int ldp = p.ntiles * 16;
+  if (reduce) launch_splitk_reduce(scratch, ns, (int64_t)p.M * ldp, ldp, p.M, p.n_valid, Y, ldy, st);
+  return true;
+}
+
+}  // namespace mp

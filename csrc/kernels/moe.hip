@@ -11,9 +11,13 @@
 namespace mpk {
 using namespace mp;
 
-// one block: softmax over E router logits per token, top-k, renormalise, bucket by expert
-__global__ __launch_bounds__(256) void moe_route_kernel(const MoeRouteParams p) {
-  for (int e = threadIdx.x; e < p.E; e += blockDim.x) p.counts[e] = 0;
+// one block of 1024 threads: softmax over E router logits per token, top-k, renormalise, bucket by
+// expert.  The bucket positions come from LDS atomics (a prompt chunk of 2048 tokens places 4096
+// slots: as global atomics on 8 addresses they serialised at one L2 channel), then the counts go out
+// once.  The order of slots inside an expert's list does not change any slot's result.
+__global__ __launch_bounds__(1024) void moe_route_kernel(const MoeRouteParams p) {
+  __shared__ int cnt[64];
+  for (int e = threadIdx.x; e < p.E; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
   for (int t = threadIdx.x; t < p.M; t += blockDim.x) {
     const float* lg = p.logits + (size_t)t * p.ld;
@@ -38,10 +42,12 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const MoeRouteParams p) 
     for (int j = 0; j < p.k; ++j) {
       const int slot = t * p.k + j;
       p.weights[slot] = wsel[j] / wsum;
-      const int pos = atomicAdd(&p.counts[esel[j]], 1);
+      const int pos = atomicAdd(&cnt[esel[j]], 1);
       p.lists[(size_t)esel[j] * p.list_cap + pos] = slot;
     }
   }
+  __syncthreads();
+  for (int e = threadIdx.x; e < p.E; e += blockDim.x) p.counts[e] = cnt[e];
 }
 
 // Grouped skinny GEMV: grid (tiles, splits, experts).  Rows = the slots routed to expert e,
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
 namespace mp {
 
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st) {
-  hipLaunchKernelGGL(mpk::moe_route_kernel, dim3(1), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(mpk::moe_route_kernel, dim3(1), dim3(1024), 0, st, p);
 }
 
 template <int PT, int EPI, int MT>

@@ -196,6 +196,33 @@ int mp_op_gemm3(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   API_CATCH(-1)
 }
 
+int mp_op_gemm4(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
+                int ldy, void* H, int ldh, int n_valid, int allow_split, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  if (!launch_gemm4(ptype, epi, p, (hipStream_t)stream, allow_split != 0)) throw std::runtime_error("gemm4: unsupported type");
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+// split-K with partial stores + the fixed-order reduction into Y; returns the split count, 0 when
+// the shape does not split (nothing launched)
+int mp_op_gemm4_splitk(int ptype, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y, int ldy,
+                       int n_valid, void* scratch, int64_t scratch_n, void* stream) {
+  API_TRY
+  GemvParams p{};
+  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
+  p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
+  int ns = 0;
+  if (!launch_gemm4_splitk(ptype, p, (float*)scratch, (size_t)scratch_n, (hipStream_t)stream, true, &ns)) return 0;
+  HIP_OK(hipGetLastError());
+  return ns;
+  API_CATCH(-1)
+}
+
 // A/B overrides of gemm3 through the knob registry (0 = auto; split_wg 0 = the default 256 of the
 // GEMM2_SPLIT_WG knob both GEMMs share)
 int mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) {

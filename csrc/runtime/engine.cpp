@@ -341,6 +341,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.kv_fp8 = j.get_str("kv_dtype", "f16") == "fp8";
   so.fused_norm = j.get_bool("fused_norm", false) && !so.deterministic;   // its sums of squares are atomics
   so.small_gemv = j.get_bool("small_gemv", true);
+  so.moe_gemm = j.get_bool("moe_gemm", true);
   packed_prefill_ = j.get_bool("packed_prefill", true);
   prefix_cache_ = j.get_bool("prefix_cache", true);
 

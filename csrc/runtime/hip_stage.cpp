@@ -498,7 +498,9 @@ void HipStage::alloc_runtime() {
       if (!m.d || is16(m.ptype)) return;
       for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
         if (M <= 64) continue;
-        const int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
+        int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
+        if (opt_.prefill_gemm_v == 4 || opt_.prefill_gemm_v == 0)
+          ns = std::max(ns, gemm4_splits(m.ptype, (int)m.dims.ntiles, (int)m.dims.nsb, M));
         if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
       }
     };
@@ -733,6 +735,23 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     launch_gemm3(P_I8, epi, p, st, allow_split && !opt_.deterministic);
     return;
   }
+  if (M > 64 && opt_.prefill_gemm && gv == 4 && gemm4_supported(m.ptype)) {
+    // v4 GEMM (gemm4.hip: 32x32x16 MFMA): split-K shapes store per-split partials like v2 (into the
+    // residual x: absorbed by the next RMSNorm), the rest run whole-K
+    GemvParams p{};
+    p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
+    p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
+    const bool sk = opt_.gemm_splitk_store && sk_part_ && epi == EPI_ATOMIC && allow_split;
+    const bool defer = sk && Y == sk_defer_;
+    if (sk) flush_sk(st);
+    int ns = 0;
+    if (sk && launch_gemm4_splitk(m.ptype, p, sk_part_, sk_part_n_, st, !defer, &ns)) {
+      if (defer) sk_pend_ = SkPending{Y, M, n_valid, ldy, ns, p.ntiles * 16, (int64_t)M * p.ntiles * 16};
+    } else {
+      launch_gemm4(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
+    }
+    return;
+  }
   if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
@@ -815,14 +834,21 @@ void HipStage::norm_x(float* x, const float* w, int M, float* zero, int64_t zero
 }
 
 void HipStage::moe_ffn(const LayerW& L, int M, hipStream_t st, float* x) {
-  // prompt chunks run in slices of <= 64 tokens, so every slice takes the workgroup-shared MoE
-  // GEMV (weights streamed once per 64 tokens, not once per 16 routed rows as in v1)
+  // > 64 tokens (wide decode micro-batches, prompt chunks): ONE grouped GEMM per projection over
+  // every routed expert (gemm4.hip MoE mode: each expert's weights read once per call, its rows
+  // gathered into 128/256-row MFMA tiles).  The deterministic mode keeps the slices (its per-slot
+  // combine buffer holds 64 tokens).
+  if (M > 64 && opt_.prefill_gemm && opt_.moe_gemm && !opt_.deterministic && gemm4_supported(L.ex.gateup.ptype) &&
+      gemm4_supported(L.ex.down.ptype))
+    return moe_ffn_rows(L, 0, M, st, x, true);
+  // otherwise slices of <= 64 tokens, so every slice takes the workgroup-shared MoE GEMV (weights
+  // streamed once per 64 tokens, not once per 16 routed rows as in v1)
   const bool v1 = knob(KNOB_MOE_V) == 1;
   const int step = v1 ? M : 64;
   for (int r0 = 0; r0 < M; r0 += step) moe_ffn_rows(L, r0, std::min(step, M - r0), st, x);
 }
 
-void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x) {
+void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x, bool grouped) {
   const int E = cfg_.n_expert, k = cfg_.n_expert_used, d = cfg_.d_model, F = cfg_.d_ff;
   const f16* xn = xn_ + (size_t)r0 * Kd_;
   float* logits = moe_logits_ + (size_t)r0 * 64;
@@ -839,6 +865,16 @@ void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, floa
   gp.X = xn; gp.ldx = Kd_; gp.x_per_slot = 0; gp.k = k;
   gp.counts = moe_counts_; gp.lists = moe_lists_; gp.list_cap = rp.list_cap; gp.E = E;
   gp.H = moe_h_; gp.ldh = Kff_; gp.n_valid = F; gp.M = M;
+  if (grouped) {
+    MoeGemvParams dp = gp;
+    dp.W = L.ex.down.d; dp.estride = L.ex.down_stride;
+    dp.ntiles = (int)L.ex.down.dims.ntiles; dp.nsb = (int)L.ex.down.dims.nsb;
+    dp.X = moe_h_; dp.ldx = Kff_; dp.x_per_slot = 1; dp.H = nullptr; dp.ldh = 0;
+    dp.Y = x + (size_t)r0 * d; dp.ldy = d; dp.weights = moe_w_; dp.n_valid = d;
+    if (!launch_moe_gemm4(L.ex.gateup.ptype, EPI_SWIGLU, gp, st) || !launch_moe_gemm4(L.ex.down.ptype, EPI_ATOMIC, dp, st))
+      throw std::runtime_error("moe_ffn: grouped GEMM does not support the expert weight type");
+    return;
+  }
   launch_moe_gemv(L.ex.gateup.ptype, EPI_SWIGLU, gp, 1, st);
   MoeGemvParams dp = gp;
   dp.W = L.ex.down.d; dp.estride = L.ex.down_stride;

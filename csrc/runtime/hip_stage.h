@@ -127,7 +127,7 @@ class HipStage : public Stage {
   void layer_forward(int li, int M, float* x, const int32_t* pos, const int32_t* kvlen, const int32_t* slot,
                      bool decode, hipStream_t st);
   void moe_ffn(const LayerW& L, int M, hipStream_t st, float* x);
-  void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x);
+  void moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, float* x, bool grouped = false);
   bool fuse_norm(int M) const;
   void build_i8_copies();
   int8_t* xq_ = nullptr; float* xqs_ = nullptr; int xq_ld_ = 0;   // int8_gemm: quantized activation rows

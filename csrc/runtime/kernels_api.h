@@ -94,6 +94,14 @@ void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_s
 // X and the raw quants staged by global_load_lds, 16x16x32 f16 MFMA; EPI_ATOMIC splits K over
 // blockIdx.y (allow_split).  A/B overrides: knobs GEMM3_BM / GEMM3_BN / GEMM3_SPLIT (tuning.h).
 void launch_gemm3(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
+// Prompt / wide-decode GEMM v4 (gemm4.hip): gemm3's LDS-DMA stream on v_mfma_f32_32x32x16 (BM 128 |
+// 256 rows x 256 columns, each wave owning 32 columns).  Q4_K, Q6_K, F16, BF16; false = type not
+// supported (nothing launched).  _splitk: split-K partial stores like launch_gemm2_splitk.
+bool gemm4_supported(int ptype);
+int gemm4_splits(int ptype, int ntiles, int nsb, int M);   // K splits of a splittable launch
+bool launch_gemm4(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
+bool launch_gemm4_splitk(int ptype, GemvParams p, float* scratch, size_t scratch_n, hipStream_t st,
+                         bool reduce = true, int* nsplit_out = nullptr);
 
 // Y[m][n] += sum_{s < nsplit} part[s][m][n], s ascending: the fixed-order split-K reduction of the
 // deterministic mode (part rows of ldp floats, splits split_stride floats apart)
@@ -292,5 +300,9 @@ struct MoeGemvParams {
 void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, float* Y, int ldy, hipStream_t st);
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
 void launch_moe_gemv(int ptype, int epi, MoeGemvParams p, int nsplit, hipStream_t st);
+// Grouped MoE dequant GEMM (gemm4.hip, any M): every routed expert's rows as one 32x32x16 MFMA GEMM
+// (rows gathered by the A staging, epilogues scattered by slot).  SWIGLU (gate/up) or ATOMIC (down,
+// weighted; Yslot rows in the deterministic mode).  false = type not supported (nothing launched).
+bool launch_moe_gemm4(int ptype, int epi, const MoeGemvParams& p, hipStream_t st);
 
 }  // namespace mp

@@ -38,6 +38,7 @@ struct StageOptions {
                                // on shared outputs): bitwise-reproducible logits, PP=1 == PP=S
   bool fused_norm = false;  // M <= 4 rows: deferred RMSNorm folded into the qkv / gate-up GEMVs (gemv2.hip);
                             // off by default: 8B mb1 470.7 vs 473.7 tok/s, 70B mb1 92.5 vs 104.8 (r2i)
+  bool moe_gemm = true;     // M > 64 MoE FFN on the grouped expert GEMM (gemm4.hip) instead of 64-row GEMV slices
   bool small_gemv = true;   // M <= 4 rows: the gemvs kernels (gemvs.hip: x staged once per workgroup,
                             // RMSNorm fused into the qkv / gate-up / LM-head GEMVs, in-workgroup split-K)
 };

@@ -37,6 +37,8 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"MOE_V", 2, 1, 2, nullptr},
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
+    {"ATTN_WAVE", 2, 0, 2, nullptr},
+    {"ATTN_WAVE_MIN", 1024, 1, 1 << 30, nullptr},
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},

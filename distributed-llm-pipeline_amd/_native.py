@@ -50,6 +50,10 @@ _SIGS = {
     "mp_op_gemm3": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                      c_int, c_int, c_int, c_void_p], c_int),
     "mp_set_gemm3_tuning": ([c_int, c_int, c_int, c_int], c_int),
+    "mp_op_gemm4": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                     c_int, c_int, c_int, c_void_p], c_int),
+    "mp_op_gemm4_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                            ctypes.c_longlong, c_void_p], c_int),
     "mp_op_gemm2_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             ctypes.c_longlong, c_void_p], c_int),
     "mp_gemm2_splits": ([c_int, c_int, c_int], c_int),

@@ -119,6 +119,8 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
     L = N.lib()
     if v == 3:
         fn = lambda *a: L.mp_op_gemm3(*a[:-1], int(allow_split), a[-1])
+    elif v == 4:
+        fn = lambda *a: L.mp_op_gemm4(*a[:-1], int(allow_split), a[-1])
     else:
         fn = L.mp_op_gemm2 if v == 2 else L.mp_op_gemm
     if epi == EPI_SWIGLU:
@@ -132,6 +134,18 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
     N.check(fn(w.ptype, epi, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
                y.stride(0), None, 0, w.n if n_valid is None else n_valid, _stream()), "gemm")
     return y
+
+
+def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4) -> int:
+    """Split-K through per-split partial stores and the fixed-order reduction added into y (the
+    engine's wide-decode path for qkv / o / down, gemm_splitk_store); returns the split count (0:
+    the shape did not split, y untouched)."""
+    assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous() and v == 4
+    M = x.shape[0]
+    scratch = torch.empty(16 * M * w.ntiles * 16, dtype=torch.float32, device=x.device)
+    return N.check(N.lib().mp_op_gemm4_splitk(w.ptype, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
+                                               y.stride(0), w.n, _ptr(scratch), scratch.numel(), _stream()),
+                   "gemm_splitk")
 
 
 class I8Weight:

@@ -470,7 +470,14 @@ def test_kv_pool_admission_waits_for_pages(native_bins, tiny_gguf):
 
         ts = [threading.Thread(target=go, args=(n, p)) for n, p in (("a", p1), ("b", p2))]
         ts[0].start()
-        time.sleep(0.2)
+        # b goes in only once a's items run in the engine (a fixed sleep raced the admission under load)
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            m = httpx.get(s.url + "/metrics", timeout=10).text
+            done_items = [float(l.split()[-1]) for l in m.splitlines() if l.startswith("mipipe_stage_items_done{")]
+            if done_items and max(done_items) > 0:   # a's prefill / decode items are running
+                break
+            time.sleep(0.01)
         ts[1].start()
         for t in ts:
             t.join()

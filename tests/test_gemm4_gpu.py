@@ -1,0 +1,147 @@
+"""GEMM v4 (csrc/kernels/gemm4.hip, gemm3's LDS-DMA stream on the 32x32x16 MFMA) against a plain
+PyTorch fp32 reference (numpy dequant of the same GGUF blocks as the oracle).
+
+Checked: every supported weight type, both row tiles (128 / 256), partial row and column blocks,
+the three epilogues, split-K by atomics and by per-split partial stores + the fixed-order
+reduction (the engine's wide-decode path for qkv / o / down), the Llama-3-70B headline widths
+(K = 8192 / 28672) and an exact-integer layout probe of the A / B / C lane maps."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from mipipe.utils import quants as Q
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [Q.Q4_K, Q.Q5_K, Q.Q6_K, Q.Q8_0, Q.F16, Q.BF16]
+
+
+def nmse(a, b):
+    a, b = a.double(), b.double()
+    return float(((a - b) ** 2).sum() / ((b ** 2).sum() + 1e-30))
+
+
+def _weights(qt, n, k, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((n, k)) / math.sqrt(k)).astype(np.float32)
+    raw = Q.quantize(x, qt)
+    return raw, torch.from_numpy(Q.dequantize(raw, qt).reshape(n, k))
+
+
+def _x(M, k, k_pad, seed):
+    g = torch.Generator().manual_seed(seed)
+    xh = torch.zeros(M, k_pad, dtype=torch.float16)
+    xh[:, :k] = torch.randn(M, k, generator=g).half()
+    return xh
+
+
+def _ref(xh, k, deq, qt):
+    xa = xh[:, :k].float()
+    if qt == Q.BF16:   # the bf16 MFMA rounds the activations to bf16
+        xa = xh[:, :k].bfloat16().float()
+    return xa @ deq.T
+
+
+@pytest.fixture
+def tuning(native):
+    from mipipe.ops.kernels import set_gemm3_tuning
+    yield set_gemm3_tuning
+    set_gemm3_tuning(0, 0, 0, 0)
+
+
+@pytest.mark.parametrize("qt", TYPES)
+@pytest.mark.parametrize("bm", [0, 128, 256])
+@pytest.mark.parametrize("M", [65, 200, 300])
+def test_gemm4_tiles(cuda, tuning, qt, bm, M):
+    """STORE / ATOMIC (auto split) / SwiGLU on 13 tiles (a partial 256-column group), 5
+    super-blocks (20 stages), partial row blocks, for every row tile."""
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
+    tuning(bm, 0, 0, 0)
+    n, k = 208, 1280
+    raw, deq = _weights(qt, n, k, 700 + qt + M)
+    w = PackedWeight(raw, qt, n, k)
+    xh = _x(M, k, w.k_pad, M + 1)
+    ref = _ref(xh, k, deq, qt)
+    y = gemm(w, xh.cuda(), EPI_STORE, v=4)
+    assert nmse(y.cpu(), ref) < 1e-5
+    base = torch.randn(M, n)
+    y2 = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4)
+    assert nmse(y2.cpu(), ref + base) < 1e-5
+    h = gemm(w, xh.cuda(), EPI_SWIGLU, v=4)
+    gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
+    href = torch.nn.functional.silu(ref[:, gi]) * ref[:, gi + 8]
+    assert nmse(h.float().cpu(), href) < 1e-4
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K])
+@pytest.mark.parametrize("shape", [(512, 8192), (256, 28672)])
+@pytest.mark.parametrize("nsplit", [1, 4, 8])
+@pytest.mark.parametrize("M", [65, 256, 300])
+def test_gemm4_headline_widths_split(cuda, tuning, qt, shape, nsplit, M):
+    """The 70B headline widths: K = 8192 (qkv / o / gate-up) and 28672 (down), ATOMIC with split-K
+    forced to 1 / 4 / 8, added into a non-zero residual."""
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_ATOMIC
+    tuning(0, 0, nsplit, 0)
+    n, k = shape
+    raw, deq = _weights(qt, n, k, 31 + qt)
+    w = PackedWeight(raw, qt, n, k)
+    xh = _x(M, k, w.k_pad, 9 + M)
+    ref = _ref(xh, k, deq, qt)
+    base = torch.randn(M, n)
+    y = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4)
+    assert nmse(y.cpu() - base, ref) < 1e-5
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K])
+@pytest.mark.parametrize("M", [128, 256])
+def test_gemm4_splitk_partial_stores(cuda, tuning, qt, M):
+    """The engine's split-K for the narrow wide-decode GEMMs: every split stores its partial tile,
+    the fixed-order reduction adds them into y.  Bitwise reproducible run to run."""
+    from mipipe.ops.kernels import PackedWeight, gemm_splitk
+    n, k = 1024, 8192
+    raw, deq = _weights(qt, n, k, 77 + qt)
+    w = PackedWeight(raw, qt, n, k)
+    xh = _x(M, k, w.k_pad, 3 + M).cuda()
+    ref = _ref(xh.cpu(), k, deq, qt)
+    base = torch.randn(M, n)
+    outs = []
+    for _ in range(2):
+        y = base.clone().cuda()
+        ns = gemm_splitk(w, xh, y)
+        assert ns >= 2
+        outs.append(y.cpu())
+    assert nmse(outs[0] - base, ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("bm", [128, 256])
+def test_gemm4_asymmetric_identity(cuda, tuning, bm):
+    """Lane-map check with exact integer data (F16 weights with an asymmetric 0/1/2 pattern,
+    distinct integer rows of x): any row / column / k swap in the 32x32x16 A, B or C maps is an
+    exact mismatch."""
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE
+    tuning(bm, 0, 0, 0)
+    n, k, M = 256, 512, 256
+    w_np = np.zeros((n, k), np.float32)
+    for j in range(n):
+        w_np[j, j] = 1.0
+        w_np[j, (3 * j + 7) % k] = 2.0
+    w = PackedWeight(Q.quantize(w_np, Q.F16), Q.F16, n, k)
+    x = ((torch.arange(M)[:, None] * 3 + torch.arange(k)[None, :] % 17) % 64).half()
+    y = gemm(w, x.cuda(), EPI_STORE, v=4).cpu()
+    ref = x.float() @ torch.from_numpy(w_np).T
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("M", [96, 256])
+def test_gemm4_matches_gemm2_q4k(cuda, native, M):
+    """Same packed Q4_K weights through the 32x32 GEMM and the 16x16 GEMM v2: equal up to f32
+    summation order."""
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE
+    n, k = 512, 4096
+    raw, _ = _weights(Q.Q4_K, n, k, 5)
+    w = PackedWeight(raw, Q.Q4_K, n, k)
+    xh = _x(M, k, w.k_pad, 8).cuda()
+    assert nmse(gemm(w, xh, EPI_STORE, v=4).cpu(), gemm(w, xh, EPI_STORE, v=2).cpu()) < 1e-9

@@ -35,7 +35,11 @@ def main():
     ap.add_argument("--copies", type=int, default=0, help="weight copies cycled (default: enough to defeat the 256 MiB MALL; 1 = hot)")
     ap.add_argument("--gemm", type=int, default=0,
                     help="time the prompt GEMM instead (1: 64x64 tiles, 2: 128x256 per-wave dequant, 3: LDS-shared dequant, "
-                         "8: the int8-activation prototype on per-row int8 weights, gemm3 P_I8)")
+                         "4: gemm3's stream on the 32x32x16 MFMA, 8: the int8-activation prototype on per-row int8 "
+                         "weights, gemm3 P_I8)")
+    ap.add_argument("--sk", action="store_true",
+                    help="ATOMIC shapes with --gemm 2 / 4: the engine's split-K (per-split partial stores + the "
+                         "fixed-order reduction into Y) instead of atomics")
     ap.add_argument("--g3", default="0,0,0", help="v3 GEMM tuning BM,BN,nsplit (0 = auto); ';'-separated list sweeps")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=V[,V..]",
                     help="tuning knob (csrc/runtime/tuning.h) swept per shape, e.g. GEMM3_PROBE=0,1,2")
@@ -71,6 +75,7 @@ def main():
                 xs = torch.full((M,), 1e-2, device="cuda")
                 Y = torch.zeros(M, n, device="cuda")
                 H = torch.zeros(M, n // 2, device="cuda", dtype=torch.float16)
+                SK = torch.empty(16 * M * ntiles * 16 if a.sk else 1, device="cuda")
                 knobs = [[]]
                 for kv in a.knob:
                     name, vals = kv.split("=", 1)
@@ -96,6 +101,18 @@ def main():
                                                          n, ctypes.c_void_p(H.data_ptr()), n // 2,
                                                          n if epi != EPI_SWIGLU else n // 2, ctypes.c_void_p(xs.data_ptr()),
                                                          ctypes.c_void_p(ws.data_ptr()), 1, st()), "gemm3_i8")
+                                return
+                            if a.sk and a.gemm in (2, 4) and epi == EPI_ATOMIC:
+                                fn = L.mp_op_gemm4_splitk if a.gemm == 4 else L.mp_op_gemm2_splitk
+                                N.check(fn(pt, ctypes.c_void_p(W.data_ptr()), ntiles, nsb, ctypes.c_void_p(X.data_ptr()),
+                                           k_pad, M, ctypes.c_void_p(Y.data_ptr()), n, n,
+                                           ctypes.c_void_p(SK.data_ptr()), SK.numel(), st()), "gemm splitk")
+                                return
+                            if a.gemm == 4:
+                                N.check(L.mp_op_gemm4(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
+                                                      ctypes.c_void_p(X.data_ptr()), k_pad, M, ctypes.c_void_p(Y.data_ptr()),
+                                                      n, ctypes.c_void_p(H.data_ptr()), n // 2,
+                                                      n if epi != EPI_SWIGLU else n // 2, 1, st()), "gemm4")
                                 return
                             if a.gemm == 3:
                                 N.check(L.mp_op_gemm3(pt, epi, ctypes.c_void_p(W.data_ptr()), ntiles, nsb,
@@ -127,7 +144,7 @@ def main():
                         print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
                                               GBps=round(nbytes / us / 1e3, 1),
                                               TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
-                                              g3=g3 if a.gemm in (3, 8) else None, knobs=dict(kn) or None)), flush=True)
+                                              g3=g3 if a.gemm in (3, 4, 8) else None, sk=a.sk or None, knobs=dict(kn) or None)), flush=True)
                 if a.gemm == 8:   # the per-row activation quantization the int8 GEMM needs first
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
