@@ -1,9 +1,9 @@
 """GEMM v3 (csrc/kernels/gemm3.hip) against a plain PyTorch fp32 reference.
 
-The v3 GEMM runs every decode micro-batch above 64 rows and every prompt chunk, so besides small
-shapes in every quant type, tile shape and epilogue, it is checked at the headline's real widths
-(Llama-3-70B K = 8192 / 28672 with split-K forced to 1, 4 and 8) -- the configuration the 70B
-decode bench runs."""
+The v3 GEMM runs the wide (> 64-row) decode micro-batches and prompt chunks of 16-bit weights
+(hip_stage.cpp HipStage::gemv picks it for F16 / BF16; quantized weights take gemm2 or gemm4), and
+every type through prefill_gemm_v=3.  Besides small shapes in every quant type, tile shape and
+epilogue, it is checked at the 70B widths (K = 8192 / 28672, split-K forced to 1, 4 and 8)."""
 import math
 
 import numpy as np
