@@ -328,7 +328,8 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   const bool rvalid = col < G;
   const int pos = p.pos[t];
   const int kvlen = pos + 1;
-  const int slot = p.slot[t];
+  // decode rows map to slots slot0 + t (HipStage::slot_of): no dependent load before the block table
+  const int slot = p.slot0 >= 0 ? p.slot0 + t : p.slot[t];
   const int h = kvh * G + g;
   const int hd2 = p.hd / 2;
   const float* row = p.qkv + (size_t)t * p.ldqkv;
@@ -338,24 +339,6 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
 
   const int start = z * p.split_len;
-  const int end = min(start + p.split_len, kvlen);
-  // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
-  // single active split writes the output directly, so short contexts pay no merge round trip
-  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
-  if (z >= n_act) return;
-
-  // 1. q fragments with RoPE applied in registers (decode_q_frags)
-  half8_t qf[KK];
-  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
-
-  // 2. append the new token's K (rotated) and V to the cache.  The split that reads the new token
-  // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
-  // wave waits for its own global append to land (no store -> barrier -> load round trip) and the
-  // first chunk's K/V loads are in flight before the append starts.
-  __shared__ __attribute__((aligned(16))) f16 sm_kn[DP];
-  __shared__ f16 sm_vn[DP];
-  const bool owns = start <= pos && pos < end;
-  const int nch = (end - start + 31) / 32;
   const int krow0 = 8 * (col >> 2) + (col & 3);
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   constexpr int EB = F8 ? 1 : 2;   // bytes per cached element
@@ -375,7 +358,31 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
   };
   KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
-  if (PF && wv < nch) load(wv, kA, vA);   // in flight during the append
+  // one split (short contexts): each wave's first chunk is loaded before the position arrives
+  // (chunks past the sequence read the pool's trash page and are never used; never past the
+  // slot's block-table row: split_len may exceed max_pages * 64)
+  const bool pre = PF && p.n_split == 1 && 32 * wv < min(p.split_len, p.max_pages * 64 - start);
+  if (pre) load(wv, kA, vA);
+
+  const int end = min(start + p.split_len, kvlen);
+  // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
+  // single active split writes the output directly, so short contexts pay no merge round trip
+  const int n_act = (kvlen + p.split_len - 1) / p.split_len;
+  if (z >= n_act) return;
+
+  // 1. q fragments with RoPE applied in registers (decode_q_frags)
+  half8_t qf[KK];
+  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+
+  // 2. append the new token's K (rotated) and V to the cache.  The split that reads the new token
+  // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
+  // wave waits for its own global append to land (no store -> barrier -> load round trip) and the
+  // first chunk's K/V loads are in flight before the append starts.
+  __shared__ __attribute__((aligned(16))) f16 sm_kn[DP];
+  __shared__ f16 sm_vn[DP];
+  const bool owns = start <= pos && pos < end;
+  const int nch = (end - start + 31) / 32;
+  if (PF && !pre && wv < nch) load(wv, kA, vA);   // in flight during the append
 
   if (owns) {
     const int page = bt[pos >> 6], idx = pos & 63;
@@ -671,7 +678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int hd2 = p.hd / 2;
   const float* row = p.qkv + (size_t)t * p.ldqkv;
   const float2* cs = p.rope_cs + (size_t)pos * hd2;
-  const int32_t* bt = p.block_table + (size_t)p.slot[t] * p.max_pages;
+  const int32_t* bt = p.block_table + (size_t)(p.slot0 >= 0 ? p.slot0 + t : p.slot[t]) * p.max_pages;
   const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
   const int nch = (end - start + 31) / 32;
   const int krow0 = 8 * (col >> 2) + (col & 3);
@@ -710,8 +717,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
     const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
 #pragma unroll
-    for (int jj = 0; jj < DP / 128; ++jj) {   // K: one pair per lane per 128 dims
+    for (int jj = 0; jj < (DP / 2 + 63) / 64; ++jj) {   // K: one pair per lane per 128 dims
       const int j = lane + 64 * jj;
+      if (j >= DP / 2) break;
       const bool kin = j < hd2;
       float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
       if (kin) {

@@ -205,14 +205,26 @@ struct G4Moe {
   float* Yslot = nullptr;
 };
 
-template <int PT, int EPI, int BM, bool MOE>
+// NWV compute waves (8, or 7: BN = 224 columns, so a 57344-column gate/up gives 256 workgroups
+// for the 256 CUs instead of 224); the x rows are staged round-robin by all of them
+template <int PT, int BM, int NWV>
+struct G4Geom {
+  static constexpr int A_BYTES = BM * 128;                    // x rows of one 64-k stage
+  static constexpr int R_WAVE = W3<PT>::RAW(2);              // one wave's raw bytes of one stage
+  static constexpr int STAGE = A_BYTES + NWV * R_WAVE;
+  static constexpr int NB = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  static constexpr int NP = BM / 8;                           // 1-KB A pieces (8 rows) per stage
+  static constexpr int A_INSTR = (NP + NWV - 1) / NWV;        // per wave (uniform: vmcnt accounting)
+};
+
+template <int PT, int EPI, int BM, bool MOE, int NWV = 8>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages, const G4Moe mo) {
   constexpr int TW = 2;
   using Q3 = W3<PT>;
   using Q = W4<PT>;
-  using G = G3Geom<PT, BM, TW>;
-  constexpr int NB = G::NB, FR = BM / 32, BN = 256;
+  using G = G4Geom<PT, BM, NWV>;
+  constexpr int NB = G::NB, FR = BM / 32, BN = 32 * NWV;
   constexpr bool BF = PT == P_BF16;
   static_assert(NB == 3, "gemm4: the cross-stage stream needs 3 stage buffers");
   __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
@@ -245,11 +257,16 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   auto stage_a = [&](int b) { return smem + b * G::STAGE; };
   auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
   // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7 (swizzled on the source side):
-  // each lane's source row pointers are fixed for the whole K loop (MoE: the gathered rows)
+  // each lane's source row pointers are fixed for the whole K loop (MoE: the gathered rows).
+  // Pieces go round-robin over the NWV waves; a wave whose last slot is past the NP pieces re-loads
+  // another wave's piece into that piece's place (identical bytes), so every wave issues A_INSTR.
+  int apc[G::A_INSTR];
   const char* xsrc[G::A_INSTR];
 #pragma unroll
   for (int i = 0; i < G::A_INSTR; ++i) {
-    const int row = 8 * (wave * G::A_INSTR + i) + (lane >> 3);
+    const int pc0 = wave + NWV * i;
+    apc[i] = pc0 < G::NP ? pc0 : pc0 - G::NP;
+    const int row = 8 * apc[i] + (lane >> 3);
     const int ch = (lane & 7) ^ g3_swz(row);
     int gr = min(m0 + row, M - 1);
     if constexpr (MOE) {
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   }
   auto issue_a = [&](int s, int b) {
 #pragma unroll
-    for (int i = 0; i < G::A_INSTR; ++i) glds<16>(xsrc[i] + s * 128, stage_a(b) + (wave * G::A_INSTR + i) * 1024);
+    for (int i = 0; i < G::A_INSTR; ++i) glds<16>(xsrc[i] + s * 128, stage_a(b) + apc[i] * 1024);
   };
   auto issue_b = [&](int s, int b) {
     src.sb = s / 4; src.q = s % 4;
@@ -406,16 +423,16 @@ static int g4_splits(int wgs, int n_stages) {
   return std::max(1, std::min(target / wgs, n_stages / 16));
 }
 
-template <int PT, int EPI, int BM, bool MOE = false>
+template <int PT, int EPI, int BM, bool MOE = false, int NWV = 8>
 static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe& mo = mpk::G4Moe{}, int E = 1) {
-  const int n_cg = (p.ntiles + 15) / 16;
+  const int n_cg = (p.ntiles + 2 * NWV - 1) / (2 * NWV);
   const int n_mb = (p.M + BM - 1) / BM;   // MoE: p.M = the most rows one expert can get
   const int n_stages = p.nsb * 4;
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
-  hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE>), dim3(n_cg * n_mb, nsplit, E), dim3(512), 0, st, p, n_mb,
-                     per, n_stages, mo);
+  hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV>), dim3(n_cg * n_mb, nsplit, E), dim3(64 * NWV), 0, st,
+                     p, n_mb, per, n_stages, mo);
 }
 
 // rows per workgroup: 256 unless one 128-row block holds M (16-bit weights: always 128, their raw
@@ -425,11 +442,31 @@ static int g4_bm(int ptype, int M) {
   return knob(KNOB_GEMM3_BM) ? knob(KNOB_GEMM3_BM) : (M <= 128 ? 128 : 256);
 }
 
+// compute waves per workgroup for an unsplit launch: 7 (224 columns) when that fills more of the
+// 256 CUs in whole rounds (70B gate/up at M = 256: 224 -> 256 workgroups), else 8; knob GEMM4_NW
+static int g4_nwv(int ntiles, int n_mb) {
+  if (knob(KNOB_GEMM4_NW)) return knob(KNOB_GEMM4_NW);
+  auto util = [&](int nw) {
+    const long w = (long)(ntiles + 2 * nw - 1) / (2 * nw) * n_mb;
+    const long rounds = (w + 255) / 256;
+    return (double)w / (rounds * 256);
+  };
+  return util(7) > util(8) + 0.05 ? 7 : 8;
+}
+
 template <int PT, int EPI>
 static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
-  if constexpr (is16(PT)) gemm4_go<PT, EPI, 128>(p, nsplit, st);
-  else if (g4_bm(PT, p.M) == 128) gemm4_go<PT, EPI, 128>(p, nsplit, st);
-  else gemm4_go<PT, EPI, 256>(p, nsplit, st);
+  const int bm = g4_bm(PT, p.M);
+  const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
+  if constexpr (is16(PT)) {
+    gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  } else if (bm == 128) {
+    if (nw7) gemm4_go<PT, EPI, 128, false, 7>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  } else {
+    if (nw7) gemm4_go<PT, EPI, 256, false, 7>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 256>(p, nsplit, st);
+  }
 }
 
 template <int PT>

@@ -1014,6 +1014,7 @@ bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slo
     return false;
   DecodeAttnParams dp{};
   dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
+    dp.slot0 = dec_slot0_;   // decode only
   dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
   dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
   dp.kv_fp8 = opt_.kv_fp8;
@@ -1036,6 +1037,7 @@ void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen
   if (decode && opt_.fused_attn) {
     DecodeAttnParams dp{};
     dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
+    dp.slot0 = decode ? dec_slot0_ : -1;
     dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
     dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
     dp.kv_fp8 = opt_.kv_fp8;
@@ -1232,6 +1234,7 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
   float* x = act_[mb];
   if (spec_.first())
     launch_embed(embd_type_, embd_raw_, (int64_t)embd_row_bytes_, cfg_.d_model, tok_[mb], B, x, cfg_.d_model, st);
+  dec_slot0_ = slot_of(mb, 0);   // slot_[mb] holds slot_of(mb, b) = dec_slot0_ + b
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
   flush_sk(st);

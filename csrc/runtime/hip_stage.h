@@ -90,6 +90,7 @@ class HipStage : public Stage {
   int32_t* prompt_buf() override { return prompt_dev_; }
   int act_rows() const { return act_rows_; }
   int slot_of(int mb, int b) const { return mb * opt_.mb_size + b; }
+  int dec_slot0_ = -1;   // decode: slot of row 0 of the micro-batch being recorded (decode attention)
 
   // positions of micro-batch mb (host values) before decode; kvlen = pos + 1
   void set_positions(int mb, const std::vector<int32_t>& pos) override;

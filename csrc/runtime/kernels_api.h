@@ -198,6 +198,7 @@ struct DecodeAttnParams {
   const float* qkv; int ldqkv;     // [M][ldqkv] f32 projections q | k | v
   const int32_t* pos;              // [M]
   const int32_t* slot;             // [M]
+  int slot0 = -1;                  // >= 0: slot of row t is slot0 + t (decode micro-batches); slot unused
   const int32_t* block_table; int max_pages;
   const float2* rope_cs;           // [max_pos][hd/2]
   float q_scale;

@@ -46,8 +46,10 @@ def test_wave_attention_matches_workgroup_kernel(cuda, wave_knob, model_dir, nam
             lg.append(eng.logits(rows=3).copy())
             res[mode] = (eng.tokens(), lg)
     assert res[1][0] == res[0][0]
+    # e4m3 pages: a 1e-7 difference in a new K / V value can round to the neighbouring fp8 code
+    tol = 1e-4 if kv == "fp8" else 1e-6
     for a, b in zip(res[1][1], res[0][1]):
-        assert nmse(a, b) < 1e-6
+        assert nmse(a, b) < tol
 
 
 def test_wave_attention_matches_reference(cuda, wave_knob, model_dir):

@@ -145,3 +145,29 @@ def test_gemm4_matches_gemm2_q4k(cuda, native, M):
     w = PackedWeight(raw, Q.Q4_K, n, k)
     xh = _x(M, k, w.k_pad, 8).cuda()
     assert nmse(gemm(w, xh, EPI_STORE, v=4).cpu(), gemm(w, xh, EPI_STORE, v=2).cpu()) < 1e-9
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
+@pytest.mark.parametrize("nw", [7, 8])
+@pytest.mark.parametrize("M", [65, 256])
+def test_gemm4_seven_wave_tiles(cuda, native, qt, nw, M):
+    """224-column workgroups (7 compute waves; the x pieces round-robin over 7 waves with one
+    duplicate load) against 256-column ones and the oracle: 40 tiles = two full 224-column groups
+    plus a partial one, STORE and SwiGLU (unsplit launches are the ones that take 7 waves)."""
+    from mipipe import _native as N
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_SWIGLU
+    N.check(N.lib().mp_set_knob(b"GEMM4_NW", nw), "knob")
+    try:
+        n, k = 640, 2048
+        raw, deq = _weights(qt, n, k, 400 + qt + M)
+        w = PackedWeight(raw, qt, n, k)
+        xh = _x(M, k, w.k_pad, M + 7)
+        ref = _ref(xh, k, deq, qt)
+        y = gemm(w, xh.cuda(), EPI_STORE, v=4)
+        assert nmse(y.cpu(), ref) < 1e-5
+        h = gemm(w, xh.cuda(), EPI_SWIGLU, v=4)
+        gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
+        href = torch.nn.functional.silu(ref[:, gi]) * ref[:, gi + 8]
+        assert nmse(h.float().cpu(), href) < 1e-4
+    finally:
+        N.lib().mp_set_knob(b"GEMM4_NW", 0)
