@@ -19,17 +19,19 @@ ring.  Two launches, the same engine:
     LocalLinks (one device copy per boundary, receiver-side xGMI read); `--same-device` puts every
     stage on GPU 0 (the 1-GPU rehearsal of the N-stage path).
 Default 256 sequences per micro-batch, sized for 288 GB of HBM: above 64 rows the Q4_K decode
-projections run on the 128-row dequant MFMA GEMM (gemm2 in gemv2.hip; hip_stage.cpp picks it for
-quantized weights, gemm3 for 16-bit ones).  Weak scaling: per-GPU work is fixed
+projections run on the dequant MFMA GEMMs (HipStage::gemv's auto choice: gate/up and the LM head
+on gemm4's 32x32x16 MFMA tiles, the split-K qkv / o / down on gemm2 in gemv2.hip; gemm3 for 16-bit
+weights).  Weak scaling: per-GPU work is fixed
 (every stage streams its own weights once per micro-batch per round), global batch =
 n_mb * mb_size sequences.  The timed region is exactly K decode rounds (every sequence emits one
 token per round), bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over
 ranks is reported.
 
-At N = 1 the same run also measures, with the same bracket, the other named BASELINE config
-(Llama-3-8B Q4_K_M PP=1, single stream), the round-1 like-for-like point (70B, 64 sequences) and
-the headline shape in the opt-in int8 compute mode (reduced precision; reported only there):
-"secondary" in the JSON line (--no-secondary skips them).  For N > 1 the line reports the data
+At N = 1 the same run also measures, with the same bracket, the other named BASELINE configs at
+one GPU (Llama-3-8B Q4_K_M single stream, Mixtral 8x7B Q4_K_M at 256 sequences on the grouped MoE
+GEMM, Llama-3-8B bf16 at 64 sequences), the round-1 like-for-like point (70B, 64 sequences) and the
+headline shape at the reference's 2K context (256 sequences decoding at positions ~2000, after a
+real prefill of their 1984-token prompts): "secondary" in the JSON line (--no-secondary skips them).  For N > 1 the line reports the data
 plane the engine built ("link": transport kind, RCCL communicator sizes as ncclCommCount returns
 them, bf16 wire bytes per token per boundary).
 """
@@ -57,13 +59,15 @@ MODELS = {
                       vocab=32000, rope_base=10000.0),
 }
 
-# (label, model, ftype, mb_size, extra engine options): the other BASELINE config, the round-1
-# like-for-like point, and the headline shape in the opt-in int8 mode (per-row int8
-# activations x per-row int8 re-quantized weights on the i8 MFMA -- reduced precision, so never the
-# headline value)
-SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1, {}),
-             ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64, {}),
-             ("llama3-70b Q4_K pp1 mb256 int8_gemm (reduced precision)", "llama3-70b", "Q4_K", 256, {"int8_gemm": True})]
+# (label, model, ftype, mb_size, extra engine options, prompt length or None for --prompt-len): the
+# other named BASELINE configs at one GPU (8B Q4_K_M single stream; Mixtral 8x7B on the grouped MoE
+# GEMM; 8B bf16), the round-1 like-for-like point (70B, 64 sequences) and the headline shape at the
+# reference CLI's 2K context (-c 2048, main.rs:45-46): 256 sequences decoding at positions ~2000
+SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1, {}, None),
+             ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64, {}, None),
+             ("mixtral-8x7b Q4_K_M pp1 mb256", "mixtral-8x7b", "Q4_K_M", 256, {}, None),
+             ("llama3-8b BF16 pp1 mb64", "llama3-8b", "BF16", 64, {}, None),
+             ("llama3-70b Q4_K pp1 mb256 ctx2048", "llama3-70b", "Q4_K", 256, {}, 1984)]
 
 
 def parse_set(items):
@@ -169,8 +173,8 @@ def main():
     tr_kw = dict(device=0, pg_backend="gloo") if args.same_device and not inproc else {}
     pg_cpu = args.same_device and not inproc
 
-    def factory(model, ftype, mb_size, n_mb, extra=None):
-        max_ctx = ((args.prompt_len + args.warmup + args.steps + 8 + 63) // 64) * 64
+    def factory(model, ftype, mb_size, n_mb, extra=None, prompt_len=None):
+        max_ctx = (((prompt_len or args.prompt_len) + args.warmup + args.steps + 8 + 63) // 64) * 64
         cfg = dict(synthetic=MODELS[model], ftype=ftype, n_mb=n_mb, mb_size=mb_size, max_ctx=max_ctx,
                    prefill_chunk=512, graphs=not args.no_graphs, split="cost", seed=1234)
         cfg.update(parse_set(args.set))
@@ -191,10 +195,11 @@ def main():
 
     secondary = {}
     if n_gpus == 1 and not args.no_secondary:
-        for label, model, ftype, mb, extra in SECONDARY:
-            if model == args.model and ftype == args.ftype and mb == args.mb_size and not extra:
+        for label, model, ftype, mb, extra, plen in SECONDARY:
+            plen = plen or args.prompt_len
+            if model == args.model and ftype == args.ftype and mb == args.mb_size and not extra and plen == args.prompt_len:
                 continue
-            sms, sp50, _ = run(factory(model, ftype, mb, 1, extra), MODELS[model]["vocab"], mb, args.prompt_len,
+            sms, sp50, _ = run(factory(model, ftype, mb, 1, extra, plen), MODELS[model]["vocab"], mb, plen,
                                args.steps, args.warmup, world, pg_cpu)
             secondary[label] = dict(tok_s=round(args.steps * mb / (sms / 1e3), 2), ms_per_round=round(sms / args.steps, 4),
                                     p50_token_ms=round(sp50, 4))

@@ -435,11 +435,16 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
                      p, n_mb, per, n_stages, mo);
 }
 
-// rows per workgroup: 256 unless one 128-row block holds M (16-bit weights: always 128, their raw
-// stage images leave no room for three 256-row x images in LDS)
-static int g4_bm(int ptype, int M) {
+// rows per workgroup: 256 unless one 128-row block holds M, or 256-row tiles leave most of the 256
+// CUs idle (8B gate/up at M = 256: 112 workgroups of 256 rows, 112 us, against 224 of 128 rows,
+// 78 us: profiles/r8a_gemm_microbench.txt).  16-bit weights: always 128, their raw stage images
+// leave no room for three 256-row x images in LDS
+static int g4_bm(int ptype, int M, int ntiles) {
   if (is16(ptype)) return 128;
-  return knob(KNOB_GEMM3_BM) ? knob(KNOB_GEMM3_BM) : (M <= 128 ? 128 : 256);
+  if (knob(KNOB_GEMM3_BM)) return knob(KNOB_GEMM3_BM);
+  if (M <= 128) return 128;
+  const int cgs = (ntiles + 15) / 16;
+  return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;
 }
 
 // compute waves per workgroup for an unsplit launch: 7 (224 columns) when that fills more of the
@@ -456,7 +461,7 @@ static int g4_nwv(int ntiles, int n_mb) {
 
 template <int PT, int EPI>
 static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
-  const int bm = g4_bm(PT, p.M);
+  const int bm = g4_bm(PT, p.M, p.ntiles);
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
@@ -475,7 +480,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
   if constexpr (!mpk::g4_supported<PT>()) {
     return false;
   } else {
-    const int bm = g4_bm(PT, p.M);
+    const int bm = g4_bm(PT, p.M, p.ntiles);
     const int wgs = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
     const int n_stages = p.nsb * 4;
     int ns = 1;
@@ -515,7 +520,7 @@ static bool gemm4_dispatch(int ptype, int epi, const GemvParams& p, bool allow_s
 
 int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
   if (!gemm4_supported(ptype)) return 1;
-  const int bm = g4_bm(ptype, M);
+  const int bm = g4_bm(ptype, M, ntiles);
   const int wgs = (ntiles + 15) / 16 * ((M + bm - 1) / bm);
   const int n_stages = nsb * 4;
   int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);

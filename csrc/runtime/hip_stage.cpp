@@ -711,12 +711,19 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // every shape, f16 weights excepted (they take the 64 x 64 GEMM)
   // v3 GEMM (gemm3.hip: 128|256 x 128|256 workgroup tiles, each weight element dequantized once
   // per workgroup, cross-stage MFMA stream): every type, 16-bit weights included
-  // auto (0): v2 for the quantized types, v3 for 16-bit weights (v2 has no 16-bit path).  Measured in
+  // (round 3, before v4) v2 for the quantized types, v3 for 16-bit weights (v2 has no 16-bit path).  Measured in
   // the 70B mb256 round: v3 wins the gate/up on some boxes and loses it on others (212 vs 249 us in
   // profiles/r6h_engine_gemm_v2_v3.txt, 268 us in r6j_gemm_select.txt), and loses o/down (114 vs 98),
   // qkv (72 vs 69) and the Q6_K LM head (1162 vs 639) everywhere; bench.py A/B in one run:
   // v2 5402 tok/s, v3 for gate/up only 5204-5217, v3 everywhere 4867 (r6j)
-  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v : is16(m.ptype) ? 3 : 2;
+  // auto for quantized weights, per epilogue (r8a, profiles/r8a_gemm_microbench.txt, 70B at M = 256):
+  // the whole-K SwiGLU / store GEMMs (gate/up, LM head) take v4 (gate/up 297 vs 316 us, Q6_K head
+  // 724 vs 820), the split-K accumulating ones (qkv, o, down) keep v2 (68.6 / 58.0 / 152.8 against
+  // v4's 75.5 / 65.9 / 150.5)
+  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v
+                 : is16(m.ptype)         ? 3
+                 : epi == EPI_ATOMIC     ? 2
+                                         : 4;
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
   const bool v3 = gv == 3;
   const bool v2 = gv == 2 && !is16(m.ptype);

@@ -30,7 +30,8 @@ struct StageOptions {
                             // re-quantized weights (+1 B/weight of HBM; reduced precision, opt-in)
   bool gemm_splitk_store = true;   // M > 64 split-K GEMMs: per-split partial stores + a fixed-order reduction
                                    // (into the residual: absorbed by the next RMSNorm) instead of float atomics
-  int prefill_gemm_v = 0;    // 0: auto (v2 for quantized, v3 for 16-bit weights); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
+  int prefill_gemm_v = 0;    // 0: auto (quantized: v4 for gate/up and the LM head, v2 for the split-K projections;
+                             // 16-bit: v3); 4: gemm4 (32x32x16); 3: gemm3; 2: gemm2 (128 x 256); 1: 64 x 64
   bool prefill_flash = true; // prompt chunks: the LDS-tiled prefill flash attention (attn_prefill.hip)
   bool kv_fp8 = false;       // kv_dtype "fp8": KV pages hold OCP e4m3 bytes
   int kv_pages = 0;          // KV pool pages per stage (64 tokens each; 0: n_slots x max_ctx / 64)

@@ -9,7 +9,7 @@ prefill_chunk, split ("even" | "mem" | "cost"), graphs, fused_attn, prefill_gemm
 temp/top_k/top_p/min_p/seed (sampling; llama.cpp chain order), repeat_penalty/repeat_last_n/
 frequency_penalty/presence_penalty (penalties over the last n tokens, prompt included), world/rank/hosts/next_host/base_port/rccl_ids (mp mode),
 threads (CPU backend), trace, watchdog_s, link_timeout_s, fault (fault injection), verbose, log_file,
-kv_dtype ("f16" | "fp8"), kv_pool_tokens (paged KV pool), prefill_gemm_v (0 auto | 1 | 2 | 3), prefill_flash,
+kv_dtype ("f16" | "fp8"), kv_pool_tokens (paged KV pool), prefill_gemm_v (0 auto | 1 | 2 | 3 | 4), prefill_flash,
 deterministic, fused_norm, small_gemv, act_dtype (stage-boundary wire: "auto" | "f32" | "bf16" | "f16"),
 device_speed ("probe" or a list; Halda-style partition weights).
 """
