@@ -219,7 +219,7 @@ struct G4Geom {
 
 template <int PT, int EPI, int BM, bool MOE, int NWV = 8>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
-                                                    const int n_stages, const G4Moe mo) {
+                                                    const int n_stages, const G4Moe mo, const int spread) {
   constexpr int TW = 2;
   using Q3 = W3<PT>;
   using Q = W4<PT>;
@@ -279,6 +279,15 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 #pragma unroll
     for (int i = 0; i < G::A_INSTR; ++i) glds<16>(xsrc[i] + s * 128, stage_a(b) + apc[i] * 1024);
   };
+  auto issue_a1 = [&](int i, int s, int b) {
+#pragma unroll
+    for (int ii = 0; ii < G::A_INSTR; ++ii)
+      if (ii == i) glds<16>(xsrc[ii] + s * 128, stage_a(b) + apc[ii] * 1024);
+  };
+  // LDS-DMA issue schedule after the stage barrier: burst (spread == 0: every piece at the barrier,
+  // so the two waves of a SIMD both stop issuing MFMAs for the whole burst), or one piece per MFMA
+  // step (1), with waves 4-7 (the second wave of each SIMD) two steps later (2)
+  const int dma_shift = spread == 2 && wave >= 4 ? 2 : 0;
   auto issue_b = [&](int s, int b) {
     src.sb = s / 4; src.q = s % 4;
     Q3::template issue<TW>(stage_r(b), src, lane);
@@ -297,8 +306,10 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 #pragma unroll
   for (int t = 0; t < 4; ++t) aoff[t] = (uint32_t)g3_off(cl, 4 * (t >> 1) + 2 * h + (t & 1));
 
-  constexpr int NA = 4 * FR, AD = 8, NR = Q::NR, JB = NA - AD - 1;
+  // A fragments read AD steps ahead (8; half the stage's NA fragments for the 64-row MoE tile)
+  constexpr int NA = 4 * FR, AD = NA >= 16 ? 8 : NA / 2, NR = Q::NR, JB = NA - AD - 1;
   static_assert(JB > FR / 2 && NA - AD > JB, "gemm4: barrier step");
+  static_assert(JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
   typename Q::Raw raw;
   typename Q::Prep pr;
   half8_t bf[4];
@@ -341,9 +352,18 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
         wait_vmcnt<NIB>();   // x(s+1) and w(s+1) in: only w(s+2) (issued after x(s+1)) may be in flight
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        issue_a(min(s + 2, s_end - 1), b2);
-        issue_b(min(s + 3, s_end - 1), b);
+        if (!spread) {
+          issue_a(min(s + 2, s_end - 1), b2);
+          issue_b(min(s + 3, s_end - 1), b);
+        }
         Q::load(stage_r(b1), lane, raw_n);
+      }
+      if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
+        if (spread) {
+          const int slot = j - JB - dma_shift;
+          if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + 2, s_end - 1), b2);
+          if (slot == G::A_INSTR) issue_b(min(s + 3, s_end - 1), b);
+        }
       }
       if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
       if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
@@ -432,7 +452,7 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
   hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV>), dim3(n_cg * n_mb, nsplit, E), dim3(64 * NWV), 0, st,
-                     p, n_mb, per, n_stages, mo);
+                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD));
 }
 
 // rows per workgroup: 256 unless one 128-row block holds M, or 256-row tiles leave most of the 256
@@ -547,13 +567,18 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   mpk::G4Moe mo;
   mo.counts = q.counts; mo.lists = q.lists; mo.list_cap = q.list_cap; mo.estride = q.estride; mo.k = q.k;
   mo.x_per_slot = q.x_per_slot; mo.weights = q.weights; mo.Yslot = q.Yslot;
-  // row tile from the mean rows per expert (M k / E); split-K (down, atomics only) for the grid the
-  // ACTIVE row blocks form
+  // row tile from the mean rows per expert (M k / E): 64 rows up to a mean of 64 (Mixtral at 256
+  // tokens: 64 rows per expert; the 128-row tile ran half its MFMA rows on padding, 431 us for the
+  // gate/up: profiles/r8b_prof_mixtral_mb256.txt), 128 up to 128, else 256; split-K (down, atomics
+  // only) for the grid the ACTIVE row blocks form
   const int avg = std::max(1, q.M * q.k / std::max(1, q.E));
   const int n_cg = (q.ntiles + 15) / 16;
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
+  } else if (avg <= 64 && knob(KNOB_GEMM3_BM) != 128) {
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
+    gemm4_go<PT, EPI, 64, true>(p, ns, st, mo, q.E);
   } else if (avg <= 128) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);

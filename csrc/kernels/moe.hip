@@ -5,11 +5,64 @@
 #include "kcommon.h"
 #include "../runtime/tuning.h"
 #include <cstdlib>
+#include <stdexcept>
 #include "dequant.h"
 #include "../runtime/kernels_api.h"
 
 namespace mpk {
 using namespace mp;
+
+// Router logits [M][ld] = x[M][K] . R[E][K]^T on the dense f16 copy of the router (E <= 64 rows,
+// HipStage::build_router_dense).  RB token rows per 256-thread workgroup; each thread takes 8-k
+// slices (16-B loads, v_dot2 accumulation), then fixed-order wave and workgroup reductions: the
+// result is bitwise repeatable (no atomics), and the launch has M / RB workgroups whatever E is.
+// Through the generic GEMM paths this N = E call took 33 us at M = 256 (gemm3: one column group,
+// split-K capped at 4: profiles/r8b_prof_mixtral_mb256.txt).
+template <int RB>
+__global__ __launch_bounds__(256) void router_logits_kernel(const f16* __restrict__ X, int ldx,
+                                                            const f16* __restrict__ R, int K, int E, int M,
+                                                            float* __restrict__ out, int ld) {
+  __shared__ float red[4][RB][8];
+  const int m0 = blockIdx.x * RB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int e0 = 0; e0 < E; e0 += 8) {
+    float acc[RB][8];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[r][e] = 0.f;
+    for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+      half8_t xv[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+        xv[r] = m0 + r < M ? *reinterpret_cast<const half8_t*>(X + (size_t)(m0 + r) * ldx + k) : half8_t{};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (e0 + e >= E) break;
+        const half8_t w = *reinterpret_cast<const half8_t*>(R + (size_t)(e0 + e) * K + k);
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+          for (int j = 0; j < 8; j += 2)
+            acc[r][e] = __builtin_amdgcn_fdot2(half2_t{xv[r][j], xv[r][j + 1]}, half2_t{w[j], w[j + 1]}, acc[r][e], false);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = wave_sum(acc[r][e]);
+        if (lane == 0) red[wave][r][e] = v;
+      }
+    __syncthreads();
+    if (threadIdx.x < RB * 8) {
+      const int r = threadIdx.x >> 3, e = threadIdx.x & 7;
+      if (m0 + r < M && e0 + e < E)
+        out[(size_t)(m0 + r) * ld + e0 + e] = red[0][r][e] + red[1][r][e] + red[2][r][e] + red[3][r][e];
+    }
+    __syncthreads();
+  }
+}
 
 // one block of 1024 threads: softmax over E router logits per token, top-k, renormalise, bucket by
 // expert.  The bucket positions come from LDS atomics (a prompt chunk of 2048 tokens places 4096
@@ -246,6 +299,11 @@ __global__ __launch_bounds__(NW * 64) void moe_gemv2_kernel(const MoeGemvParams 
 }  // namespace mpk
 
 namespace mp {
+
+void launch_router_logits(const f16* X, int ldx, const f16* R, int K, int E, int M, float* out, int ld, hipStream_t st) {
+  if (K % 8 || E < 1 || E > 64 || M < 1) throw std::runtime_error("launch_router_logits: K % 8, 1 <= E <= 64, M >= 1");
+  hipLaunchKernelGGL(mpk::router_logits_kernel<4>, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, R, K, E, M, out, ld);
+}
 
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st) {
   hipLaunchKernelGGL(mpk::moe_route_kernel, dim3(1), dim3(1024), 0, st, p);

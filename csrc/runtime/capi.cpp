@@ -208,6 +208,45 @@ int mp_op_gemm4(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   API_CATCH(-1)
 }
 
+// MoE (K13): device-side top-k routing of router logits [M][ld] into per-expert slot lists
+int mp_op_moe_route(const void* logits, int ld, int M, int E, int k, void* counts, void* lists, int list_cap,
+                    void* weights, void* stream) {
+  API_TRY
+  MoeRouteParams rp{};
+  rp.logits = (const float*)logits; rp.ld = ld; rp.M = M; rp.E = E; rp.k = k;
+  rp.counts = (int32_t*)counts; rp.lists = (int32_t*)lists; rp.list_cap = list_cap; rp.weights = (float*)weights;
+  launch_moe_route(rp, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+// grouped expert GEMM (gemm4 MoE mode): SWIGLU (gate/up of every routed slot into H[slot]) or ATOMIC
+// (down: router-weighted into Y[slot / k]); W = E packed matrices, estride bytes apart
+int mp_op_moe_gemm4(int ptype, int epi, const void* W, int64_t estride, int ntiles, int nsb, const void* X, int ldx,
+                    int x_per_slot, int M, int E, int k, const void* counts, const void* lists, int list_cap,
+                    const void* weights, void* Y, int ldy, void* H, int ldh, int n_valid, void* stream) {
+  API_TRY
+  MoeGemvParams q{};
+  q.W = (const uint8_t*)W; q.estride = (size_t)estride; q.ntiles = ntiles; q.nsb = nsb;
+  q.X = (const f16*)X; q.ldx = ldx; q.x_per_slot = x_per_slot; q.M = M; q.E = E; q.k = k;
+  q.counts = (const int32_t*)counts; q.lists = (const int32_t*)lists; q.list_cap = list_cap;
+  q.weights = (const float*)weights; q.Y = (float*)Y; q.ldy = ldy; q.H = (f16*)H; q.ldh = ldh; q.n_valid = n_valid;
+  if (!launch_moe_gemm4(ptype, epi, q, (hipStream_t)stream)) throw std::runtime_error("moe_gemm4: unsupported type/epilogue");
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
+// router logits [M][ld] = X [M][ldx] . R [E][K]^T (dense f16 router)
+int mp_op_router_logits(const void* X, int ldx, const void* R, int K, int E, int M, void* out, int ld, void* stream) {
+  API_TRY
+  launch_router_logits((const f16*)X, ldx, (const f16*)R, K, E, M, (float*)out, ld, (hipStream_t)stream);
+  HIP_OK(hipGetLastError());
+  return 0;
+  API_CATCH(-1)
+}
+
 // split-K with partial stores + the fixed-order reduction into Y; returns the split count, 0 when
 // the shape does not split (nothing launched)
 int mp_op_gemm4_splitk(int ptype, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y, int ldy,

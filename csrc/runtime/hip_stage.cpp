@@ -425,6 +425,17 @@ void HipStage::build_i8_copies() {
 void HipStage::alloc_runtime() {
   HIP_OK(hipSetDevice(spec_.device));
   if (opt_.int8_gemm && opt_.prefill_gemm) build_i8_copies();
+  // MoE routers as dense f16 (E x d x 2 B per layer: 64 KB at Mixtral): the router-logits kernel
+  // reads them row-major, one launch of M / 4 workgroups for any micro-batch width
+  for (LayerW& L : layers_) {
+    if (!L.moe || !L.ex.router.d) continue;
+    const PackedMat& r = L.ex.router;
+    const size_t bytes = (size_t)r.dims.ntiles * 16 * r.dims.nsb * 256 * 2;
+    L.ex.router_dense = (f16*)dmalloc(bytes);
+    launch_unpack(r.ptype, r.d, (int)r.dims.ntiles, (int)r.dims.nsb, L.ex.router_dense, (int)r.dims.nsb * 256, stream_);
+    weight_bytes_ += bytes;
+  }
+  HIP_OK(hipStreamSynchronize(stream_));
   const int B = opt_.mb_size, NM = opt_.n_mb;
   const int d = cfg_.d_model, Hq = cfg_.n_head, Hkv = cfg_.n_head_kv;
   scratch_rows_ = std::max(B, opt_.prefill_chunk);
@@ -861,7 +872,10 @@ void HipStage::moe_ffn_rows(const LayerW& L, int r0, int M, hipStream_t st, floa
   float* logits = moe_logits_ + (size_t)r0 * 64;
   // router logits [M][E]: one 16-row tile, so split-K over the super-blocks (atomics into the
   // buffer the ffn RMSNorm cleared) instead of one serial workgroup (28.5 us -> a few us per layer)
-  gemv(L.ex.router, EPI_ATOMIC, xn, Kd_, M, logits, 64, nullptr, 0, E, true, st);
+  if (L.ex.router_dense && Kd_ >= (int)L.ex.router.dims.nsb * 256)
+    launch_router_logits(xn, Kd_, L.ex.router_dense, (int)L.ex.router.dims.nsb * 256, E, M, logits, 64, st);
+  else
+    gemv(L.ex.router, EPI_ATOMIC, xn, Kd_, M, logits, 64, nullptr, 0, E, true, st);
   MoeRouteParams rp{};
   rp.logits = logits; rp.ld = 64; rp.M = M; rp.E = E; rp.k = k;
   rp.counts = moe_counts_; rp.lists = moe_lists_; rp.list_cap = scratch_rows_ * k; rp.weights = moe_w_;

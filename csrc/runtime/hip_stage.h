@@ -54,6 +54,7 @@ struct ExpertW {  // MoE layer weights (Mixtral); experts stored back to back
   PackedMat down;              // E down matrices
   size_t down_stride = 0;
   PackedMat router;            // [E][d] router (f16 packed)
+  f16* router_dense = nullptr;  // the router unpacked to dense f16 [E_pad][nsb*256] (launch_router_logits)
 };
 
 struct LayerW {

@@ -280,6 +280,8 @@ struct MoeRouteParams {
   float* weights;        // [M*k] renormalised top-k softmax weights
 };
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st);
+// router logits [M][ld] (f32, stored) from x [M][ldx] f16 and the dense f16 router R [E][K], E <= 64
+void launch_router_logits(const f16* X, int ldx, const f16* R, int K, int E, int M, float* out, int ld, hipStream_t st);
 struct MoeGemvParams {
   const uint8_t* W;      // [E] packed matrices, each `estride` bytes
   size_t estride;

@@ -162,11 +162,13 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     int pages = 0;   // KV pages reserved for prompt + n_predict (paged KV admission control)
     std::vector<int32_t> prompt;   // for re-admission into a replacement engine after a fault
     double t0 = 0, t1 = 0;
+    bool resumed = false;          // requeued by a failover: keeps its timings and produced tokens
   };
   struct Pending {
     Served s;
-    std::vector<int32_t> prompt;
+    std::vector<int32_t> prompt;   // a resumed request: its prompt + the tokens it already produced
     int pages = 0;
+    std::unique_ptr<Live> resume;  // a running request a failover could not re-admit at once
   };
   // engine geometry: re-read after a failover (the replacement runs on fewer GPUs, so its KV
   // pool, context and slot count can all be smaller)
@@ -235,23 +237,40 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     live.clear();
     live.resize(cap);
     reserved = 0;
-    for (auto& pd : waiting) pd.pages = pages_for((long)pd.prompt.size(), pd.s.req.n_predict);
+    for (auto& pd : waiting)
+      pd.pages = pd.resume ? pages_for((long)pd.resume->prompt.size(), pd.resume->s.req.n_predict)
+                           : pages_for((long)pd.prompt.size(), pd.s.req.n_predict);
     // re-admit in order while the new engine has a slot, the context and the pages for the
-    // request's prompt + produced tokens + what it may still generate; the rest stop ("context")
+    // request's prompt + produced tokens + what it may still generate.  A request that fits the new
+    // engine but not right now (its slots or pages are taken) goes back to the FRONT of the queue,
+    // prompt + produced tokens as its prompt, and resumes when pages come back; only one that can
+    // never fit ends: stop "context" (its context exceeds the new max_ctx) or "failover" (its pages
+    // exceed the smaller engine's whole pool)
     std::vector<std::vector<int32_t>> prompts;
+    std::vector<Pending> requeue;
     for (auto& m : moved) {
       std::vector<int32_t> pr = m->prompt;
       pr.insert(pr.end(), m->res.tokens.begin(), m->res.tokens.end());
       const int pages = pages_for((long)m->prompt.size(), m->s.req.n_predict);
-      if ((int)prompts.size() < cap && (int)pr.size() + 1 < max_ctx && reserved + pages <= pool) {
+      const bool ctx_ok = (int)pr.size() + 1 < max_ctx, pool_ok = pages <= pool;
+      if ((int)prompts.size() < cap && ctx_ok && reserved + pages <= pool) {
         m->pages = pages;
         reserved += pages;
         live[prompts.size()] = std::move(m);
         prompts.push_back(std::move(pr));
         continue;
       }
+      if (ctx_ok && pool_ok) {
+        Pending pd;
+        pd.prompt = std::move(pr);
+        pd.pages = pages;
+        m->resumed = true;
+        pd.resume = std::move(m);
+        requeue.push_back(std::move(pd));
+        continue;
+      }
       Live& L = *m;
-      L.res.stop = "context";
+      L.res.stop = ctx_ok ? "failover" : "context";
       if (!L.acc.buf.empty()) {
         L.res.text += L.acc.buf;
         if (L.s.req.on_piece) L.s.req.on_piece(L.acc.buf);
@@ -259,6 +278,7 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       L.res.decode_ms = now_ms() - L.t1;
       if (L.s.done) L.s.done(L.res);
     }
+    for (auto it = requeue.rbegin(); it != requeue.rend(); ++it) waiting.push_front(std::move(*it));
     if (prompts.empty()) return false;
     eng_->start(prompts);   // a replacement fault propagates (the handler already had its turn)
     for (size_t i = 0; i < prompts.size(); ++i)
@@ -286,12 +306,15 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       waiting.pop_front();
       int sl = 0;
       while (live[sl] || std::find(slots.begin(), slots.end(), sl) != slots.end()) ++sl;
-      auto L = std::make_unique<Live>();
-      L->res.n_prompt = (int)pd.prompt.size();
+      std::unique_ptr<Live> L = std::move(pd.resume);
+      if (!L) {
+        L = std::make_unique<Live>();
+        L->res.n_prompt = (int)pd.prompt.size();
+        L->prompt = pd.prompt;
+        L->s = std::move(pd.s);
+        L->t0 = now_ms();
+      }
       L->pages = pd.pages;
-      L->prompt = pd.prompt;
-      L->s = std::move(pd.s);
-      L->t0 = now_ms();
       reserved += L->pages;
       live[sl] = std::move(L);
       slots.push_back(sl);
@@ -307,8 +330,10 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       const double t = now_ms();
       for (int sl : slots) {
         Live& L = *live[sl];
-        L.t1 = t;
-        L.res.prefill_ms = t - L.t0;
+        if (!L.resumed) {
+          L.t1 = t;
+          L.res.prefill_ms = t - L.t0;
+        }
         if (L.s.req.n_predict <= 0 || !consume(sl, eng_->last_token(sl))) finish(sl);
       }
     }

@@ -52,6 +52,11 @@ _SIGS = {
     "mp_set_gemm3_tuning": ([c_int, c_int, c_int, c_int], c_int),
     "mp_op_gemm4": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                      c_int, c_int, c_int, c_void_p], c_int),
+    "mp_op_moe_route": ([c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p], c_int),
+    "mp_op_moe_gemm4": ([c_int, c_int, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                         c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
+                        c_int),
+    "mp_op_router_logits": ([c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_gemm4_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             ctypes.c_longlong, c_void_p], c_int),
     "mp_op_gemm2_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,

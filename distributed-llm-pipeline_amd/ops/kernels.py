@@ -148,6 +148,42 @@ def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4) -
                    "gemm_splitk")
 
 
+def moe_route(logits: torch.Tensor, k: int, list_cap: int | None = None):
+    """Top-k routing of router logits [M][E] (f32, contiguous): returns (counts [E], lists [E][list_cap]
+    of token-slot ids t * k + j, renormalised top-k weights [M * k])."""
+    M, E = logits.shape
+    list_cap = list_cap or M * k
+    counts = torch.zeros(E, dtype=torch.int32, device=logits.device)
+    lists = torch.full((E, list_cap), -1, dtype=torch.int32, device=logits.device)
+    weights = torch.zeros(M * k, dtype=torch.float32, device=logits.device)
+    N.check(N.lib().mp_op_moe_route(_ptr(logits), logits.stride(0), M, E, k, _ptr(counts), _ptr(lists), list_cap,
+                                    _ptr(weights), _stream()), "moe_route")
+    return counts, lists, weights
+
+
+def moe_gemm(w_dev: torch.Tensor, estride: int, ptype: int, ntiles: int, nsb: int, n_valid: int, epi: int,
+             x: torch.Tensor, M: int, E: int, k: int, counts, lists, weights=None, *, x_per_slot: bool = False,
+             h: torch.Tensor | None = None, y: torch.Tensor | None = None) -> None:
+    """Grouped expert GEMM (gemm4 MoE mode, K13) over E packed matrices estride bytes apart:
+    EPI_SWIGLU writes h[slot] = SwiGLU(x[slot // k] W_e^T) for every routed slot; EPI_ATOMIC adds
+    weights[slot] * (x[slot] W_e^T) into y[slot // k] (x_per_slot: x rows are slots)."""
+    assert x.dtype == torch.float16 and x.is_contiguous()
+    N.check(N.lib().mp_op_moe_gemm4(ptype, epi, _ptr(w_dev), estride, ntiles, nsb, _ptr(x), x.stride(0),
+                                    int(x_per_slot), M, E, k, _ptr(counts), _ptr(lists), lists.shape[1],
+                                    _ptr(weights), _ptr(y), y.stride(0) if y is not None else 0, _ptr(h),
+                                    h.stride(0) if h is not None else 0, n_valid, _stream()), "moe_gemm4")
+
+
+def router_logits(x: torch.Tensor, r_dense: torch.Tensor) -> torch.Tensor:
+    """logits [M][E] f32 = x [M][K] f16 . r_dense [E][K]^T (the dense-router kernel, E <= 64)."""
+    M, K = x.shape[0], r_dense.shape[1]
+    E = r_dense.shape[0]
+    out = torch.zeros(M, 64, dtype=torch.float32, device=x.device)
+    N.check(N.lib().mp_op_router_logits(_ptr(x), x.stride(0), _ptr(r_dense.contiguous()), K, E, M, _ptr(out), 64,
+                                        _stream()), "router_logits")
+    return out[:, :E]
+
+
 class I8Weight:
     """Per-row int8 re-quantization of a packed weight for the int8-activation GEMM prototype
     (SURVEY K15): w8[n][k] = round(w[n][k] / ws[n]), ws[n] = max_k |w[n][k]| / 127, packed into P_I8
