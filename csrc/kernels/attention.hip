@@ -370,31 +370,24 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   const int n_act = (kvlen + p.split_len - 1) / p.split_len;
   if (z >= n_act) return;
 
-  // 1. q fragments with RoPE applied in registers (decode_q_frags)
-  half8_t qf[KK];
-  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
-
-  // 2. append the new token's K (rotated) and V to the cache.  The split that reads the new token
-  // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
-  // wave waits for its own global append to land (no store -> barrier -> load round trip) and the
-  // first chunk's K/V loads are in flight before the append starts.
+  // 1. the new token's K / V inputs (the split that owns the position) and, without the pre-load,
+  // this wave's first chunk: issued BEFORE the q fragments' loads, so the one wait the q build
+  // ends with covers them too (issued after it, the append's loads had cost a third dependent
+  // global round trip per call: the single-stream fixed cost, profiles/r8d_attn_ctx_sweep.txt)
   __shared__ __attribute__((aligned(16))) f16 sm_kn[DP];
   __shared__ f16 sm_vn[DP];
   const bool owns = start <= pos && pos < end;
   const int nch = (end - start + 31) / 32;
-  if (PF && !pre && wv < nch) load(wv, kA, vA);   // in flight during the append
-
+  if (PF && !pre && wv < nch) load(wv, kA, vA);   // in flight during the q build and the append
+  const int j = threadIdx.x;   // the append: one K pair and one V element per thread (DP <= 256 threads)
+  float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
+  float vx = 0.f, vb = 0.f;
+  const bool kin = j < hd2, vin = j < p.hd;
+  int a_page = 0;
   if (owns) {
-    const int page = bt[pos >> 6], idx = pos & 63;
+    a_page = bt[pos >> 6];
     const int kr = p.Hq * p.hd + kvh * p.hd;
     const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
-    const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;     // element offsets
-    const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
-    // one K pair and one V element per thread (DP <= 256 threads), all reads issued before any use
-    const int j = threadIdx.x;
-    float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
-    float vx = 0.f, vb = 0.f;
-    const bool kin = j < hd2, vin = j < p.hd;
     if (kin) {
       kx = *reinterpret_cast<const float2*>(row + kr + 2 * j);
       c = cs[j];
@@ -404,6 +397,19 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       vx = row[vr + j];
       if (p.bias) vb = p.bias[vr + j];
     }
+  }
+
+  // 2. q fragments with RoPE applied in registers (decode_q_frags)
+  half8_t qf[KK];
+  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+
+  // 3. append the new token's K (rotated) and V to the cache.  The split that reads the new token
+  // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
+  // wave waits for its own global append to land (no store -> barrier -> load round trip).
+  if (owns) {
+    const int page = a_page, idx = pos & 63;
+    const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;     // element offsets
+    const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
     if (j < DP / 2) {
       const float x0 = fmaf(nrs, kx.x, kb.x), x1 = fmaf(nrs, kx.y, kb.y);
       const float r0 = kin ? x0 * c.x - x1 * c.y : 0.f, r1 = kin ? x0 * c.y + x1 * c.x : 0.f;
@@ -702,32 +708,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   load(0, kA, vA);   // in flight during the q build and the append
   if (nch > 1) load(1, kB, vB);
 
-  half8_t qf[KK];
-  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
-
   // the split holding the new position appends its K (rotated) / V and keeps them in this wave's
-  // LDS slice to patch the chunk that holds it (the chunk's loads may predate the append)
+  // LDS slice to patch the chunk that holds it (the chunk's loads may predate the append).  Its
+  // inputs are loaded before the q build, so the q build's wait covers them (no third round trip)
   const bool owns = start <= pos && pos < end;
   f16* kn = sm_kn[wv];
   f16* vn = sm_vn[wv];
+  constexpr int KJ = (DP / 2 + 63) / 64, VJ = DP / 64;
+  float2 kx[KJ], kb[KJ], cc[KJ];
+  float vx[VJ], vb[VJ];
+  int a_page = 0;
+  const int kr = p.Hq * p.hd + kvh * p.hd;
+  const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
   if (owns) {
-    const int page = bt[pos >> 6], idx = pos & 63;
-    const int kr = p.Hq * p.hd + kvh * p.hd;
-    const int vr = (p.Hq + p.Hkv) * p.hd + kvh * p.hd;
+    a_page = bt[pos >> 6];
+#pragma unroll
+    for (int jj = 0; jj < KJ; ++jj) {   // K: one pair per lane per 128 dims
+      const int j = lane + 64 * jj;
+      kx[jj] = kb[jj] = float2{0.f, 0.f};
+      cc[jj] = float2{1.f, 0.f};
+      if (j < DP / 2 && j < hd2) {
+        kx[jj] = *reinterpret_cast<const float2*>(row + kr + 2 * j);
+        cc[jj] = cs[j];
+        if (p.bias) kb[jj] = *reinterpret_cast<const float2*>(p.bias + kr + 2 * j);
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < VJ; ++jj) {    // V: one element per lane per 64 dims
+      const int j = lane + 64 * jj;
+      vx[jj] = vb[jj] = 0.f;
+      if (j < p.hd) {
+        vx[jj] = row[vr + j];
+        if (p.bias) vb[jj] = p.bias[vr + j];
+      }
+    }
+  }
+
+  half8_t qf[KK];
+  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+
+  if (owns) {
+    const int page = a_page, idx = pos & 63;
     const size_t koff = (((size_t)page * p.Hkv + kvh) * 64 + idx) * DP;
     const size_t voff = ((size_t)page * p.Hkv + kvh) * DP * 64 + idx;
 #pragma unroll
-    for (int jj = 0; jj < (DP / 2 + 63) / 64; ++jj) {   // K: one pair per lane per 128 dims
+    for (int jj = 0; jj < KJ; ++jj) {
       const int j = lane + 64 * jj;
       if (j >= DP / 2) break;
       const bool kin = j < hd2;
-      float2 kx = {0.f, 0.f}, kb = {0.f, 0.f}, c = {1.f, 0.f};
-      if (kin) {
-        kx = *reinterpret_cast<const float2*>(row + kr + 2 * j);
-        c = cs[j];
-        if (p.bias) kb = *reinterpret_cast<const float2*>(p.bias + kr + 2 * j);
-      }
-      const float x0 = fmaf(nrs, kx.x, kb.x), x1 = fmaf(nrs, kx.y, kb.y);
+      const float x0 = fmaf(nrs, kx[jj].x, kb[jj].x), x1 = fmaf(nrs, kx[jj].y, kb[jj].y);
+      const float2 c = cc[jj];
       const float r0 = kin ? x0 * c.x - x1 * c.y : 0.f, r1 = kin ? x0 * c.y + x1 * c.x : 0.f;
       half2_t o;
       if constexpr (F8) {
@@ -741,10 +771,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       *reinterpret_cast<half2_t*>(kn + 2 * j) = o;
     }
 #pragma unroll
-    for (int jj = 0; jj < DP / 64; ++jj) {    // V: one element per lane per 64 dims
+    for (int jj = 0; jj < VJ; ++jj) {
       const int j = lane + 64 * jj;
       const bool vin = j < p.hd;
-      const float vv = vin ? fmaf(nrs, row[vr + j], p.bias ? p.bias[vr + j] : 0.f) : 0.f;
+      const float vv = vin ? fmaf(nrs, vx[jj], vb[jj]) : 0.f;
       f16 v;
       if constexpr (F8) {
         const uint32_t q = f8x2_pack(vv, 0.f);

@@ -573,6 +573,9 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   // only) for the grid the ACTIVE row blocks form
   const int avg = std::max(1, q.M * q.k / std::max(1, q.E));
   const int n_cg = (q.ntiles + 15) / 16;
+  auto g4_splits = [&](int wgs, int n_stages) {   // the GEMM3_SPLIT knob forces it (A/B runs)
+    return knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : mp::g4_splits(wgs, n_stages);
+  };
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);

@@ -26,8 +26,9 @@ def _run(syn, ftype, mb, stages=1, **kw):
 
 @pytest.mark.parametrize("mb", [1, 16, 64, 128, 256])
 def test_deterministic_bitwise_runs_and_pp2(cuda, native, mb):
-    """mb > 64 runs the decode projections on the GEMMs (gemm2 / gemm3): deterministic mode turns
-    their split-K off, so every output element has one writer and a fixed k order."""
+    """mb > 64 runs the decode projections on the GEMMs: the split-K ones (qkv / o / down, gemm2)
+    store per-split partials that a fixed-order reduction adds (`gemm_splitk_store`, the default);
+    the whole-K ones (gate/up, the LM head, gemm4) have one writer per output element."""
     a, ta = _run(WIDE, "Q4_K", mb, deterministic=True)
     b, tb = _run(WIDE, "Q4_K", mb, deterministic=True)
     assert np.array_equal(a, b), float(np.abs(a - b).max())
@@ -35,6 +36,16 @@ def test_deterministic_bitwise_runs_and_pp2(cuda, native, mb):
     c, tc = _run(WIDE, "Q4_K", mb, stages=2, deterministic=True)
     assert np.array_equal(a, c), float(np.abs(a - c).max())
     assert ta == tc
+
+
+@pytest.mark.parametrize("ftype,mb,sk", [("Q4_K", 128, False), ("BF16", 128, True), ("BF16", 256, False)])
+def test_deterministic_wide_paths(cuda, native, ftype, mb, sk):
+    """The other wide-batch paths of deterministic mode: split-K partial stores off (the GEMMs then
+    run unsplit) and 16-bit weights (gemm3, unsplit in deterministic mode)."""
+    a, ta = _run(WIDE, ftype, mb, deterministic=True, gemm_splitk_store=sk)
+    b, tb = _run(WIDE, ftype, mb, deterministic=True, gemm_splitk_store=sk)
+    assert np.array_equal(a, b), float(np.abs(a - b).max())
+    assert ta == tb
 
 
 def test_deterministic_close_to_default(cuda, native):
