@@ -306,6 +306,10 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
 
 }
 
+#ifdef MIPIPE_TIMING_PROBES
+__device__ int g_attn_probe_calls = 0;
+#endif
+
 template <int DP, bool F8, bool PF>
 __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
                                                  f16* xo = nullptr) {
@@ -322,6 +326,16 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   __shared__ int sm_last;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef MIPIPE_TIMING_PROBES
+  // bit 2 of the probe: per-phase timestamps of wave 0 (100 MHz s_memrealtime), printed for the
+  // first calls by block (0, 0, 0): where a short context's fixed cost goes
+  uint64_t ts[8] = {};
+  const bool stamp = (p.probe & 4) && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0;
+#define ATT_STAMP(i) do { if (stamp) ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define ATT_STAMP(i) do {} while (0)
+#endif
+  ATT_STAMP(0);
   const int q4 = lane >> 4, col = lane & 15;
   const int G = p.Hq / p.Hkv;
   const int g = col;
@@ -363,12 +377,18 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // slot's block-table row: split_len may exceed max_pages * 64)
   const bool pre = PF && p.n_split == 1 && 32 * wv < min(p.split_len, p.max_pages * 64 - start);
   if (pre) load(wv, kA, vA);
+  // and its second chunk (keys 128-255 of the split): with it loaded only inside the chunk loop,
+  // after the q build, wave 0 waited one more dependent round trip at 129-256 keys (the 8B single
+  // stream's ~2.8 us chunk phase, r8i attention stamps)
+  const bool pre2 = pre && 32 * (wv + 4) < min(p.split_len, p.max_pages * 64 - start);
+  if (pre2) load(wv + 4, kB, vB);
 
   const int end = min(start + p.split_len, kvlen);
   // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
   // single active split writes the output directly, so short contexts pay no merge round trip
   const int n_act = (kvlen + p.split_len - 1) / p.split_len;
   if (z >= n_act) return;
+  ATT_STAMP(1);
 
   // 1. the new token's K / V inputs (the split that owns the position) and, without the pre-load,
   // this wave's first chunk: issued BEFORE the q fragments' loads, so the one wait the q build
@@ -402,6 +422,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // 2. q fragments with RoPE applied in registers (decode_q_frags)
   half8_t qf[KK];
   decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+  ATT_STAMP(2);
 
   // 3. append the new token's K (rotated) and V to the cache.  The split that reads the new token
   // also keeps them in LDS and patches them into the registers of the chunk that holds it, so no
@@ -442,6 +463,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   }
+  ATT_STAMP(3);
 
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[DT];
@@ -526,7 +548,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // waves take chunks wv, wv + 4, ...; the next chunk's loads are issued before this one's math
   if constexpr (PF) {
     for (int ci = wv; ci < nch;) {
-      if (ci + 4 < nch) load(ci + 4, kB, vB);
+      if (ci + 4 < nch && !(pre2 && ci == wv)) load(ci + 4, kB, vB);
       step(ci, kA, vA);
       ci += 4;
       if (ci >= nch) break;
@@ -542,6 +564,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   }
   l_run += __shfl_xor(l_run, 16);
   l_run += __shfl_xor(l_run, 32);
+  ATT_STAMP(4);
   if (q4 == 0) { sm_m[wave][col] = m_run; sm_l[wave][col] = l_run; }
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -580,6 +603,15 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       }
     }
   }
+#ifdef MIPIPE_TIMING_PROBES
+  if (stamp) {
+    __builtin_amdgcn_s_waitcnt(0);
+    ts[5] = __builtin_amdgcn_s_memrealtime();
+    if (atomicAdd(&g_attn_probe_calls, 1) < 6)
+      printf("attn stamps (x10 ns from entry): pos %d  pos/bt %d  q+loads %d  append %d  chunks %d  merge+store %d\n", pos,
+             (int)(ts[1] - ts[0]), (int)(ts[2] - ts[0]), (int)(ts[3] - ts[0]), (int)(ts[4] - ts[0]), (int)(ts[5] - ts[0]));
+  }
+#endif
   if (n_act == 1) return;
   // 4. last arriver of this (token, kv head) merges the splits.
   // Hand-off invariant (MI355X_MICROARCH.md 'Valid forms', first row of the sc1 table, measured on

@@ -212,7 +212,10 @@ struct G4Geom {
   static constexpr int A_BYTES = BM * 128;                    // x rows of one 64-k stage
   static constexpr int R_WAVE = W3<PT>::RAW(2);              // one wave's raw bytes of one stage
   static constexpr int STAGE = A_BYTES + NWV * R_WAVE;
-  static constexpr int NB = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  // stage buffers (x issued NB - 1 stages ahead, weights NB; the kernel handles 3-5)
+  // (4-5 buffers for the 128-row tiles measured slower: MoE gate/up 454 -> 454 us at 128 rows, 499
+  // -> 713 at 64 rows, where 5 buffers also cost the second workgroup per CU; r8j)
+  static constexpr int NB = 3;
   static constexpr int NP = BM / 8;                           // 1-KB A pieces (8 rows) per stage
   static constexpr int A_INSTR = (NP + NWV - 1) / NWV;        // per wave (uniform: vmcnt accounting)
 };
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   using G = G4Geom<PT, BM, NWV>;
   constexpr int NB = G::NB, FR = BM / 32, BN = 32 * NWV;
   constexpr bool BF = PT == P_BF16;
-  static_assert(NB == 3, "gemm4: the cross-stage stream needs 3 stage buffers");
+  static_assert(NB >= 3 && NB <= 5, "gemm4: 3-5 stage buffers");
   __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 
   W3Src src;
   src.W = Wbase; src.t0 = cg * (BN / 16) + wave * TW; src.ntiles = p.ntiles; src.nsb = p.nsb;
+  src.nt = (spread & 4) != 0;   // flags: bits 0-1 DMA spread mode, bit 2 non-temporal weights
   auto stage_a = [&](int b) { return smem + b * G::STAGE; };
   auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
   // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7 (swizzled on the source side):
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   // LDS-DMA issue schedule after the stage barrier: burst (spread == 0: every piece at the barrier,
   // so the two waves of a SIMD both stop issuing MFMAs for the whole burst), or one piece per MFMA
   // step (1), with waves 4-7 (the second wave of each SIMD) two steps later (2)
-  const int dma_shift = spread == 2 && wave >= 4 ? 2 : 0;
+  const int dma_shift = (spread & 3) == 2 && wave >= 4 ? 2 : 0;
   auto issue_b = [&](int s, int b) {
     src.sb = s / 4; src.q = s % 4;
     Q3::template issue<TW>(stage_r(b), src, lane);
@@ -319,13 +323,15 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
     ds_b128o<(j % FR) * 4096>(dst, lds_addr(stage_a(b)) + aoff[j / FR]);
   };
 
-  // prologue: stages 0, 1 (and 2's weights) in flight; stage 0's raw, first AD fragments, frag 0
-  issue_a(s_begin, 0);
-  issue_b(s_begin, 0);
-  issue_a(min(s_begin + 1, s_end - 1), 1);
-  issue_b(min(s_begin + 1, s_end - 1), 1);
-  issue_b(min(s_begin + 2, s_end - 1), 2);
-  wait_vmcnt<G::A_INSTR + 2 * NIB>();
+  // prologue: x of stages 0 .. NB-2 and weights of 0 .. NB-1 in flight (issue order x0 w0 x1 w1 ..
+  // w(NB-1)); then stage 0's raw, first AD fragments, frag 0
+  static_for<NB - 1>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    issue_a(min(s_begin + i, s_end - 1), i);
+    issue_b(min(s_begin + i, s_end - 1), i);
+  });
+  issue_b(min(s_begin + NB - 1, s_end - 1), NB - 1);
+  wait_vmcnt<(NB - 2) * (G::A_INSTR + NIB) + NIB>();
   __builtin_amdgcn_s_barrier();
   Q::load(stage_r(0), lane, raw);
   static_for<AD>([&](auto jc) { read_a(jc, af[decltype(jc)::value], 0); });
@@ -337,7 +343,8 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   using PrepT = typename Q::Prep;
   auto stage = [&](const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n, PrepT& pr,
                    PrepT& pr_n) {
-    const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;   // buffers of stages s+1, s+2 (= s-1)
+    // buffers of stages s+1 and s-1 (= s+NB-1, the next x issue); weights of s+NB go to b itself
+    const int b1 = b + 1 == NB ? 0 : b + 1, b2 = b == 0 ? NB - 1 : b - 1;
     static_for<NA>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       constexpr int t = j / FR, i = j % FR;
@@ -349,20 +356,22 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       // stage's value was FR steps ago)
       if constexpr (i == FR / 2 && t < 3) bf[t + 1] = Q::frag(raw, pr, t + 1, h, kc);
       if constexpr (j == JB) {
-        wait_vmcnt<NIB>();   // x(s+1) and w(s+1) in: only w(s+2) (issued after x(s+1)) may be in flight
+        // x(s+1) and w(s+1) in: w(s+2) (issued with x(s+1)) and the NB - 3 later stages' x and w may
+        // be in flight
+        wait_vmcnt<NIB + (NB - 3) * (G::A_INSTR + NIB)>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (!spread) {
-          issue_a(min(s + 2, s_end - 1), b2);
-          issue_b(min(s + 3, s_end - 1), b);
+        if (!(spread & 3)) {
+          issue_a(min(s + NB - 1, s_end - 1), b2);
+          issue_b(min(s + NB, s_end - 1), b);
         }
         Q::load(stage_r(b1), lane, raw_n);
       }
       if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
-        if (spread) {
+        if (spread & 3) {
           const int slot = j - JB - dma_shift;
-          if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + 2, s_end - 1), b2);
-          if (slot == G::A_INSTR) issue_b(min(s + 3, s_end - 1), b);
+          if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + NB - 1, s_end - 1), b2);
+          if (slot == G::A_INSTR) issue_b(min(s + NB, s_end - 1), b);
         }
       }
       if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
@@ -379,9 +388,9 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   int s = s_begin, b = 0;
   for (; s + 1 < s_end; s += 2) {
     stage(s, b, af, afB, raw, rawB, pr, prB);
-    b = b == 2 ? 0 : b + 1;
+    b = b + 1 == NB ? 0 : b + 1;
     stage(s + 1, b, afB, af, rawB, raw, prB, pr);
-    b = b == 2 ? 0 : b + 1;
+    b = b + 1 == NB ? 0 : b + 1;
   }
   if (s < s_end) stage(s, b, af, afB, raw, rawB, pr, prB);
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
@@ -452,7 +461,7 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
   hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV>), dim3(n_cg * n_mb, nsplit, E), dim3(64 * NWV), 0, st,
-                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD));
+                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD) | (knob(KNOB_GEMM4_WNT) ? 4 : 0));
 }
 
 // rows per workgroup: 256 unless one 128-row block holds M, or 256-row tiles leave most of the 256
@@ -567,10 +576,10 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   mpk::G4Moe mo;
   mo.counts = q.counts; mo.lists = q.lists; mo.list_cap = q.list_cap; mo.estride = q.estride; mo.k = q.k;
   mo.x_per_slot = q.x_per_slot; mo.weights = q.weights; mo.Yslot = q.Yslot;
-  // row tile from the mean rows per expert (M k / E): 64 rows up to a mean of 64 (Mixtral at 256
-  // tokens: 64 rows per expert; the 128-row tile ran half its MFMA rows on padding, 431 us for the
-  // gate/up: profiles/r8b_prof_mixtral_mb256.txt), 128 up to 128, else 256; split-K (down, atomics
-  // only) for the grid the ACTIVE row blocks form
+  // row tile from the mean rows per expert (M k / E): 128 up to 128, else 256; split-K (down, atomics
+  // only) for the grid the ACTIVE row blocks form.  A 64-row tile (knob GEMM4_MOE64) drops the
+  // padding rows of Mixtral's 64 rows per expert at 256 tokens but halves the MFMAs per stage for
+  // the same per-stage overhead: gate/up 499 vs 454 us, 8036 vs 8920 tok/s (profiles/r8ij_engine_ab.txt)
   const int avg = std::max(1, q.M * q.k / std::max(1, q.E));
   const int n_cg = (q.ntiles + 15) / 16;
   auto g4_splits = [&](int wgs, int n_stages) {   // the GEMM3_SPLIT knob forces it (A/B runs)
@@ -579,7 +588,7 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
-  } else if (avg <= 64 && knob(KNOB_GEMM3_BM) != 128) {
+  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64)) {   // opt-in: measured slower (r8i)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 64, true>(p, ns, st, mo, q.E);
   } else if (avg <= 128) {

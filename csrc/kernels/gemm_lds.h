@@ -32,11 +32,22 @@ __device__ __forceinline__ void glds(const void* g, char* lds) {
   else
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
 }
+// the same with the non-temporal policy when nt (wave-uniform): streamed weights that one workgroup
+// reads once, so they do not evict the x rows every column group re-reads from L2
+template <int SZ>
+__device__ __forceinline__ void glds(bool nt, const void* g, char* lds) {
+  if (!nt) return glds<SZ>(g, lds);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_t*)lds);
+  if constexpr (SZ == 16)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+}
 // one LDS-DMA wave instruction whose lanes >= n are masked off (every wave issues it: uniform
 // vmcnt accounting)
 template <int SZ, class F>
-__device__ __forceinline__ void glds_n(char* lds, int n, int lane, F src) {
-  if (lane < n) glds<SZ>(src(lane), lds);
+__device__ __forceinline__ void glds_n(bool nt, char* lds, int n, int lane, F src) {
+  if (lane < n) glds<SZ>(nt, src(lane), lds);
 }
 
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima), gfx9 encoding
@@ -78,6 +89,7 @@ __device__ __forceinline__ half8_t nib8(uint32_t w, half2_t S, half2_t M, const 
 struct W3Src {
   const uint8_t* W;
   int t0, ntiles, nsb, sb, q;   // t0: the wave's first tile
+  bool nt = false;              // non-temporal weight DMA
   __device__ __forceinline__ const uint8_t* chunk(int u, int CB) const {
     const int t = min(t0 + u, ntiles - 1);
     return W + ((size_t)t * nsb + sb) * CB;
@@ -134,10 +146,10 @@ template <> struct W3<P_Q4_K> {
   struct Prep { half2_t S2, M2; };
   template <int TW>
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<16>(R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16; });
+    glds_n<16>(c.nt, R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -171,14 +183,14 @@ template <> struct W3<P_Q5_K> {
   struct Prep { half2_t S2, M2; };
   template <int TW>
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
     // 16-B entries = 4 rows' high-bit words: entry f -> (u, h, rows 4 (f & 3) ..)
-    glds_n<16>(R + TW * 512, 8 * TW, lane, [&](int f) {
+    glds_n<16>(c.nt, R + TW * 512, 8 * TW, lane, [&](int f) {
       return c.chunk(f >> 3, CB) + 2048 + ((f >> 2) & 1) * 256 + (16 * c.q + 4 * (f & 3)) * 4;
     });
-    glds_n<16>(R + TW * 640, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2560 + (e & 15) * 16; });
+    glds_n<16>(c.nt, R + TW * 640, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2560 + (e & 15) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -226,14 +238,14 @@ template <> struct W3<P_Q6_K> {
   struct Prep { uint32_t sc; f16 d; };
   template <int TW>
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<16>(R + TW * 512, 16 * TW, lane, [&](int f) {   // (u, h): 16 rows x 8 B contiguous
+    glds_n<16>(c.nt, R + TW * 512, 16 * TW, lane, [&](int f) {   // (u, h): 16 rows x 8 B contiguous
       return c.chunk(f >> 4, CB) + 2048 + ((f >> 3) & 1) * 512 + 16 * c.q * 8 + (f & 7) * 16;
     });
-    glds_n<4>(R + TW * 768, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 3072 + (e & 15) * 16 + 4 * c.q; });
-    glds_n<16>(R + TW * 832, 2 * TW, lane, [&](int f) { return c.chunk(f >> 1, CB) + 3328 + (f & 1) * 16; });
+    glds_n<4>(c.nt, R + TW * 768, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 3072 + (e & 15) * 16 + 4 * c.q; });
+    glds_n<16>(c.nt, R + TW * 832, 2 * TW, lane, [&](int f) { return c.chunk(f >> 1, CB) + 3328 + (f & 1) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -285,8 +297,8 @@ template <> struct W3<P_Q8_0> {
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
 #pragma unroll
     for (int u = 0; u < TW; ++u)   // 64 entries of 16 B per tile: (h, r, half)
-      glds<16>(c.chunk(u, CB) + (lane >> 5) * 2048 + (16 * c.q + ((lane >> 1) & 15)) * 32 + 16 * (lane & 1), R + u * 1024);
-    glds_n<4>(R + TW * 1024, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 4096 + (e & 15) * 16 + 4 * c.q; });
+      glds<16>(c.nt, c.chunk(u, CB) + (lane >> 5) * 2048 + (16 * c.q + ((lane >> 1) & 15)) * 32 + 16 * (lane & 1), R + u * 1024);
+    glds_n<4>(c.nt, R + TW * 1024, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 4096 + (e & 15) * 16 + 4 * c.q; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -322,10 +334,10 @@ template <> struct W3<P_Q4_0> {
   struct Prep { uint32_t dd; };
   template <int TW>
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(R, 32 * TW, lane, [&](int e) {
+    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<4>(R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16 + 4 * c.q; });
+    glds_n<4>(c.nt, R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16 + 4 * c.q; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -363,7 +375,7 @@ template <int PT> struct W3_16 {
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
 #pragma unroll
     for (int f = 0; f < 2 * TW; ++f)
-      glds<16>(c.chunk(f >> 1, CB) + (4 * (f & 1) + (lane >> 4)) * 1024 + (16 * c.q + (lane & 15)) * 16, R + f * 1024);
+      glds<16>(c.nt, c.chunk(f >> 1, CB) + (4 * (f & 1) + (lane >> 4)) * 1024 + (16 * c.q + (lane & 15)) * 16, R + f * 1024);
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -398,7 +410,7 @@ template <> struct W3<P_I8> {
   __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
 #pragma unroll
     for (int f = 0; f < 2 * TW; ++f)
-      glds<16>(c.chunk(f >> 1, CB) + ((2 * c.q + (f & 1)) * 64 + lane) * 16, R + f * 1024);
+      glds<16>(c.nt, c.chunk(f >> 1, CB) + ((2 * c.q + (f & 1)) * 64 + lane) * 16, R + f * 1024);
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {

@@ -302,7 +302,10 @@ namespace mp {
 
 void launch_router_logits(const f16* X, int ldx, const f16* R, int K, int E, int M, float* out, int ld, hipStream_t st) {
   if (K % 8 || E < 1 || E > 64 || M < 1) throw std::runtime_error("launch_router_logits: K % 8, 1 <= E <= 64, M >= 1");
-  hipLaunchKernelGGL(mpk::router_logits_kernel<4>, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, R, K, E, M, out, ld);
+  // one row per workgroup up to 1024 rows (M = 256: 256 workgroups; 4 rows each took 10.5 us per
+  // Mixtral layer on 64 workgroups, profiles/r8i_*), 4 rows per workgroup for longer prompt chunks
+  if (M <= 1024) hipLaunchKernelGGL(mpk::router_logits_kernel<1>, dim3(M), dim3(256), 0, st, X, ldx, R, K, E, M, out, ld);
+  else hipLaunchKernelGGL(mpk::router_logits_kernel<4>, dim3((M + 3) / 4), dim3(256), 0, st, X, ldx, R, K, E, M, out, ld);
 }
 
 void launch_moe_route(const MoeRouteParams& p, hipStream_t st) {

@@ -10,3 +10,10 @@ export MIPIPE_GEMM4_SPREAD=2; pr 70sp2
 unset MIPIPE_GEMM4_SPREAD
 pr mx64 --model mixtral-8x7b --ftype Q4_K_M
 export MIPIPE_GEMM3_BM=128; pr mx128 --model mixtral-8x7b --ftype Q4_K_M; unset MIPIPE_GEMM3_BM
+# single-stream attention phase stamps (probe library, printf from block 0; graphs off so prints flush)
+cd $R
+MIPIPE_LIB=../lib_probes/libmipipe.so MIPIPE_ATTN_PROBE=4 timeout -k 10 200 python3 bench.py --model llama3-8b --ftype Q4_K_M --mb-size 1 --no-secondary --steps 3 --warmup 1 --no-graphs > $O/r8i_stamps.log 2>&1 || { tail -3 $O/r8i_stamps.log; exit 1; }
+grep "attn stamps" $O/r8i_stamps.log | head -6
+# the driver's default bench line (all secondaries), timed
+t0=$(date +%s); timeout -k 10 600 python3 bench.py > $O/r8i_bench.log 2>&1 || { tail -3 $O/r8i_bench.log; exit 1; }; echo "bench wall $(( $(date +%s) - t0 )) s"
+tail -2 $O/r8i_bench.log | cut -c1-3000

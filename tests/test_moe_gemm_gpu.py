@@ -4,9 +4,9 @@ at Mixtral-8x7B widths (d 4096, d_ff 14336, 8 experts, top-2) against a plain Py
 The weights are random GGUF blocks (Q4_K gate/up, Q6_K down, as in Mixtral Q4_K_M), packed by the
 engine's packer; the oracle dequantizes them with the unpack kernel (itself checked against the
 numpy dequantizer in test_kernels_gpu.py) and runs fp32 matmuls per routed expert.  M covers a
-65-token call (16 rows per expert: the 64-row tile, most row blocks idle), the 256-sequence decode
-micro-batch (64 rows per expert: the 64-row tile, full) and a 512-token prompt chunk (128 per
-expert: the 128-row tile)."""
+65-token call (16 rows per expert), the 256-sequence decode micro-batch (64 rows per expert) and a
+512-token prompt chunk (128 per expert), with the default 128-row tiles and the opt-in 64-row ones
+(knob GEMM4_MOE64)."""
 import numpy as np
 import pytest
 import torch
@@ -53,8 +53,16 @@ def experts(native):
     return gu, dn, gu_all, dn_all
 
 
+@pytest.fixture(params=[0, 1], ids=["tile128", "tile64"])
+def moe64(request, native):
+    from mipipe import _native as N
+    N.check(N.lib().mp_set_knob(b"GEMM4_MOE64", request.param), "knob")
+    yield request.param
+    N.lib().mp_set_knob(b"GEMM4_MOE64", 0)
+
+
 @pytest.mark.parametrize("M", [65, 256, 512])
-def test_moe_grouped_gemm_mixtral_widths(cuda, experts, M):
+def test_moe_grouped_gemm_mixtral_widths(cuda, experts, moe64, M):
     from mipipe.ops.kernels import moe_route, moe_gemm, EPI_SWIGLU, EPI_ATOMIC
     gu, dn, gu_all, dn_all = experts
     g = torch.Generator().manual_seed(M)
