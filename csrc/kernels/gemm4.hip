@@ -460,8 +460,14 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   nsplit = std::max(1, std::min(nsplit, n_stages));
   const int per = (n_stages + nsplit - 1) / nsplit;
   nsplit = (n_stages + per - 1) / per;
+  // non-temporal weight DMA where one row block reads each weight (GEMM4_WNT 0 = auto, 1 on, 2 off):
+  // 70B gate/up 322 -> 287 us cold, +0.8 % / +1.4 % tok/s on 70B mb256 / Mixtral in the engine; with
+  // two row blocks per column group (8B gate/up at M = 256) the second read needs the L2 copy (86.5
+  // -> 89.7 us): profiles/r8k_wnt_ab.txt
+  const int wk = knob(KNOB_GEMM4_WNT);
+  const bool wnt = wk == 1 || (wk == 0 && (MOE || n_mb == 1));
   hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV>), dim3(n_cg * n_mb, nsplit, E), dim3(64 * NWV), 0, st,
-                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD) | (knob(KNOB_GEMM4_WNT) ? 4 : 0));
+                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0));
 }
 
 // rows per workgroup: 256 unless one 128-row block holds M, or 256-row tiles leave most of the 256
