@@ -310,7 +310,7 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
 __device__ int g_attn_probe_calls = 0;
 #endif
 
-template <int DP, bool F8, bool PF>
+template <int DP, bool F8, bool PF, int NW = 4>
 __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
                                                  f16* xo = nullptr) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
@@ -320,8 +320,8 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   };
   constexpr int KK = DP / 32;
   constexpr int DT = DP / 16;
-  __shared__ float sm_m[4][16], sm_l[4][16];
-  __shared__ float sm_o[4][16][DP];
+  __shared__ float sm_m[NW][16], sm_l[NW][16];
+  __shared__ float sm_o[NW][16][DP];
   __shared__ float sm_mz[16][ATTN_MAX_SPLITS], sm_lz[16][ATTN_MAX_SPLITS];   // split merge
   __shared__ int sm_last;
 
@@ -380,8 +380,8 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // and its second chunk (keys 128-255 of the split): with it loaded only inside the chunk loop,
   // after the q build, wave 0 waited one more dependent round trip at 129-256 keys (the 8B single
   // stream's ~2.8 us chunk phase, r8i attention stamps)
-  const bool pre2 = pre && 32 * (wv + 4) < min(p.split_len, p.max_pages * 64 - start);
-  if (pre2) load(wv + 4, kB, vB);
+  const bool pre2 = pre && 32 * (wv + NW) < min(p.split_len, p.max_pages * 64 - start);
+  if (pre2) load(wv + NW, kB, vB);
 
   const int end = min(start + p.split_len, kvlen);
   // splits past the sequence's length take no part (no partials, no counter): with n_act == 1 the
@@ -545,19 +545,19 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       step_h(ci, kraw, vraw);
     }
   };
-  // waves take chunks wv, wv + 4, ...; the next chunk's loads are issued before this one's math
+  // waves take chunks wv, wv + NW, ...; the next chunk's loads are issued before this one's math
   if constexpr (PF) {
     for (int ci = wv; ci < nch;) {
-      if (ci + 4 < nch && !(pre2 && ci == wv)) load(ci + 4, kB, vB);
+      if (ci + NW < nch && !(pre2 && ci == wv)) load(ci + NW, kB, vB);
       step(ci, kA, vA);
-      ci += 4;
+      ci += NW;
       if (ci >= nch) break;
-      if (ci + 4 < nch) load(ci + 4, kA, vA);
+      if (ci + NW < nch) load(ci + NW, kA, vA);
       step(ci, kB, vB);
-      ci += 4;
+      ci += NW;
     }
   } else {
-    for (int ci = wv; ci < nch; ci += 4) {
+    for (int ci = wv; ci < nch; ci += NW) {
       load(ci, kA, vA);
       step(ci, kA, vA);
     }
@@ -574,14 +574,14 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
 
   // 3. merge the 4 waves; publish (n_split > 1) or write the output
   const size_t stride = (size_t)p.M * p.Hq;
-  for (int e = threadIdx.x; e < G * DP; e += 256) {
+  for (int e = threadIdx.x; e < G * DP; e += NW * 64) {
     const int r = e / DP, d = e % DP;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w][r]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sm_m[w][r]);
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       if (sm_m[w][r] == -INFINITY) continue;
       const float f = __expf(sm_m[w][r] - M);
       L += sm_l[w][r] * f;
@@ -635,14 +635,14 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // head's max, weights and sum are formed there by one wave; then every output element sums its
   // n_act partials with independent loads.  (Reading the pairs per element in a serial loop made
   // the merge the long-context bottleneck: 8B single stream at 32K context spent ~60 us/layer.)
-  for (int i = threadIdx.x; i < G * n_act; i += 256) {
+  for (int i = threadIdx.x; i < G * n_act; i += NW * 64) {
     const int r = i / n_act, zz = i - r * n_act;
     const size_t rid = (size_t)t * p.Hq + kvh * G + r;
     sm_mz[r][zz] = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
     sm_lz[r][zz] = ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1);
   }
   __syncthreads();
-  for (int r = wave; r < G; r += 4) {
+  for (int r = wave; r < G; r += NW) {
     float M = -INFINITY;
     for (int zz = lane; zz < n_act; zz += 64) M = fmaxf(M, sm_mz[r][zz]);
 #pragma unroll
@@ -658,7 +658,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
     if (lane == 0) sm_m[0][r] = L;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < G * DP; e += 256) {
+  for (int e = threadIdx.x; e < G * DP; e += NW * 64) {
     const int r = e / DP, d = e % DP;
     const int hh = kvh * G + r;
     const size_t rid = (size_t)t * p.Hq + hh;
@@ -675,6 +675,13 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
 template <int DP, bool F8>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
   attn_decode_body<DP, F8, true>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+// single stream / tiny micro-batches (few (token, kv head) workgroups, short contexts): 8 waves, so
+// every 32-key chunk of a context up to 256 keys has its own wave (with 4, wave 0 computed chunks 0
+// and 4 one after the other: the ~2.8 us chunk phase of profiles/r8j_attn_stamps.txt)
+template <int DP, bool F8>
+__global__ __launch_bounds__(512) void attn_decode_kernel8(const DecodeAttnParams p) {
+  attn_decode_body<DP, F8, true, 8>(p, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 // many-split long contexts: 3 workgroups per CU (occupancy, not per-wave latency, is what they need)
 template <int DP, bool F8>
@@ -693,7 +700,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 // here every wave has 32 KB of K / V in flight from its first chunk on.
 // Splits (few pairs, long contexts): partials + the last-arriving wave of the (token, kv head)
 // merges, with the same sc1 publish / counter / sc1 load hand-off as attn_decode_body.
-template <int DP, bool F8>
+template <int DP, bool F8, bool FL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_wave_kernel(const DecodeAttnParams p) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;
   constexpr int KK = DP / 32, DT = DP / 16, EB = F8 ? 1 : 2;
@@ -727,11 +734,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     const int in_page = P0 & 63;
     const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
     const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
+    if constexpr (FL) {
+      // whole-line K loads (f16 pages): instruction (c, h, I|J) reads 8 keys x the 128-B line of dims
+      // 64h .. 64h+63; lanes m < 8 / m >= 8 carry fragments kk = 2h / 2h+1 of different keys, sorted
+      // into the MFMA fragments at use (fl_fix).  The fragment-shaped form reads 16 keys x 64 B per
+      // instruction (half lines, the other half by the next instruction)
+      const int m = col;
+      const int rI = m < 8 ? m : m - 8, rJ = m < 8 ? 8 + m : m;
+      const int kI = m < 8 ? 0 : 1, kJ = 1 - kI;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int keyI = in_page + 8 * (rI >> 2) + (rI & 3) + 4 * c, keyJ = in_page + 8 * (rJ >> 2) + (rJ & 3) + 4 * c;
+#pragma unroll
+        for (int hh = 0; hh < KK / 2; ++hh) {
+          kf[c][2 * hh] = *reinterpret_cast<const KR*>(kbase + ((size_t)keyI * DP + 32 * (2 * hh + kI) + 8 * q4) * EB);
+          kf[c][2 * hh + 1] = *reinterpret_cast<const KR*>(kbase + ((size_t)keyJ * DP + 32 * (2 * hh + kJ) + 8 * q4) * EB);
+        }
+      }
+    } else {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
         kf[c][kk] = *reinterpret_cast<const KR*>(kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
+    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
       vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
@@ -883,8 +909,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
   };
+  // whole-line K loads: register pair (I, J) of (c, h) -> fragments kk = 2h (lanes m < 8 from I,
+  // m >= 8 from J) and 2h + 1 (the other register, rows rotated by 8 within each 16-lane row: DPP)
+  auto fl_fix = [&](KR (&kf)[2][KK]) {
+    if constexpr (FL && !F8) {
+      const bool lo = col < 8;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int hh = 0; hh < KK / 2; ++hh) {
+          const u32x4 I = __builtin_bit_cast(u32x4, kf[c][2 * hh]), J = __builtin_bit_cast(u32x4, kf[c][2 * hh + 1]);
+          u32x4 f0, f1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f0[e] = lo ? I[e] : J[e];
+            const uint32_t t = lo ? J[e] : I[e];
+            f1[e] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);   // row_ror:8
+          }
+          kf[c][2 * hh] = __builtin_bit_cast(KR, f0);
+          kf[c][2 * hh + 1] = __builtin_bit_cast(KR, f1);
+        }
+    }
+  };
   // f16 pages: the loaded registers are used (and patched) in place; e4m3: converted at use
   auto step = [&](int ci, KR (&kraw)[2][KK], KR (&vraw)[DT]) {
+    fl_fix(kraw);
     if constexpr (F8) {
       half8_t kf[2][KK], vf[DT];
 #pragma unroll
@@ -1127,6 +1176,7 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
     const dim3 grid((items + 3) / 4);
     if (p.Dp == 128) {
       if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
+      else if (knob(KNOB_ATTN_KFL)) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, true>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
     } else {
       if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, true>), grid, dim3(256), 0, st, p);
@@ -1139,6 +1189,17 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
   // MIPIPE_ATTN_PF_MAXWG) need occupancy more than per-wave latency: the 3-per-CU variant
   const int pf_max = knob(KNOB_ATTN_PF_MAXWG);
   const bool pf = p.n_split == 1 && p.M * p.Hkv <= pf_max;
+  if (pf && p.M * p.Hkv <= knob(KNOB_ATTN_NW8_MAXWG)) {
+    const dim3 grid(p.M, p.Hkv, 1);
+    if (p.Dp == 128) {
+      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_kernel8<128, true>), grid, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((mpk::attn_decode_kernel8<128, false>), grid, dim3(512), 0, st, p);
+    } else {
+      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_kernel8<64, true>), grid, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((mpk::attn_decode_kernel8<64, false>), grid, dim3(512), 0, st, p);
+    }
+    return;
+  }
   if (p.kv_fp8) pf ? attn_decode_go<true, true>(p, st) : attn_decode_go<true, false>(p, st);
   else pf ? attn_decode_go<false, true>(p, st) : attn_decode_go<false, false>(p, st);
 }
