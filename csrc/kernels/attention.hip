@@ -218,12 +218,68 @@ constexpr int ATTN_MAX_SPLITS = 128;   // host clamps n_split (hip_stage.cpp)
 // q fragments of the G query heads of kv head kvh for token t with RoPE applied in registers:
 // lane (q4, col) holds q[h = kvh G + col][d = 32kk + 8q4 + j] (zero for col >= G).  Used by the
 // fused decode attention bodies (workgroup- and wave-level).
+// A block-table entry through the scalar cache: the table is read-only for the whole launch, but
+// with K / V stores in the same kernel the compiler cannot prove that and loads it with a VECTOR
+// load -- whose use then waits vmcnt(0), draining every K / V chunk still in flight (in the wave
+// kernel that serialised the two-chunks-in-flight loop to one chunk; r8o ISA).  The constant
+// address space lets it use s_load (lgkm counter only).
+__device__ __forceinline__ int ld_bt(const int32_t* p) {
+  typedef const __attribute__((address_space(4))) int32_t cint;
+  return *(cint*)(uintptr_t)p;
+}
+
+// One 32-key chunk's online softmax for the decode attention, in the exp2 domain (the q fragments
+// carry log2(e) in their scale, decode_q_frags) with a lazy rescale: the running reference m_run
+// moves only when some lane's chunk maximum exceeds it by more than 8 (p = 2^(s - m_run) <= 256,
+// exact enough in f16 for the PV MFMA; l and O stay relative to the same reference), so most
+// chunks skip the exp of alpha and the 4 DT multiplies of O * alpha; the key mask only in the
+// chunk that crosses the context end.  (Per 32-key chunk the old form spent ~240 VALU; the decode
+// attention is bound by this per-chunk work, not by its loads: profiles/r8n_attn_variants.txt.)
+template <int DT>
+__device__ __forceinline__ half8_t softmax_chunk(f32x4 (&sc)[2], bool mask, int P0, int q4, int end, float& m_run,
+                                                 float& l_run, f32x4 (&o)[DT]) {
+  if (mask) {   // wave-uniform
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (P0 + 8 * q4 + 4 * c + i >= end) sc[c][i] = -INFINITY;
+  }
+  float mx = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                   fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+  mx = fmaxf(mx, __shfl_xor(mx, 16));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f) != 0) {   // wave-uniform rescale
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    l_run *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    m_run = m_new;
+  }
+  const float mr = m_run == -INFINITY ? 0.f : m_run;   // (a lane with no finite score yet: p = 0)
+  float pv[2][4];
+  float psum = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = __builtin_amdgcn_exp2f(sc[c][i] - mr);
+      pv[c][i] = e;
+      psum += e;
+    }
+  l_run += psum;
+  return half8_t{(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
+                 (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
+}
+
 template <int KK>
 __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const float* row, const float2* cs, float nrs,
                                                int kvh, int G, int q4, int col, half8_t (&qf)[KK]) {
   const int g = col;
   const bool rvalid = col < G;
   const int h = kvh * G + g;
+  const float qsc = p.q_scale * 1.4426950408889634f;   // exp2-domain scores (softmax_chunk)
   auto qkv_at = [&](int i) { return p.bias ? fmaf(nrs, row[i], p.bias[i]) : nrs * row[i]; };
   // q fragments with RoPE applied in registers: lane holds q[h][d = 32kk + 8q4 + j].  Built
   // before the append so its loads overlap the append's, and (head_dim % 8 == 0) from
@@ -273,8 +329,8 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
         half8_t v = {};
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-          v[j] = ok ? (f16)((x[j] * c[j] - x[j + 1] * c[j + 1]) * p.q_scale) : (f16)0.f;
-          v[j + 1] = ok ? (f16)((x[j] * c[j + 1] + x[j + 1] * c[j]) * p.q_scale) : (f16)0.f;
+          v[j] = ok ? (f16)((x[j] * c[j] - x[j + 1] * c[j + 1]) * qsc) : (f16)0.f;
+          v[j + 1] = ok ? (f16)((x[j] * c[j + 1] + x[j + 1] * c[j]) * qsc) : (f16)0.f;
         }
         qf[kk] = v;
       }
@@ -295,8 +351,8 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
           if (d < p.hd) {
             const float x0 = qkv_at(qr + d), x1 = qkv_at(qr + d + 1);
             const float2 c = cs[d >> 1];
-            v[j] = (f16)((x0 * c.x - x1 * c.y) * p.q_scale);
-            v[j + 1] = (f16)((x0 * c.y + x1 * c.x) * p.q_scale);
+            v[j] = (f16)((x0 * c.x - x1 * c.y) * qsc);
+            v[j + 1] = (f16)((x0 * c.y + x1 * c.x) * qsc);
           }
         }
       }
@@ -343,7 +399,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   const int pos = p.pos[t];
   const int kvlen = pos + 1;
   // decode rows map to slots slot0 + t (HipStage::slot_of): no dependent load before the block table
-  const int slot = p.slot0 >= 0 ? p.slot0 + t : p.slot[t];
+  const int slot = __builtin_amdgcn_readfirstlane(p.slot0 >= 0 ? p.slot0 + t : p.slot[t]);
   const int h = kvh * G + g;
   const int hd2 = p.hd / 2;
   const float* row = p.qkv + (size_t)t * p.ldqkv;
@@ -358,7 +414,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   constexpr int EB = F8 ? 1 : 2;   // bytes per cached element
   auto load = [&](int ci, KR (&kf)[2][KK], KR (&vf)[DT]) {
     const int P0 = start + ci * 32;
-    const int page = bt[P0 >> 6];
+    const int page = ld_bt(bt + (P0 >> 6));
     const int in_page = P0 & 63;
     const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
     const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
@@ -500,36 +556,9 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
       for (int kk = 0; kk < KK; ++kk) a = mfma16x16x32(kf[c][kk], qf[kk], a);
       sc[c] = a;
     }
-    float mx = -INFINITY;
+    const half8_t pf = softmax_chunk<DT>(sc, P0 + 32 > end, P0, q4, end, m_run, l_run, o);
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int kpos = P0 + 8 * q4 + 4 * c + i;
-        const float v = kpos < end ? sc[c][i] : -INFINITY;
-        sc[c][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
-    float pv[2][4];
-    float psum = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = (m_new == -INFINITY) ? 0.f : __expf(sc[c][i] - m_new);
-        pv[c][i] = e;
-        psum += e;
-      }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-    half8_t pf = {(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
-                  (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt]);
   };
   auto step = [&](int ci, KR (&kraw)[2][KK], KR (&vraw)[DT]) {
     if constexpr (F8) {   // convert the raw e4m3 fragments at use (the prefetch holds raw bytes)
@@ -583,7 +612,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       if (sm_m[w][r] == -INFINITY) continue;
-      const float f = __expf(sm_m[w][r] - M);
+      const float f = __builtin_amdgcn_exp2f(sm_m[w][r] - M);
       L += sm_l[w][r] * f;
       O += sm_o[w][r][d] * f;
     }
@@ -650,7 +679,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
     float L = 0.f;
     for (int zz = lane; zz < n_act; zz += 64) {
       const float mz = sm_mz[r][zz];
-      const float f = mz == -INFINITY ? 0.f : __expf(mz - M);
+      const float f = mz == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mz - M);
       sm_mz[r][zz] = f;   // becomes the split's weight
       L += sm_lz[r][zz] * f;
     }
@@ -700,7 +729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 // here every wave has 32 KB of K / V in flight from its first chunk on.
 // Splits (few pairs, long contexts): partials + the last-arriving wave of the (token, kv head)
 // merges, with the same sc1 publish / counter / sc1 load hand-off as attn_decode_body.
-template <int DP, bool F8, bool FL = false>
+template <int DP, bool F8, bool FL = false, bool AL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_wave_kernel(const DecodeAttnParams p) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;
   constexpr int KK = DP / 32, DT = DP / 16, EB = F8 ? 1 : 2;
@@ -723,14 +752,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int hd2 = p.hd / 2;
   const float* row = p.qkv + (size_t)t * p.ldqkv;
   const float2* cs = p.rope_cs + (size_t)pos * hd2;
-  const int32_t* bt = p.block_table + (size_t)(p.slot0 >= 0 ? p.slot0 + t : p.slot[t]) * p.max_pages;
+  const int32_t* bt = p.block_table + (size_t)__builtin_amdgcn_readfirstlane(p.slot0 >= 0 ? p.slot0 + t : p.slot[t]) * p.max_pages;
   const float nrs = p.ssq ? rsqrtf(p.ssq[t] / (float)p.d_model + p.eps) : 1.f;
   const int nch = (end - start + 31) / 32;
   const int krow0 = 8 * (col >> 2) + (col & 3);
 
+  // AL: the chunk loads as inline asm with this kernel's own counted vmcnt waits.  Left to the
+  // compiler, the two register sets' loads were scheduled so that each chunk's last PV MFMA waited
+  // for vmcnt(0): about one chunk in flight per wave instead of two (the loop was memory-latency
+  // bound: ~6.7 us per 32-key chunk at 2K contexts, r8o)
+  auto gload = [&](KR& dst, const uint8_t* a) {
+    if constexpr (AL) {
+      if constexpr (F8) asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(a) : "memory");
+      else asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(a) : "memory");
+    } else {
+      dst = *reinterpret_cast<const KR*>(a);
+    }
+  };
   auto load = [&](int ci, KR (&kf)[2][KK], KR (&vf)[DT]) {
     const int P0 = start + ci * 32;
-    const int page = bt[P0 >> 6];
+    const int page = ld_bt(bt + (P0 >> 6));
     const int in_page = P0 & 63;
     const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
     const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
@@ -747,8 +788,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         const int keyI = in_page + 8 * (rI >> 2) + (rI & 3) + 4 * c, keyJ = in_page + 8 * (rJ >> 2) + (rJ & 3) + 4 * c;
 #pragma unroll
         for (int hh = 0; hh < KK / 2; ++hh) {
-          kf[c][2 * hh] = *reinterpret_cast<const KR*>(kbase + ((size_t)keyI * DP + 32 * (2 * hh + kI) + 8 * q4) * EB);
-          kf[c][2 * hh + 1] = *reinterpret_cast<const KR*>(kbase + ((size_t)keyJ * DP + 32 * (2 * hh + kJ) + 8 * q4) * EB);
+          gload(kf[c][2 * hh], kbase + ((size_t)keyI * DP + 32 * (2 * hh + kI) + 8 * q4) * EB);
+          gload(kf[c][2 * hh + 1], kbase + ((size_t)keyJ * DP + 32 * (2 * hh + kJ) + 8 * q4) * EB);
         }
       }
     } else {
@@ -756,11 +797,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
-        kf[c][kk] = *reinterpret_cast<const KR*>(kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
+        gload(kf[c][kk], kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
-      vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
+      gload(vf[dt], vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
   };
   KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
   load(0, kA, vA);   // in flight during the q build and the append
@@ -878,36 +919,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       for (int kk = 0; kk < KK; ++kk) a = mfma16x16x32(kf[c][kk], qf[kk], a);
       sc[c] = a;
     }
-    float mx = -INFINITY;
+    const half8_t pf = softmax_chunk<DT>(sc, P0 + 32 > end, P0, q4, end, m_run, l_run, o);
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int kpos = P0 + 8 * q4 + 4 * c + i;
-        const float v = kpos < end ? sc[c][i] : -INFINITY;
-        sc[c][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = (m_new == -INFINITY) ? 1.f : __expf(m_run - m_new);
-    float pv[2][4];
-    float psum = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = (m_new == -INFINITY) ? 0.f : __expf(sc[c][i] - m_new);
-        pv[c][i] = e;
-        psum += e;
-      }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-    half8_t pf = {(f16)pv[0][0], (f16)pv[0][1], (f16)pv[0][2], (f16)pv[0][3],
-                  (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt] * alpha);
+    for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt]);
   };
   // whole-line K loads: register pair (I, J) of (c, h) -> fragments kk = 2h (lanes m < 8 from I,
   // m >= 8 from J) and 2h + 1 (the other register, rows rotated by 8 within each 16-lane row: DPP)
@@ -947,11 +961,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       step_h(ci, kraw, vraw);
     }
   };
-  // two chunks in flight: chunk ci + 2 is loaded into the registers chunk ci frees
+  // two chunks in flight: chunk ci + 2 is loaded into the registers chunk ci frees.  AL: before a
+  // chunk's math, wait until only the other set's loads (issued after this chunk's) are in flight
+  constexpr int NL = 2 * KK + DT;   // load instructions per chunk
+  auto vm_wait = [&](int ci) {
+    if constexpr (AL) {
+      if (ci + 1 < nch) __builtin_amdgcn_s_waitcnt((NL & 15) | ((NL >> 4) << 14) | (7 << 4) | (15 << 8));
+      else __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   for (int ci = 0; ci < nch;) {
+    vm_wait(ci);
     step(ci, kA, vA);
     if (ci + 2 < nch) load(ci + 2, kA, vA);
     if (++ci >= nch) break;
+    vm_wait(ci);
     step(ci, kB, vB);
     if (ci + 2 < nch) load(ci + 2, kB, vB);
     ++ci;
@@ -1004,7 +1029,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int zz = 0; zz < n_act; ++zz) {
       const float mz = ld_sc1(p.ml_part + (zz * stride + rid) * 2);
-      const float f = mz == -INFINITY ? 0.f : __expf(mz - M);
+      const float f = mz == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mz - M);
       L += ld_sc1(p.ml_part + (zz * stride + rid) * 2 + 1) * f;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
@@ -1175,9 +1200,17 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
     const int items = p.M * p.Hkv * p.n_split;
     const dim3 grid((items + 3) / 4);
     if (p.Dp == 128) {
-      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
-      else if (knob(KNOB_ATTN_KFL)) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, true>), grid, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
+      const bool al = knob(KNOB_ATTN_ASMLD) != 0;
+      if (p.kv_fp8) {
+        if (al) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true, false, true>), grid, dim3(256), 0, st, p);
+        else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
+      } else if (knob(KNOB_ATTN_KFL)) {
+        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, true>), grid, dim3(256), 0, st, p);
+      } else if (al) {
+        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, false, true>), grid, dim3(256), 0, st, p);
+      } else {
+        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
+      }
     } else {
       if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, true>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, false>), grid, dim3(256), 0, st, p);

@@ -13,6 +13,7 @@ enum Knob : int {
   KNOB_ATTN_WG_TARGET,      // decode attention: workgroup target of the automatic KV split
   KNOB_ATTN_NW8_MAXWG,      // decode attention: 8-wave workgroups while M * Hkv <= this (one split; 0 off)
   KNOB_ATTN_KFL,            // wave decode attention: whole-line K loads + register sort (0 / 1; f16 pages, head_dim 128)
+  KNOB_ATTN_ASMLD,          // wave decode attention: chunk loads as inline asm with counted vmcnt waits (0 / 1; head_dim 128)
   KNOB_GEMM2_SPLIT_WG,      // gemm2: workgroup target of its split-K
   KNOB_GEMM2_TW1_BELOW,     // gemm2: one tile per wave below this many two-tile workgroups
   KNOB_GEMVS_NS,            // gemvs: weight super-blocks in flight per wave (2, 3 or 4)

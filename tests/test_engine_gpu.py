@@ -222,19 +222,32 @@ def test_microbatch_invariance(cuda, native, model_dir):
 @pytest.mark.parametrize("mb_size", [24, 40, 64, 96, 200])
 def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
     """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment;
-    above 64 rows the decode projections and the LM head run on the prompt GEMM (gemm2).  Rows on
-    both sides of every 64-row boundary and the last row are compared: a single-block 64-thread
-    position advance once froze rows >= 64 at their prompt position (found by the 70B-width test)."""
+    above 64 rows the decode projections and the LM head run on the GEMMs (gemm2 / gemm4).  Rows on
+    both sides of every 64-row boundary and the last row are checked against the fp32 oracle: a
+    single-block 64-thread position advance once froze rows >= 64 at their prompt position (found by
+    the 70B-width test)."""
     from mipipe.engine import Engine
+    from mipipe.models.reference import RefLlama
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
     rng = np.random.default_rng(mb_size)
     prompts = [[int(t) for t in rng.integers(3, cfg.vocab, size=int(rng.integers(1, 9)))] for _ in range(mb_size)]
     rows = sorted({0, 1, 2, mb_size - 1} | {r for b in range(64, mb_size, 64) for r in (b - 1, b)})
-    with Engine(gguf=path, max_ctx=128) as eng:
-        singles = [eng.generate([prompts[r]], 6)[0][0] for r in rows]
     with Engine(gguf=path, max_ctx=128, n_mb=1, mb_size=mb_size) as eng:
         o, _ = eng.generate(prompts, 6)
-    assert [o[r] for r in rows] == singles
+    # every generated token is the fp32 oracle's argmax at its position, teacher-forced on the row's own
+    # tokens, up to near-ties (a random tiny model has top-2 logits within 1e-3 of each other: exact
+    # token equality with the single-stream GEMV path flipped on such ties when only a summation
+    # order changed)
+    ref = RefLlama.from_gguf(path)
+    for r in rows:
+        seq = prompts[r] + o[r]
+        ref.reset()
+        lg = ref.forward(seq[:-1], 0).numpy()
+        for i, tok in enumerate(o[r]):
+            lo = lg[len(prompts[r]) - 1 + i]
+            # within 5 % of the logit range of the oracle's max (f16 activations / KV move logits by
+            # ~1 % of it; a token decoded from a wrong context lands near the mean, ~40 % below)
+            assert lo[tok] >= lo.max() - 0.05 * (lo.max() - lo.min()), (r, i, float(lo.max() - lo[tok]))
 
 
 def test_wide_microbatches_pipelined_match_single(cuda, native, model_dir):
