@@ -729,8 +729,10 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // v2 5402 tok/s, v3 for gate/up only 5204-5217, v3 everywhere 4867 (r6j)
   // auto for quantized weights, per epilogue (r8a, profiles/r8a_gemm_microbench.txt, 70B at M = 256):
   // the whole-K SwiGLU / store GEMMs (gate/up, LM head) take v4 (gate/up 297 vs 316 us, Q6_K head
-  // 724 vs 820), the split-K accumulating ones (qkv, o, down) keep v2 (68.6 / 58.0 / 152.8 against
-  // v4's 75.5 / 65.9 / 150.5)
+  // 724 vs 820), the split-K accumulating ones (qkv, o, down) keep v2.  (v4 there too,
+  // prefill_gemm_v=4, ran 70B mb256 at 5953-5970 vs 5764 tok/s but 8B mb256 at 27.3k vs 29.4k, prompt
+  // processing 2-5 % slower, and missed the 70B-width oracle at row 128 after two decode rounds
+  // (NMSE 1.1e-3): profiles/r8s_v4_everywhere.txt -- not the default)
   const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v
                  : is16(m.ptype)         ? 3
                  : epi == EPI_ATOMIC     ? 2
