@@ -62,12 +62,14 @@ MODELS = {
 # (label, model, ftype, mb_size, extra engine options, prompt length or None for --prompt-len): the
 # other named BASELINE configs at one GPU (8B Q4_K_M single stream; Mixtral 8x7B on the grouped MoE
 # GEMM; 8B bf16), the round-1 like-for-like point (70B, 64 sequences) and the headline shape at the
-# reference CLI's 2K context (-c 2048, main.rs:45-46): 256 sequences decoding at positions ~2000
+# reference CLI's 2K context (-c 2048, main.rs:45-46): 256 sequences decoding at positions ~2000,
+# with the f16 KV cache (its attention is HBM-bound: 2.15 GB per layer) and the fp8 one
 SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1, {}, None),
              ("llama3-70b Q4_K pp1 mb64", "llama3-70b", "Q4_K", 64, {}, None),
              ("mixtral-8x7b Q4_K_M pp1 mb256", "mixtral-8x7b", "Q4_K_M", 256, {}, None),
              ("llama3-8b BF16 pp1 mb64", "llama3-8b", "BF16", 64, {}, None),
-             ("llama3-70b Q4_K pp1 mb256 ctx2048", "llama3-70b", "Q4_K", 256, {}, 1984)]
+             ("llama3-70b Q4_K pp1 mb256 ctx2048", "llama3-70b", "Q4_K", 256, {}, 1984),
+             ("llama3-70b Q4_K pp1 mb256 ctx2048 kv-fp8", "llama3-70b", "Q4_K", 256, {"kv_dtype": "fp8"}, 1984)]
 
 
 def parse_set(items):

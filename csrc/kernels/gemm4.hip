@@ -220,9 +220,13 @@ struct G4Geom {
   static constexpr int A_INSTR = (NP + NWV - 1) / NWV;        // per wave (uniform: vmcnt accounting)
 };
 
-template <int PT, int EPI, int BM, bool MOE, int NWV = 8>
+// FL (compile-time flags): bits 0-1 LDS-DMA spread mode, bit 2 non-temporal weights.  Compile-time
+// because every weight DMA of a stage branched on them at run time: the 2-stage loop body of the MoE
+// gate/up kernel carried 485 scalar instructions (36 of them 64-bit compares, 44 s_nop) against 32
+// MFMAs.
+template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
-                                                    const int n_stages, const G4Moe mo, const int spread) {
+                                                    const int n_stages, const G4Moe mo) {
   constexpr int TW = 2;
   using Q3 = W3<PT>;
   using Q = W4<PT>;
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 
   W3Src src;
   src.W = Wbase; src.t0 = cg * (BN / 16) + wave * TW; src.ntiles = p.ntiles; src.nsb = p.nsb;
-  src.nt = (spread & 4) != 0;   // flags: bits 0-1 DMA spread mode, bit 2 non-temporal weights
+  src.nt = (FL & 4) != 0;
   auto stage_a = [&](int b) { return smem + b * G::STAGE; };
   auto stage_r = [&](int b) { return smem + b * G::STAGE + G::A_BYTES + wave * G::R_WAVE; };
   // A piece pc = 8 rows; lane -> row 8 pc + (l >> 3), chunk l & 7 (swizzled on the source side):
@@ -291,7 +295,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   // LDS-DMA issue schedule after the stage barrier: burst (spread == 0: every piece at the barrier,
   // so the two waves of a SIMD both stop issuing MFMAs for the whole burst), or one piece per MFMA
   // step (1), with waves 4-7 (the second wave of each SIMD) two steps later (2)
-  const int dma_shift = (spread & 3) == 2 && wave >= 4 ? 2 : 0;
+  const int dma_shift = (FL & 3) == 2 && wave >= 4 ? 2 : 0;
   auto issue_b = [&](int s, int b) {
     src.sb = s / 4; src.q = s % 4;
     Q3::template issue<TW>(stage_r(b), src, lane);
@@ -361,14 +365,14 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
         wait_vmcnt<NIB + (NB - 3) * (G::A_INSTR + NIB)>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (!(spread & 3)) {
+        if constexpr (!(FL & 3)) {
           issue_a(min(s + NB - 1, s_end - 1), b2);
           issue_b(min(s + NB, s_end - 1), b);
         }
         Q::load(stage_r(b1), lane, raw_n);
       }
       if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
-        if (spread & 3) {
+        if constexpr ((FL & 3) != 0) {
           const int slot = j - JB - dma_shift;
           if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + NB - 1, s_end - 1), b2);
           if (slot == G::A_INSTR) issue_b(min(s + NB, s_end - 1), b);
@@ -466,8 +470,22 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   // -> 89.7 us): profiles/r8k_wnt_ab.txt
   const int wk = knob(KNOB_GEMM4_WNT);
   const bool wnt = wk == 1 || (wk == 0 && (MOE || n_mb == 1));
-  hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV>), dim3(n_cg * n_mb, nsplit, E), dim3(64 * NWV), 0, st,
-                     p, n_mb, per, n_stages, mo, knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0));
+  const dim3 grid(n_cg * n_mb, nsplit, E), block(64 * NWV);
+#define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
+#ifdef MIPIPE_TIMING_PROBES
+  // the LDS-DMA spread schedules (knob GEMM4_SPREAD, measured no faster: PERFORMANCE.md) exist in
+  // the probe build only
+  switch (knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0)) {
+    case 1: G4_LAUNCH(1); return;
+    case 2: G4_LAUNCH(2); return;
+    case 5: G4_LAUNCH(5); return;
+    case 6: G4_LAUNCH(6); return;
+    default: break;
+  }
+#endif
+  if (wnt) G4_LAUNCH(4);
+  else G4_LAUNCH(0);
+#undef G4_LAUNCH
 }
 
 // rows per workgroup: 256 unless one 128-row block holds M, or 256-row tiles leave most of the 256
