@@ -23,10 +23,16 @@ __device__ __forceinline__ int g3_off(int row, int c) { return row * 128 + ((c ^
 // first ds_read after it (it cannot tell which LDS bytes a DMA writes), which drains the whole
 // prefetch pipeline every stage.  These loads are invisible to the compiler's waitcnt pass: every
 // wait on them is the kernel's own counted s_waitcnt vmcnt (wait_vmcnt) before a barrier.
+// LDS byte address of a generic pointer into a __shared__ array: its low 32 bits (a generic LDS
+// address is the shared aperture in the high half and the LDS offset in the low half).  Not an
+// address-space cast: that one null-checks the 64-bit pointer (s_cmp_lg_u64 + s_cselect per DMA /
+// read address, 14 scalar instructions of gemm4's 2-stage loop)
+__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
+
 template <int SZ>
 __device__ __forceinline__ void glds(const void* g, char* lds) {
   static_assert(SZ == 16 || SZ == 4, "glds: 16 or 4 bytes per lane");
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_t*)lds);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds));
   if constexpr (SZ == 16)
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
   else
@@ -37,7 +43,7 @@ __device__ __forceinline__ void glds(const void* g, char* lds) {
 template <int SZ>
 __device__ __forceinline__ void glds(bool nt, const void* g, char* lds) {
   if (!nt) return glds<SZ>(g, lds);
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_t*)lds);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds));
   if constexpr (SZ == 16)
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
   else
@@ -101,7 +107,7 @@ template <int PT> struct W3;
 // LDS reads issued as inline asm (the kernel counts lgkmcnt itself, so A fragments can be kept
 // in flight AD deep: left to the compiler, each ds_read was followed by lgkmcnt(0) before its two
 // MFMAs -- one LDS round trip per 32 MFMA cycles)
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const lds_t*)p; }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return lds_off(p); }
 __device__ __forceinline__ void ds_b32(uint32_t& v, const void* p) {
   asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
 }
