@@ -249,12 +249,14 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   const int s_end = min(s_begin + st_per_split, n_stages);
   if (s_begin >= s_end) return;   // uniform over the workgroup
   int M = p.M;
+  int fr_live = FR;   // 32-row fragments holding rows < M (MoE: uniform per expert tile)
   const int32_t* list = nullptr;
   const uint8_t* Wbase = p.W;
   if constexpr (MOE) {
     const int e = blockIdx.z;
     M = mo.counts[e];
     if (m0 >= M) return;   // uniform: this expert has fewer routed rows
+    fr_live = min(FR, (M - m0 + 31) >> 5);
     list = mo.lists + (size_t)e * mo.list_cap;
     Wbase += (size_t)e * mo.estride;
   }
@@ -354,7 +356,9 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       constexpr int t = j / FR, i = j % FR;
       constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (j > JB ? NR + (j - JB - 1) : 0);
       wait_lgkm<(later < 15 ? later : 15)>();
-      acc[i] = mma32<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[t], acc[i]);
+      // MoE: no MFMAs on 32-row fragments past the expert's rows (their A reads stay: the counted
+      // lgkmcnt waits assume every read issued)
+      if (i == 0 || !MOE || i < fr_live) acc[i] = mma32<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[t], acc[i]);
       if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], b);
       // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
       // stage's value was FR steps ago)
