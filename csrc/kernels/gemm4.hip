@@ -620,7 +620,9 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 64, true>(p, ns, st, mo, q.E);
   } else if (avg <= 128) {
-    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
+    // the down projection unsplit: Mixtral at 256 tokens 10225-10246 vs 10091-10093 tok/s with the
+    // 2 K splits that fill the 256 CUs (half the float atomics into the residual; r9i)
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot && knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
   } else {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 255) / 256), q.nsb * 4) : 1;
