@@ -605,7 +605,7 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   mo.counts = q.counts; mo.lists = q.lists; mo.list_cap = q.list_cap; mo.estride = q.estride; mo.k = q.k;
   mo.x_per_slot = q.x_per_slot; mo.weights = q.weights; mo.Yslot = q.Yslot;
   // row tile from the mean rows per expert (M k / E): 128 up to 128, else 256; split-K (down, atomics
-  // only) for the grid the ACTIVE row blocks form.  A 64-row tile (knob GEMM4_MOE64) drops the
+  // only) for the grid the ACTIVE row blocks form, except at 128-row tiles (unsplit, below).  A 64-row tile (knob GEMM4_MOE64) drops the
   // padding rows of Mixtral's 64 rows per expert at 256 tokens but halves the MFMAs per stage for
   // the same per-stage overhead: gate/up 499 vs 454 us, 8036 vs 8920 tok/s (profiles/r8ij_engine_ab.txt)
   const int avg = std::max(1, q.M * q.k / std::max(1, q.E));
