@@ -27,6 +27,8 @@ n_mb * mb_size sequences.  The timed region is exactly K decode rounds (every se
 token per round), bracketed by barrier + torch.cuda.synchronize() on both sides; the MAX over
 ranks is reported.
 
+At N > 1 (no replicas) it also measures BASELINE configs 3 and 5 on the same N-stage pipeline:
+Llama-3-8B bf16 (64 sequences per micro-batch) and Mixtral 8x7B Q4_K_M (256), N + 1 micro-batches.
 At N = 1 the same run also measures, with the same bracket, the other named BASELINE configs at
 one GPU (Llama-3-8B Q4_K_M single stream, Mixtral 8x7B Q4_K_M at 256 sequences on the grouped MoE
 GEMM, Llama-3-8B bf16 at 64 sequences), the round-1 like-for-like point (70B, 64 sequences) and the
@@ -70,6 +72,11 @@ SECONDARY = [("llama3-8b Q4_K_M pp1 mb1", "llama3-8b", "Q4_K_M", 1, {}, None),
              ("llama3-8b BF16 pp1 mb64", "llama3-8b", "BF16", 64, {}, None),
              ("llama3-70b Q4_K pp1 mb256 ctx2048", "llama3-70b", "Q4_K", 256, {}, 1984),
              ("llama3-70b Q4_K pp1 mb256 ctx2048 kv-fp8", "llama3-70b", "Q4_K", 256, {"kv_dtype": "fp8"}, 1984)]
+
+# N > 1: BASELINE configs 3 (Llama-3-8B bf16, PP=4) and 5 (Mixtral 8x7B, PP=4) on the same pipeline
+# as the headline (PP = N, N + 1 micro-batches): measured by the driver's multi-GPU runs too
+SECONDARY_PP = [("llama3-8b BF16 pp{N} mb64", "llama3-8b", "BF16", 64),
+                ("mixtral-8x7b Q4_K_M pp{N} mb256", "mixtral-8x7b", "Q4_K_M", 256)]
 
 
 def parse_set(items):
@@ -205,6 +212,16 @@ def main():
                                args.steps, args.warmup, world, pg_cpu)
             secondary[label] = dict(tok_s=round(args.steps * mb / (sms / 1e3), 2), ms_per_round=round(sms / args.steps, 4),
                                     p50_token_ms=round(sp50, 4))
+
+    elif n_gpus > 1 and replicas == 1 and not args.no_secondary:
+        for label, model, ftype, mb in SECONDARY_PP:
+            if model == args.model and ftype == args.ftype:
+                continue
+            sms, sp50, _ = run(factory(model, ftype, mb, n_mb), MODELS[model]["vocab"], n_mb * mb, args.prompt_len,
+                               args.steps, args.warmup, world, pg_cpu, sorted(set(devices)))
+            secondary[label.format(N=pp)] = dict(tok_s=round(args.steps * n_mb * mb / (sms / 1e3), 2),
+                                                 ms_per_round=round(sms / args.steps, 4), p50_token_ms=round(sp50, 4),
+                                                 micro_batches=n_mb, mb_size=mb)
 
     link_info = None
     if n_gpus > 1:

@@ -1054,7 +1054,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+  // m0 bound as an input operand (a clobbered m0 is a reserved register: -Winline-asm, gemm_lds.h glds)
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
 
 // Fused single-stream decode attention + output projection (one launch instead of two: the o GEMV

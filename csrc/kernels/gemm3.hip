@@ -160,8 +160,12 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   // end of the stage: a v_mov would read them early)
   using RawT = typename Q::template Raw<TW>;
   using PrepT = typename Q::Prep;
-  auto stage = [&](const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n,
+  // LAST (the split's final stage, compile-time) issues nothing for a next stage: no LDS-DMA, no
+  // barrier, no raw_n / af_n reads -- no LDS read is ever left unconsumed (a dead read's VGPRs are
+  // recycled by the compiler while its data is in flight: tools/isa_lint.py "clobber")
+  auto stage = [&](auto lastc, const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n,
                    PrepT (&pr)[TW], PrepT (&pr_n)[TW]) {
+    constexpr bool LAST = decltype(lastc)::value;
     const int b1 = b == 2 ? 0 : b + 1, b2 = b1 == 2 ? 0 : b1 + 1;   // buffers of stages s+1, s+2 (= s-1)
     const uint32_t a0 = abase(b, 0), a1 = abase(b, 1);
     const uint32_t n0 = abase(b1, 0);
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
       // reads issued after fragment j: the rest of this stage's look-ahead, plus (from step JB on)
       // the next stage's raw bytes and its first fragments (exact issue counts: completion is in
       // order, so lgkmcnt(n) retires everything but the n youngest); capped at the counter's 15
-      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (j > JB ? NR + (j - JB - 1) : 0);
+      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (!LAST && j > JB ? NR + (j - JB - 1) : 0);
       wait_lgkm<(later < 15 ? later : 15)>();
       if constexpr (PROBE & 1) {
         asm volatile("" ::"v"(af[j]));
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
           else bf[1][u] = Q::template frag<TW>(raw, pr[u], u, 1, lane, kc);
         }
       }
-      if constexpr (j == JB) {
+      if constexpr (!LAST && j == JB) {
         wait_vmcnt<NIB>();   // x(s+1) and w(s+1) in: only w(s+2) (issued after x(s+1)) may be in flight
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -200,10 +204,10 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
         issue_b(min(s + 3, s_end - 1), b);
         Q::template load<TW>(stage_r(b1), lane, raw_n);
       }
-      if constexpr (j > JB) {   // stage s+1's fragment j - JB - 1 (all k-half 0: AD <= FM)
+      if constexpr (!LAST && j > JB) {   // stage s+1's fragment j - JB - 1 (all k-half 0: AD <= FM)
         read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], n0);
       }
-      if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
+      if constexpr (!LAST && j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
         wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
         dequant0(raw_n, pr_n, (s + 1) & 3);   // (bf[0] of stage s is consumed: last use at j = FM - 1)
       }
@@ -215,17 +219,22 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
         for (int u = 0; u < TW; ++u) asm volatile("" ::"v"(bf[kk][u]));
     }
   };
+  using F_ = std::false_type;
+  using T_ = std::true_type;
   u32x4 afB[NA];
   RawT rawB;
   PrepT prB[TW];
   int s = s_begin, b = 0;
+  // pairs of stages, then an odd last stage as LAST (its next-stage reads would be dead).  After
+  // an even count the loop's final next-stage reads are dead too, but live up to the loop exit (the
+  // back edge uses them), and the exit goes straight to the lgkmcnt(0) below
   for (; s + 1 < s_end; s += 2) {
-    stage(s, b, af, afB, raw, rawB, pr, prB);
+    stage(F_{}, s, b, af, afB, raw, rawB, pr, prB);
     b = b == 2 ? 0 : b + 1;
-    stage(s + 1, b, afB, af, rawB, raw, prB, pr);
+    stage(F_{}, s + 1, b, afB, af, rawB, raw, prB, pr);
     b = b == 2 ? 0 : b + 1;
   }
-  if (s < s_end) stage(s, b, af, afB, raw, rawB, pr, prB);
+  if (s < s_end) stage(T_{}, s, b, af, afB, raw, rawB, pr, prB);
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
   wait_lgkm<0>();
 

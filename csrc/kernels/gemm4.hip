@@ -347,14 +347,20 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 
   using RawT = typename Q::Raw;
   using PrepT = typename Q::Prep;
-  auto stage = [&](const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n, PrepT& pr,
-                   PrepT& pr_n) {
+  // One stage.  LAST (the split's final stage, compile-time) issues nothing for a next stage: no
+  // LDS-DMA, no barrier, no raw_n / af_n reads -- so no LDS read is ever left unconsumed.  (A read
+  // whose result is dead frees its destination VGPRs to the register allocator at once, while the
+  // data is still in flight; whatever the compiler puts there next is overwritten when it lands:
+  // tools/isa_lint.py "clobber".)  The counted waits count exactly the reads each form issues.
+  auto stage = [&](auto lastc, const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n,
+                   PrepT& pr, PrepT& pr_n) {
+    constexpr bool LAST = decltype(lastc)::value;
     // buffers of stages s+1 and s-1 (= s+NB-1, the next x issue); weights of s+NB go to b itself
     const int b1 = b + 1 == NB ? 0 : b + 1, b2 = b == 0 ? NB - 1 : b - 1;
     static_for<NA>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       constexpr int t = j / FR, i = j % FR;
-      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (j > JB ? NR + (j - JB - 1) : 0);
+      constexpr int later = (NA - 1 - j < AD - 1 ? NA - 1 - j : AD - 1) + (!LAST && j > JB ? NR + (j - JB - 1) : 0);
       wait_lgkm<(later < 15 ? later : 15)>();
       // MoE: no MFMAs on 32-row fragments past the expert's rows (their A reads stay: the counted
       // lgkmcnt waits assume every read issued)
@@ -363,44 +369,51 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
       // stage's value was FR steps ago)
       if constexpr (i == FR / 2 && t < 3) bf[t + 1] = Q::frag(raw, pr, t + 1, h, kc);
-      if constexpr (j == JB) {
-        // x(s+1) and w(s+1) in: w(s+2) (issued with x(s+1)) and the NB - 3 later stages' x and w may
-        // be in flight
-        wait_vmcnt<NIB + (NB - 3) * (G::A_INSTR + NIB)>();
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(FL & 3)) {
-          issue_a(min(s + NB - 1, s_end - 1), b2);
-          issue_b(min(s + NB, s_end - 1), b);
+      if constexpr (!LAST) {
+        if constexpr (j == JB) {
+          // x(s+1) and w(s+1) in: w(s+2) (issued with x(s+1)) and the NB - 3 later stages' x and w may
+          // be in flight
+          wait_vmcnt<NIB + (NB - 3) * (G::A_INSTR + NIB)>();
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!(FL & 3)) {
+            issue_a(min(s + NB - 1, s_end - 1), b2);
+            issue_b(min(s + NB, s_end - 1), b);
+          }
+          Q::load(stage_r(b1), lane, raw_n);
         }
-        Q::load(stage_r(b1), lane, raw_n);
-      }
-      if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
-        if constexpr ((FL & 3) != 0) {
-          const int slot = j - JB - dma_shift;
-          if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + NB - 1, s_end - 1), b2);
-          if (slot == G::A_INSTR) issue_b(min(s + NB, s_end - 1), b);
+        if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
+          if constexpr ((FL & 3) != 0) {
+            const int slot = j - JB - dma_shift;
+            if (slot >= 0 && slot < G::A_INSTR) issue_a1(slot, min(s + NB - 1, s_end - 1), b2);
+            if (slot == G::A_INSTR) issue_b(min(s + NB, s_end - 1), b);
+          }
         }
-      }
-      if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
-      if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
-        wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
-        pr_n = Q::prep(raw_n, (s + 1) & 3);
-        bf[0] = Q::frag(raw_n, pr_n, 0, h, kc);   // (bf[0] of stage s: last use at j = FR - 1)
+        if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
+        if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
+          wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
+          pr_n = Q::prep(raw_n, (s + 1) & 3);
+          bf[0] = Q::frag(raw_n, pr_n, 0, h, kc);   // (bf[0] of stage s: last use at j = FR - 1)
+        }
       }
     });
   };
+  using F_ = std::false_type;
+  using T_ = std::true_type;
   u32x4 afB[NA];
   RawT rawB;
   PrepT prB;
   int s = s_begin, b = 0;
+  // pairs of stages, then an odd last stage as LAST (its next-stage reads would be dead).  After
+  // an even count the loop's final next-stage reads are dead too, but live up to the loop exit (the
+  // back edge uses them), and the exit goes straight to the lgkmcnt(0) below
   for (; s + 1 < s_end; s += 2) {
-    stage(s, b, af, afB, raw, rawB, pr, prB);
+    stage(F_{}, s, b, af, afB, raw, rawB, pr, prB);
     b = b + 1 == NB ? 0 : b + 1;
-    stage(s + 1, b, afB, af, rawB, raw, prB, pr);
+    stage(F_{}, s + 1, b, afB, af, rawB, raw, prB, pr);
     b = b + 1 == NB ? 0 : b + 1;
   }
-  if (s < s_end) stage(s, b, af, afB, raw, rawB, pr, prB);
+  if (s < s_end) stage(T_{}, s, b, af, afB, raw, rawB, pr, prB);
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
   wait_lgkm<0>();
 

@@ -29,14 +29,18 @@ __device__ __forceinline__ int g3_off(int row, int c) { return row * 128 + ((c ^
 // read address, 14 scalar instructions of gemm4's 2-stage loop)
 __device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
 
+// m0 (the DMA's LDS base) is an input operand bound to the register ("{m0}"), not a clobber: the
+// compiler then knows what m0 holds (a clobbered m0 is a reserved register it does not preserve,
+// -Winline-asm).  The s_nop covers the m0 write -> LDS-DMA hazard, which the compiler's hazard
+// recognizer does not see through the asm.
 template <int SZ>
 __device__ __forceinline__ void glds(const void* g, char* lds) {
   static_assert(SZ == 16 || SZ == 4, "glds: 16 or 4 bytes per lane");
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds));
   if constexpr (SZ == 16)
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
   else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
 // the same with the non-temporal policy when nt (wave-uniform): streamed weights that one workgroup
 // reads once, so they do not evict the x rows every column group re-reads from L2
@@ -45,9 +49,9 @@ __device__ __forceinline__ void glds(bool nt, const void* g, char* lds) {
   if (!nt) return glds<SZ>(g, lds);
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds));
   if constexpr (SZ == 16)
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "{m0}"(m0) : "memory");
   else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(g), "{m0}"(m0) : "memory");
 }
 // one LDS-DMA wave instruction whose lanes >= n are masked off (every wave issues it: uniform
 // vmcnt accounting)

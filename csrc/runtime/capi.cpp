@@ -266,10 +266,12 @@ int mp_op_gemm4_splitk(int ptype, const void* W, int ntiles, int nsb, const void
 // GEMM2_SPLIT_WG knob both GEMMs share)
 int mp_set_gemm3_tuning(int bm, int bn, int nsplit, int split_wg) {
   API_TRY
-  set_knob("GEMM3_BM", bm);
-  set_knob("GEMM3_BN", bn);
-  set_knob("GEMM3_SPLIT", nsplit);
-  set_knob("GEMM2_SPLIT_WG", split_wg > 0 ? split_wg : 256);
+  // 0 = back to the process's own value (environment or default), not a hard-coded one
+  auto put = [](const char* k, int v) { v > 0 ? set_knob(k, v) : reset_knob(k); };
+  put("GEMM3_BM", bm);
+  put("GEMM3_BN", bn);
+  put("GEMM3_SPLIT", nsplit);
+  put("GEMM2_SPLIT_WG", split_wg);
   return 0;
   API_CATCH(-1)
 }

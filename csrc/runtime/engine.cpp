@@ -797,11 +797,16 @@ void Engine::run_all(const std::vector<Item>& items) {
       throw;
     }
   } else {
-    std::vector<std::thread> th;
+    // persistent stage workers: one pool thread per owned stage (thread i always runs stage i, the
+    // calling thread runs stage 0), created on the first multi-stage call and reused by every
+    // decode round (the serving loop calls run_all once per round)
+    if (!pool_ || pool_->size() != (int)workers_.size()) pool_.reset(new ThreadPool((int)workers_.size()));
     std::vector<std::exception_ptr> errs(workers_.size());
     std::atomic<int> first_err{-1};   // the root cause; the others are usually "link aborted"
-    for (size_t i = 0; i < workers_.size(); ++i)
-      th.emplace_back([&, i] {
+    int dev0 = 0;
+    if (!cpu_) HIP_OK(hipGetDevice(&dev0));
+    pool_->parallel_for((int64_t)workers_.size(), [&](int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) {
         try {
           run_items(*workers_[i], items);
         } catch (...) {
@@ -810,8 +815,9 @@ void Engine::run_all(const std::vector<Item>& items) {
           first_err.compare_exchange_strong(expect, (int)i);
           for (auto& l : links_) l->abort();
         }
-      });
-    for (auto& t : th) t.join();
+      }
+    });
+    if (!cpu_) (void)hipSetDevice(dev0);   // run_items set the calling thread's device to stage 0's
     if (first_err >= 0) {
       failed_ = true;
       failed_stage_ = workers_[first_err]->stage->spec().stage;

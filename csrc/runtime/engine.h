@@ -27,6 +27,7 @@
 #include "json.h"
 #include "kvpager.h"
 #include "model.h"
+#include "threadpool.h"
 #include "transport.h"
 
 namespace mp {
@@ -199,6 +200,9 @@ class Engine {
   void push_positions(int mb);
   std::vector<Item> prefill_items(const std::vector<size_t>& seqs, bool admission);
   double load_ms_ = 0;
+  // persistent stage-worker threads of run_all (declared last: joined before anything they use
+  // is destroyed)
+  std::unique_ptr<ThreadPool> pool_;
 };
 
 }  // namespace mp

@@ -180,9 +180,13 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
   int reserved = 0;
   std::deque<Pending> waiting;
   std::vector<std::unique_ptr<Live>> live(cap);
-  auto pages_for = [&](long prompt_len, int n_predict) {
+  // pages a request can ever need (its context is capped at max_ctx), and that clamped to the pool
+  auto pages_need = [&](long prompt_len, int n_predict) {
     const long want = prompt_len + std::max(0, n_predict) + 1;
-    return (int)std::min<long>({(want + 63) / 64, (long)max_ctx / 64, (long)pool});
+    return (int)std::min<long>((want + 63) / 64, (long)max_ctx / 64);
+  };
+  auto pages_for = [&](long prompt_len, int n_predict) {
+    return (int)std::min<long>(pages_need(prompt_len, n_predict), (long)pool);
   };
   auto consume = [&](int slot, int32_t t) -> bool {   // false: the request is finished
     Live& L = *live[slot];
@@ -237,9 +241,30 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
     live.clear();
     live.resize(cap);
     reserved = 0;
-    for (auto& pd : waiting)
+    // the waiting queue under the new engine's limits: a resumed request (prompt + produced tokens)
+    // that no longer fits the context ends with stop "context" (admit would reject it, and that
+    // rejection would read as a pipeline fault); a new one is truncated like a fresh admission
+    for (auto it = waiting.begin(); it != waiting.end();) {
+      Pending& pd = *it;
+      if ((int)pd.prompt.size() + 1 >= max_ctx) {
+        if (pd.resume) {
+          Live& L = *pd.resume;
+          L.res.stop = "context";
+          if (!L.acc.buf.empty()) {
+            L.res.text += L.acc.buf;
+            if (L.s.req.on_piece) L.s.req.on_piece(L.acc.buf);
+          }
+          L.res.decode_ms = now_ms() - L.t1;
+          if (L.s.done) L.s.done(L.res);
+          it = waiting.erase(it);
+          continue;
+        }
+        pd.prompt.erase(pd.prompt.begin(), pd.prompt.end() - (max_ctx / 2));
+      }
       pd.pages = pd.resume ? pages_for((long)pd.resume->prompt.size(), pd.resume->s.req.n_predict)
                            : pages_for((long)pd.prompt.size(), pd.s.req.n_predict);
+      ++it;
+    }
     // re-admit in order while the new engine has a slot, the context and the pages for the
     // request's prompt + produced tokens + what it may still generate.  A request that fits the new
     // engine but not right now (its slots or pages are taken) goes back to the FRONT of the queue,
@@ -252,7 +277,8 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       std::vector<int32_t> pr = m->prompt;
       pr.insert(pr.end(), m->res.tokens.begin(), m->res.tokens.end());
       const int pages = pages_for((long)m->prompt.size(), m->s.req.n_predict);
-      const bool ctx_ok = (int)pr.size() + 1 < max_ctx, pool_ok = pages <= pool;
+      const bool ctx_ok = (int)pr.size() + 1 < max_ctx,
+                 pool_ok = pages_need((long)m->prompt.size(), m->s.req.n_predict) <= pool;
       if ((int)prompts.size() < cap && ctx_ok && reserved + pages <= pool) {
         m->pages = pages;
         reserved += pages;

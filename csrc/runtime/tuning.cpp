@@ -60,19 +60,28 @@ std::once_flag g_once;
 
 bool ok(const KnobDef& d, int v) { return v >= d.lo && v <= d.hi && (!d.valid || d.valid(v)); }
 
-void init() {
-  for (int i = 0; i < KNOB_COUNT; ++i) {
-    const KnobDef& d = kDefs[i];
-    int v = d.dflt;
-    const std::string env = std::string("MIPIPE_") + d.name;
-    if (const char* e = std::getenv(env.c_str())) {
-      char* end = nullptr;
-      const long x = std::strtol(e, &end, 10);
-      if (end != e && *end == 0 && ok(d, (int)x)) v = (int)x;
-      else std::fprintf(stderr, "mipipe: ignoring %s=%s (invalid value; using %d)\n", env.c_str(), e, d.dflt);
-    }
-    g_vals[i].store(v, std::memory_order_relaxed);
+// the knob's start value: its MIPIPE_* environment variable when valid, else the default
+int initial_value(int i) {
+  const KnobDef& d = kDefs[i];
+  int v = d.dflt;
+  const std::string env = std::string("MIPIPE_") + d.name;
+  if (const char* e = std::getenv(env.c_str())) {
+    char* end = nullptr;
+    const long x = std::strtol(e, &end, 10);
+    if (end != e && *end == 0 && ok(d, (int)x)) v = (int)x;
+    else std::fprintf(stderr, "mipipe: ignoring %s=%s (invalid value; using %d)\n", env.c_str(), e, d.dflt);
   }
+  return v;
+}
+
+void init() {
+  for (int i = 0; i < KNOB_COUNT; ++i) g_vals[i].store(initial_value(i), std::memory_order_relaxed);
+}
+
+int find(const char* name) {
+  for (int i = 0; i < KNOB_COUNT; ++i)
+    if (std::strcmp(kDefs[i].name, name) == 0) return i;
+  throw std::invalid_argument(std::string("set_knob: unknown knob ") + name);
 }
 
 }  // namespace
@@ -84,14 +93,15 @@ int knob(Knob k) {
 
 void set_knob(const char* name, int value) {
   std::call_once(g_once, init);
-  for (int i = 0; i < KNOB_COUNT; ++i)
-    if (std::strcmp(kDefs[i].name, name) == 0) {
-      if (!ok(kDefs[i], value))
-        throw std::invalid_argument(std::string("set_knob: value out of range for ") + name);
-      g_vals[i].store(value, std::memory_order_relaxed);
-      return;
-    }
-  throw std::invalid_argument(std::string("set_knob: unknown knob ") + name);
+  const int i = find(name);
+  if (!ok(kDefs[i], value)) throw std::invalid_argument(std::string("set_knob: value out of range for ") + name);
+  g_vals[i].store(value, std::memory_order_relaxed);
+}
+
+void reset_knob(const char* name) {
+  std::call_once(g_once, init);
+  const int i = find(name);
+  g_vals[i].store(initial_value(i), std::memory_order_relaxed);
 }
 
 }  // namespace mp

@@ -47,5 +47,7 @@ int knob(Knob k);
 // name is the knob's environment variable without the MIPIPE_ prefix (e.g. "GEMVS_NS");
 // throws std::invalid_argument for an unknown name or a value outside the knob's range
 void set_knob(const char* name, int value);
+// back to the value the process started with (its environment variable, else the default)
+void reset_knob(const char* name);
 
 }  // namespace mp

@@ -136,13 +136,14 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
     return y
 
 
-def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4) -> int:
+def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4, max_splits: int = 16) -> int:
     """Split-K through per-split partial stores and the fixed-order reduction added into y (the
     engine's wide-decode path for qkv / o / down, gemm_splitk_store); returns the split count (0:
-    the shape did not split, y untouched)."""
+    the shape did not split, y untouched).  The scratch starts as NaN, so a partial element the
+    kernel never writes poisons y instead of reading as a plausible value."""
     assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous() and v == 4
     M = x.shape[0]
-    scratch = torch.empty(16 * M * w.ntiles * 16, dtype=torch.float32, device=x.device)
+    scratch = torch.full((max_splits * M * w.ntiles * 16,), float("nan"), dtype=torch.float32, device=x.device)
     return N.check(N.lib().mp_op_gemm4_splitk(w.ptype, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
                                                y.stride(0), w.n, _ptr(scratch), scratch.numel(), _stream()),
                    "gemm_splitk")
@@ -239,7 +240,8 @@ def gemm_i8(w: I8Weight, x: torch.Tensor | None = None, epi: int = EPI_STORE, y:
 
 def set_gemm3_tuning(bm: int = 0, bn: int = 0, nsplit: int = 0, split_wg: int = 0) -> None:
     """Force the v3 GEMM's tile rows / columns (128 | 256) and ATOMIC split-K factor (0 = auto);
-    split_wg: workgroup target of the automatic split (default 256)."""
+    split_wg: workgroup target of the automatic split.  0 restores a knob to the process's own value
+    (its MIPIPE_* environment variable, else the default)."""
     N.check(N.lib().mp_set_gemm3_tuning(bm, bn, nsplit, split_wg), "set_gemm3_tuning")
 
 

@@ -129,7 +129,7 @@ def test_bench_py_inprocess_pipeline_cpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--same-device", "--model", "tinyllama",
            "--ftype", "Q4_K_M", "--steps", "1", "--warmup", "0", "--mb-size", "1", "--prompt-len", "4",
-           "--set", "backend=cpu", "--set", "threads=4"]
+           "--set", "backend=cpu", "--set", "threads=4", "--no-secondary"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -607,7 +607,7 @@ def test_bench_two_ranks_torchrun(cuda, native):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(repo, "bench.py"),
            "--gpus", "2", "--same-device", "--model", "tinyllama", "--ftype", "Q4_K_M", "--steps", "3",
-           "--warmup", "1", "--mb-size", "4", "--prompt-len", "16", "--set", f"base_port={port + 7}"]
+           "--warmup", "1", "--mb-size", "4", "--prompt-len", "16", "--set", f"base_port={port + 7}", "--no-secondary"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -632,7 +632,7 @@ def test_bench_inprocess_same_device(cuda, native, gpus, link):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(gpus), "--same-device", "--link", link,
            "--model", "tinyllama", "--ftype", "Q4_K_M", "--steps", "3", "--warmup", "1", "--mb-size", "4",
-           "--prompt-len", "16"]
+           "--prompt-len", "16", "--no-secondary"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])

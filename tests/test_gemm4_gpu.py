@@ -171,3 +171,68 @@ def test_gemm4_seven_wave_tiles(cuda, native, qt, nw, M):
         assert nmse(h.float().cpu(), href) < 1e-4
     finally:
         N.lib().mp_set_knob(b"GEMM4_NW", 0)
+
+
+def _ref_gpu(xh, k, deq, qt):
+    """fp32 reference on the GPU (the 70B-width shapes are ~20 GFLOP each)."""
+    xa = xh[:, :k].float()
+    if qt == Q.BF16:
+        xa = xh[:, :k].bfloat16().float()
+    return (xa.cuda() @ deq.cuda().T).cpu()
+
+
+# Per-split stage counts of 1, 2, 3, 4 (= the 3-buffer ring + 1) and 5 at K = 8192 (128 stages):
+# the forced split count and the stage count of its LAST split.  Odd counts run the kernel's odd
+# tail stage (gemm4.hip `if (s < s_end) stage(...)`), whose next-stage LDS reads are never consumed
+# (tools/isa_lint.py: their registers must stay pinned until the final lgkmcnt(0)).
+TAIL_SPLITS = [(128, 1), (64, 2), (43, 2), (32, 4), (26, 3), (3, 42)]
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K])
+@pytest.mark.parametrize("ns_last", TAIL_SPLITS, ids=[f"ns{a}" for a, _ in TAIL_SPLITS])
+@pytest.mark.parametrize("M", [65, 129, 256])
+def test_gemm4_splitk_tail_stage_counts(cuda, tuning, qt, ns_last, M):
+    """Split-K at 70B width K = 8192 with every per-split stage count from 1 to 5 and the odd 43
+    (3 splits): ATOMIC into a residual and the per-split partial stores over a NaN-filled scratch,
+    both finite and at the oracle; partial stores bitwise equal over three runs."""
+    from mipipe.ops.kernels import PackedWeight, gemm, gemm_splitk, EPI_ATOMIC
+    ns, _ = ns_last
+    tuning(0, 0, ns, 0)
+    n, k = 512, 8192
+    raw, deq = _weights(qt, n, k, 900 + qt)
+    w = PackedWeight(raw, qt, n, k)
+    xh = _x(M, k, w.k_pad, 17 + M)
+    ref = _ref_gpu(xh, k, deq, qt)
+    base = torch.randn(M, n)
+    y = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4).cpu()
+    assert torch.isfinite(y).all()
+    assert nmse(y - base, ref) < 1e-5
+    outs = []
+    for _ in range(3):
+        y2 = base.clone().cuda()
+        got = gemm_splitk(w, xh.cuda(), y2, max_splits=ns)
+        assert got == ns
+        outs.append(y2.cpu())
+    assert torch.isfinite(outs[0]).all()
+    assert nmse(outs[0] - base, ref) < 1e-5
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("M", [65, 129, 256])
+def test_gemm4_splitk_qkv_width_three_splits(cuda, tuning, M):
+    """The advisor's probe shape: 70B qkv N = 10240, K = 8192, 3 splits of 43 / 43 / 42 stages (the
+    odd tail in two of them), per-split partial stores over a NaN scratch: finite, every row at the
+    oracle."""
+    from mipipe.ops.kernels import PackedWeight, gemm_splitk
+    tuning(0, 0, 3, 0)
+    n, k = 10240, 8192
+    raw, deq = _weights(Q.Q4_K, n, k, 4242)
+    w = PackedWeight(raw, Q.Q4_K, n, k)
+    xh = _x(M, k, w.k_pad, 5 + M)
+    ref = _ref_gpu(xh, k, deq, Q.Q4_K)
+    y = torch.zeros(M, n).cuda()
+    assert gemm_splitk(w, xh.cuda(), y, max_splits=3) == 3
+    y = y.cpu()
+    assert torch.isfinite(y).all()
+    rows = ((y - ref) ** 2).sum(1) / (ref ** 2).sum(1)
+    assert float(rows.max()) < 1e-5, f"worst row {int(rows.argmax())}: {float(rows.max()):.3e}"
