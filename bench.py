@@ -87,9 +87,10 @@ def parse_set(items):
     return out
 
 
-def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, devices=(0,)):
+def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, devices=(0,), dump_tokens=None):
     """Start n_seq synthetic prompts, warm up, time exactly `steps` decode rounds; returns
-    (ms, p50 ms, engine info) with ms and p50 the MAX over ranks."""
+    (ms, p50 ms, engine info) with ms and p50 the MAX over ranks.  dump_tokens: write the generated
+    tokens (where the last stage lives) to that JSON file, after the timed region."""
     eng = eng_factory()
     try:
         g = torch.Generator().manual_seed(0)
@@ -117,6 +118,9 @@ def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, dev
             dist.all_reduce(vals, op=dist.ReduceOp.MAX)   # p50 only non-zero on the last stage
         from mipipe import _native as N
         info = N.jcall(N.lib().mp_engine_info, eng._h, what="engine info")
+        if dump_tokens:
+            with open(dump_tokens, "w") as f:
+                json.dump(eng.tokens(), f)
         return float(vals[0]), float(vals[1]), info
     finally:
         eng.close()
@@ -147,6 +151,8 @@ def main():
                          "torchrun: a gloo process group and TCP links, RCCL refuses two ranks of a communicator "
                          "on one GPU)")
     ap.add_argument("--no-secondary", action="store_true", help="N = 1: skip the secondary configs")
+    ap.add_argument("--dump-tokens", default=None, metavar="PATH",
+                    help="write the headline run's generated tokens to PATH (JSON; A/B of e.g. the bf16 wire)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra engine option (A/B runs), e.g. --set fused_norm=false")
     args = ap.parse_args()
@@ -198,7 +204,8 @@ def main():
     n_mb = args.n_mb or (pp + 1 if pp > 1 else 1)
     ms, p50, info = run(factory(args.model, args.ftype, args.mb_size, n_mb), MODELS[args.model]["vocab"],
                         n_mb * args.mb_size, args.prompt_len, args.steps, args.warmup, world, pg_cpu,
-                        sorted(set(devices)))
+                        sorted(set(devices)),
+                        dump_tokens=args.dump_tokens if rank == world - 1 else None)   # the last stage's rank
     n_tok = args.steps * n_mb * args.mb_size * replicas
     value = n_tok / (ms / 1e3)
 

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(const GemvParams p, const in
   auto issue_b = [&](int s, int b) {
     if constexpr (PROBE & 4) return;
     src.sb = s / SPB; src.q = s % SPB;
-    Q::template issue<TW>(stage_r(b), src, lane);
+    Q::template issue<TW>(stage_r(b), src, EmitDirect{src.nt, lane});
   };
   constexpr int NIB = (PROBE & 4) ? 0 : Q::NI(TW);
 

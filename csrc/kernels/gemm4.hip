@@ -27,6 +27,7 @@
 #include "../runtime/tuning.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace mpk {
 using namespace mp;
@@ -40,16 +41,18 @@ __device__ __forceinline__ f32x16 mma32(half8_t a, half8_t b, f32x16 c) {
   else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// Per-type reads of one wave's raw stage image (W3<PT>::issue layout, TW = 2) in the 32x32 mapping.
+// Per-type reads of one wave's raw stage image (W3<PT>::issue layout, TW tiles) in the 32x32
+// mapping: column pair `pair` = tiles 2 pair, 2 pair + 1 (32 columns, one MFMA B operand).
 template <int PT> struct W4;
 
 template <> struct W4<P_Q4_K> {
   static constexpr int NR = 3;   // LDS reads per stage per lane
   struct Raw { u32x4 hdr; u32x2 q[2]; };
   struct Prep { half2_t S2, M2; };
-  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
-    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
-    ds_b128(w.hdr, R + 2 * 512 + (u * 16 + r) * 16);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, int pair, Raw& w) {
+    const int c = lane & 31, u = 2 * pair + (c >> 4), r = c & 15, h = lane >> 5;
+    ds_b128(w.hdr, R + TW * 512 + (u * 16 + r) * 16);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
   }
@@ -71,15 +74,16 @@ template <> struct W4<P_Q6_K> {
   static constexpr int NR = 6;
   struct Raw { uint32_t sc, d; u32x2 q[2]; uint32_t qd[2]; };
   struct Prep { uint32_t sc; f16 d; };
-  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
-    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
-    ds_b32(w.sc, R + 2 * 768 + (u * 16 + r) * 4);
-    ds_u16(w.d, R + 2 * 832 + (u * 16 + r) * 2);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, int pair, Raw& w) {
+    const int c = lane & 31, u = 2 * pair + (c >> 4), r = c & 15, h = lane >> 5;
+    ds_b32(w.sc, R + TW * 768 + (u * 16 + r) * 4);
+    ds_u16(w.d, R + TW * 832 + (u * 16 + r) * 2);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
       // high bits of dwords g = 2h, 2h+1: the 16-bit halves 0, 1 of dword (g >> 1) = h
-      ds_b32(w.qd[kk], R + 2 * 512 + ((u * 2 + kk) * 16 + r) * 8 + 4 * h);
+      ds_b32(w.qd[kk], R + TW * 512 + ((u * 2 + kk) * 16 + r) * 8 + 4 * h);
     }
   }
   __device__ static __forceinline__ Prep prep(const Raw& w, int) {
@@ -108,13 +112,14 @@ template <> struct W4<P_Q5_K> {
   static constexpr int NR = 5;
   struct Raw { u32x4 hdr; u32x2 q[2]; uint32_t qh[2]; };
   struct Prep { half2_t S2, M2; };
-  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
-    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
-    ds_b128(w.hdr, R + 2 * 640 + (u * 16 + r) * 16);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, int pair, Raw& w) {
+    const int c = lane & 31, u = 2 * pair + (c >> 4), r = c & 15, h = lane >> 5;
+    ds_b128(w.hdr, R + TW * 640 + (u * 16 + r) * 16);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       ds_b64(w.q[kk], R + ((u * 2 + kk) * 16 + r) * 16 + 8 * h);
-      ds_b32(w.qh[kk], R + 2 * 512 + ((u * 2 + kk) * 16 + r) * 4);
+      ds_b32(w.qh[kk], R + TW * 512 + ((u * 2 + kk) * 16 + r) * 4);
     }
   }
   __device__ static __forceinline__ Prep prep(const Raw& w, int q) {
@@ -143,9 +148,10 @@ template <> struct W4<P_Q8_0> {
   static constexpr int NR = 3;
   struct Raw { uint32_t dd; u32x4 v[2]; };
   struct Prep { uint32_t dd; };
-  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
-    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
-    ds_b32(w.dd, R + 2 * 1024 + (u * 16 + r) * 4);
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, int pair, Raw& w) {
+    const int c = lane & 31, u = 2 * pair + (c >> 4), r = c & 15, h = lane >> 5;
+    ds_b32(w.dd, R + TW * 1024 + (u * 16 + r) * 4);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) ds_b128(w.v[kk], R + ((u * 2 + kk) * 16 + r) * 32 + 16 * h);
   }
@@ -169,8 +175,9 @@ template <int PT> struct W4_16 {
   static constexpr int NR = 4;
   struct Raw { u32x4 v[4]; };
   struct Prep {};
-  __device__ static __forceinline__ void load(const char* R, int lane, Raw& w) {
-    const int c = lane & 31, u = c >> 4, r = c & 15, h = lane >> 5;
+  template <int TW>
+  __device__ static __forceinline__ void load(const char* R, int lane, int pair, Raw& w) {
+    const int c = lane & 31, u = 2 * pair + (c >> 4), r = c & 15, h = lane >> 5;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int kk = t >> 1, g = 2 * h + (t & 1);
@@ -207,10 +214,10 @@ struct G4Moe {
 
 // NWV compute waves (8, or 7: BN = 224 columns, so a 57344-column gate/up gives 256 workgroups
 // for the 256 CUs instead of 224); the x rows are staged round-robin by all of them
-template <int PT, int BM, int NWV>
+template <int PT, int BM, int NWV, int TW = 2>
 struct G4Geom {
   static constexpr int A_BYTES = BM * 128;                    // x rows of one 64-k stage
-  static constexpr int R_WAVE = W3<PT>::RAW(2);              // one wave's raw bytes of one stage
+  static constexpr int R_WAVE = W3<PT>::RAW(TW);             // one wave's raw bytes of one stage
   static constexpr int STAGE = A_BYTES + NWV * R_WAVE;
   // stage buffers (x issued NB - 1 stages ahead, weights NB; the kernel handles 3-5)
   // (4-5 buffers for the 128-row tiles measured slower: MoE gate/up 454 -> 454 us at 128 rows, 499
@@ -224,14 +231,18 @@ struct G4Geom {
 // because every weight DMA of a stage branched on them at run time: the 2-stage loop body of the MoE
 // gate/up kernel carried 485 scalar instructions (36 of them 64-bit compares, 44 s_nop) against 32
 // MFMAs.
-template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0>
+// TW (tiles per wave): 2 (32 columns, one MFMA column block) or 4 (64 columns: two column pairs
+// share every A fragment; the 64-row MoE tile, where 32-column waves left half the MFMAs of a
+// 128-row tile on padding rows)
+template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0, int TW = 2>
 __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages, const G4Moe mo) {
-  constexpr int TW = 2;
+  static_assert(TW == 2 || TW == 4, "gemm4: 2 or 4 tiles per wave");
+  constexpr int NPR = TW / 2;   // 32-column pairs per wave
   using Q3 = W3<PT>;
   using Q = W4<PT>;
-  using G = G4Geom<PT, BM, NWV>;
-  constexpr int NB = G::NB, FR = BM / 32, BN = 32 * NWV;
+  using G = G4Geom<PT, BM, NWV, TW>;
+  constexpr int NB = G::NB, FR = BM / 32, BN = 16 * TW * NWV;
   constexpr bool BF = PT == P_BF16;
   static_assert(NB >= 3 && NB <= 5, "gemm4: 3-5 stage buffers");
   __shared__ __attribute__((aligned(16))) char smem[NB * G::STAGE];
@@ -270,8 +281,10 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   // each lane's source row pointers are fixed for the whole K loop (MoE: the gathered rows).
   // Pieces go round-robin over the NWV waves; a wave whose last slot is past the NP pieces re-loads
   // another wave's piece into that piece's place (identical bytes), so every wave issues A_INSTR.
+  // All DMA addresses in the saddr form (glds_s): a wave-uniform base per stage plus a per-lane
+  // 32-bit offset fixed for the whole K loop (x rows: the host checks they stay under 4 GiB)
   int apc[G::A_INSTR];
-  const char* xsrc[G::A_INSTR];
+  uint32_t xoff[G::A_INSTR];
 #pragma unroll
   for (int i = 0; i < G::A_INSTR; ++i) {
     const int pc0 = wave + NWV * i;
@@ -283,32 +296,45 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       const int slot = list[gr];
       gr = mo.x_per_slot ? slot : slot / mo.k;
     }
-    xsrc[i] = reinterpret_cast<const char*>(p.X) + (size_t)gr * p.ldx * 2 + 16 * ch;
+    xoff[i] = (uint32_t)gr * (uint32_t)p.ldx * 2u + 16u * ch;
   }
+  const uint8_t* const xbase = reinterpret_cast<const uint8_t*>(p.X);
   auto issue_a = [&](int s, int b) {
+    const uint8_t* sb = uniform_ptr(xbase + (size_t)s * 128);
 #pragma unroll
-    for (int i = 0; i < G::A_INSTR; ++i) glds<16>(xsrc[i] + s * 128, stage_a(b) + apc[i] * 1024);
+    for (int i = 0; i < G::A_INSTR; ++i) glds_s<16>(false, sb, xoff[i], stage_a(b) + apc[i] * 1024);
   };
   auto issue_a1 = [&](int i, int s, int b) {
+    const uint8_t* sb = uniform_ptr(xbase + (size_t)s * 128);
 #pragma unroll
     for (int ii = 0; ii < G::A_INSTR; ++ii)
-      if (ii == i) glds<16>(xsrc[ii] + s * 128, stage_a(b) + apc[ii] * 1024);
+      if (ii == i) glds_s<16>(false, sb, xoff[ii], stage_a(b) + apc[ii] * 1024);
   };
   // LDS-DMA issue schedule after the stage barrier: burst (spread == 0: every piece at the barrier,
   // so the two waves of a SIMD both stop issuing MFMAs for the whole burst), or one piece per MFMA
   // step (1), with waves 4-7 (the second wave of each SIMD) two steps later (2)
   const int dma_shift = (FL & 3) == 2 && wave >= 4 ? 2 : 0;
+  // weight DMA: per-lane offsets from Wbase recorded once at (sb, q) = (0, 0) (EmitRecord), each
+  // stage's scalar base from lane 0's address (EmitSaddr); the host checks the matrix < 4 GiB
+  constexpr int NIB = Q3::NI(TW);
+  uint32_t boff[NIB], boff0[NIB];
+  {
+    W3Src c0 = src;
+    c0.sb = 0; c0.q = 0;
+    Q3::template issue<TW>(smem, c0, EmitRecord<NIB>{Wbase, lane, boff, boff0});
+  }
   auto issue_b = [&](int s, int b) {
     src.sb = s / 4; src.q = s % 4;
-    Q3::template issue<TW>(stage_r(b), src, lane);
+    Q3::template issue<TW>(stage_r(b), src, EmitSaddr<NIB>{src.nt, lane, boff, boff0});
   };
-  constexpr int NIB = Q3::NI(TW);
 
-  f32x16 acc[FR];
+  f32x16 acc[FR][NPR];
 #pragma unroll
   for (int i = 0; i < FR; ++i)
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+    for (int pp = 0; pp < NPR; ++pp)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][pp][v] = 0.f;
   const Consts kc = make_consts();
   const int h = lane >> 5, cl = lane & 31;
   // per-lane byte offset of A fragment (t, row cl) inside a stage image; row 32 i + cl adds 4096 i
@@ -317,12 +343,16 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   for (int t = 0; t < 4; ++t) aoff[t] = (uint32_t)g3_off(cl, 4 * (t >> 1) + 2 * h + (t & 1));
 
   // A fragments read AD steps ahead (8; half the stage's NA fragments for the 64-row MoE tile)
-  constexpr int NA = 4 * FR, AD = NA >= 16 ? 8 : NA / 2, NR = Q::NR, JB = NA - AD - 1;
+  constexpr int NA = 4 * FR, AD = NA >= 16 ? 8 : NA / 2, NR = Q::NR * NPR, JB = NA - AD - 1;
+  // B fragment t + 1 is dequantized at step i = IB of fragment t (behind the first MFMAs of t)
+  constexpr int IB = FR >= 4 ? FR / 2 : 0;
   static_assert(JB > FR / 2 && NA - AD > JB, "gemm4: barrier step");
   static_assert(JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
-  typename Q::Raw raw;
-  typename Q::Prep pr;
-  half8_t bf[4];
+  using RawT = typename Q::Raw;
+  using PrepT = typename Q::Prep;
+  RawT raw[NPR];
+  PrepT pr[NPR];
+  half8_t bf[NPR][4];
   u32x4 af[NA];
   auto read_a = [&](auto jc, u32x4& dst, int b) {
     constexpr int j = decltype(jc)::value;
@@ -339,21 +369,23 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   issue_b(min(s_begin + NB - 1, s_end - 1), NB - 1);
   wait_vmcnt<(NB - 2) * (G::A_INSTR + NIB) + NIB>();
   __builtin_amdgcn_s_barrier();
-  Q::load(stage_r(0), lane, raw);
+#pragma unroll
+  for (int pp = 0; pp < NPR; ++pp) Q::template load<TW>(stage_r(0), lane, pp, raw[pp]);
   static_for<AD>([&](auto jc) { read_a(jc, af[decltype(jc)::value], 0); });
   wait_lgkm<AD>();   // raw in (the oldest reads)
-  pr = Q::prep(raw, s_begin & 3);
-  bf[0] = Q::frag(raw, pr, 0, h, kc);
+#pragma unroll
+  for (int pp = 0; pp < NPR; ++pp) {
+    pr[pp] = Q::prep(raw[pp], s_begin & 3);
+    bf[pp][0] = Q::frag(raw[pp], pr[pp], 0, h, kc);
+  }
 
-  using RawT = typename Q::Raw;
-  using PrepT = typename Q::Prep;
   // One stage.  LAST (the split's final stage, compile-time) issues nothing for a next stage: no
   // LDS-DMA, no barrier, no raw_n / af_n reads -- so no LDS read is ever left unconsumed.  (A read
   // whose result is dead frees its destination VGPRs to the register allocator at once, while the
   // data is still in flight; whatever the compiler puts there next is overwritten when it lands:
   // tools/isa_lint.py "clobber".)  The counted waits count exactly the reads each form issues.
-  auto stage = [&](auto lastc, const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT& raw, RawT& raw_n,
-                   PrepT& pr, PrepT& pr_n) {
+  auto stage = [&](auto lastc, const int s, const int b, u32x4 (&af)[NA], u32x4 (&af_n)[NA], RawT (&raw)[NPR],
+                   RawT (&raw_n)[NPR], PrepT (&pr)[NPR], PrepT (&pr_n)[NPR]) {
     constexpr bool LAST = decltype(lastc)::value;
     // buffers of stages s+1 and s-1 (= s+NB-1, the next x issue); weights of s+NB go to b itself
     const int b1 = b + 1 == NB ? 0 : b + 1, b2 = b == 0 ? NB - 1 : b - 1;
@@ -364,11 +396,18 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       wait_lgkm<(later < 15 ? later : 15)>();
       // MoE: no MFMAs on 32-row fragments past the expert's rows (their A reads stay: the counted
       // lgkmcnt waits assume every read issued)
-      if (i == 0 || !MOE || i < fr_live) acc[i] = mma32<BF>(x_op<BF>(__builtin_bit_cast(half8_t, af[j])), bf[t], acc[i]);
+      if (i == 0 || !MOE || i < fr_live) {
+        const half8_t a = x_op<BF>(__builtin_bit_cast(half8_t, af[j]));
+#pragma unroll
+        for (int pp = 0; pp < NPR; ++pp) acc[i][pp] = mma32<BF>(a, bf[pp][t], acc[i][pp]);
+      }
       if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], b);
       // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
       // stage's value was FR steps ago)
-      if constexpr (i == FR / 2 && t < 3) bf[t + 1] = Q::frag(raw, pr, t + 1, h, kc);
+      if constexpr (i == IB && t < 3) {
+#pragma unroll
+        for (int pp = 0; pp < NPR; ++pp) bf[pp][t + 1] = Q::frag(raw[pp], pr[pp], t + 1, h, kc);
+      }
       if constexpr (!LAST) {
         if constexpr (j == JB) {
           // x(s+1) and w(s+1) in: w(s+2) (issued with x(s+1)) and the NB - 3 later stages' x and w may
@@ -380,7 +419,8 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
             issue_a(min(s + NB - 1, s_end - 1), b2);
             issue_b(min(s + NB, s_end - 1), b);
           }
-          Q::load(stage_r(b1), lane, raw_n);
+#pragma unroll
+          for (int pp = 0; pp < NPR; ++pp) Q::template load<TW>(stage_r(b1), lane, pp, raw_n[pp]);
         }
         if constexpr (j >= JB && j < JB + G::A_INSTR + 3) {   // spread issue (uniform branches)
           if constexpr ((FL & 3) != 0) {
@@ -392,8 +432,11 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
         if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
         if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
           wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
-          pr_n = Q::prep(raw_n, (s + 1) & 3);
-          bf[0] = Q::frag(raw_n, pr_n, 0, h, kc);   // (bf[0] of stage s: last use at j = FR - 1)
+#pragma unroll
+          for (int pp = 0; pp < NPR; ++pp) {   // (bf[.][0] of stage s: last use at j = FR - 1)
+            pr_n[pp] = Q::prep(raw_n[pp], (s + 1) & 3);
+            bf[pp][0] = Q::frag(raw_n[pp], pr_n[pp], 0, h, kc);
+          }
         }
       }
     });
@@ -401,8 +444,8 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   using F_ = std::false_type;
   using T_ = std::true_type;
   u32x4 afB[NA];
-  RawT rawB;
-  PrepT prB;
+  RawT rawB[NPR];
+  PrepT prB[NPR];
   int s = s_begin, b = 0;
   // pairs of stages, then an odd last stage as LAST (its next-stage reads would be dead).  After
   // an even count the loop's final next-stage reads are dead too, but live up to the loop exit (the
@@ -417,20 +460,23 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
   wait_lgkm<0>();
 
-  // epilogue: lane holds C[row 32 i + 8 (v >> 2) + 4 h + (v & 3)][col cl] of the wave's 32 columns
-  const int n = cg * BN + wave * 32 + cl;
+  // epilogue: lane holds C[row 32 i + 8 (v >> 2) + 4 h + (v & 3)][col cl] of each of the wave's
+  // 32-column pairs
   const int rowb = m0 + 4 * h;
+#pragma unroll
+  for (int pp = 0; pp < NPR; ++pp) {
+  const int n = cg * BN + wave * 16 * TW + 32 * pp + cl;
   if constexpr (EPI == EPI_SWIGLU) {
     const int o = (n >> 4) * 8 + (cl & 15);   // tile rows 0-7 gate, 8-15 up of the same 8 outputs
 #pragma unroll
     for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const float other = __shfl_xor(acc[i][v], 8);
+        const float other = __shfl_xor(acc[i][pp][v], 8);
         const int m = rowb + 32 * i + 8 * (v >> 2) + (v & 3);
         if ((cl & 8) == 0 && m < M && o < p.n_valid) {
           const int hr = MOE ? list[m] : m;   // MoE: the slot's row of H
-          p.H[(size_t)hr * p.ldh + o] = sat_f16(silu(acc[i][v]) * other);
+          p.H[(size_t)hr * p.ldh + o] = sat_f16(silu(acc[i][pp][v]) * other);
         }
       }
   } else {
@@ -445,18 +491,19 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
           if (m < M) {
             if constexpr (MOE) {   // down projection: weighted into the slot's token (or its own row)
               const int slot = list[m];
-              const float wv = mo.weights[slot] * acc[i][v];
+              const float wv = mo.weights[slot] * acc[i][pp][v];
               if (mo.Yslot) mo.Yslot[(size_t)slot * p.ldy + n] = wv;
               else unsafeAtomicAdd(p.Y + (size_t)(slot / mo.k) * p.ldy + n, wv);
             } else if constexpr (EPI == EPI_ATOMIC) {
-              unsafeAtomicAdd(Y + (size_t)m * p.ldy, acc[i][v] + bias);
+              unsafeAtomicAdd(Y + (size_t)m * p.ldy, acc[i][pp][v] + bias);
             } else {
-              Y[(size_t)m * p.ldy] = acc[i][v] + bias;
+              Y[(size_t)m * p.ldy] = acc[i][pp][v] + bias;
             }
           }
         }
     }
   }
+  }   // column pairs
 }
 
 }  // namespace mpk
@@ -473,9 +520,9 @@ static int g4_splits(int wgs, int n_stages) {
   return std::max(1, std::min(target / wgs, n_stages / 16));
 }
 
-template <int PT, int EPI, int BM, bool MOE = false, int NWV = 8>
+template <int PT, int EPI, int BM, bool MOE = false, int NWV = 8, int TW = 2>
 static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe& mo = mpk::G4Moe{}, int E = 1) {
-  const int n_cg = (p.ntiles + 2 * NWV - 1) / (2 * NWV);
+  const int n_cg = (p.ntiles + TW * NWV - 1) / (TW * NWV);
   const int n_mb = (p.M + BM - 1) / BM;   // MoE: p.M = the most rows one expert can get
   const int n_stages = p.nsb * 4;
   nsplit = std::max(1, std::min(nsplit, n_stages));
@@ -485,10 +532,15 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   // 70B gate/up 322 -> 287 us cold, +0.8 % / +1.4 % tok/s on 70B mb256 / Mixtral in the engine; with
   // two row blocks per column group (8B gate/up at M = 256) the second read needs the L2 copy (86.5
   // -> 89.7 us): profiles/r8k_wnt_ab.txt
+  // the kernel's DMA offsets are 32-bit per lane: the weight matrix (one expert's) and the x rows
+  // it addresses must stay under 4 GiB
+  if ((size_t)p.ntiles * p.nsb * mpk::W3<PT>::CB >= (size_t(1) << 32) ||
+      (size_t)std::max(p.M * std::max(1, mo.k), 1) * p.ldx * 2 >= (size_t(1) << 32))
+    throw std::runtime_error("gemm4: operand over 4 GiB (32-bit DMA offsets)");
   const int wk = knob(KNOB_GEMM4_WNT);
   const bool wnt = wk == 1 || (wk == 0 && (MOE || n_mb == 1));
   const dim3 grid(n_cg * n_mb, nsplit, E), block(64 * NWV);
-#define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
+#define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F, TW>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
 #ifdef MIPIPE_TIMING_PROBES
   // the LDS-DMA spread schedules (knob GEMM4_SPREAD, measured no faster: PERFORMANCE.md) exist in
   // the probe build only
@@ -629,7 +681,13 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
-  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64)) {   // opt-in: measured slower (r8i)
+  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64) == 2) {
+    // 64-row tiles with 64 columns per wave (two column pairs share each A fragment): no padding
+    // rows at Mixtral's 64 rows per expert and the same MFMAs per stage as a full 128-row tile
+    const int n_cg4 = (q.ntiles + 31) / 32;
+    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg4 * q.E, q.nsb * 4) : 1;
+    gemm4_go<PT, EPI, 64, true, 8, 4>(p, ns, st, mo, q.E);
+  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64) == 1) {   // opt-in: measured slower (r8i)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 64, true>(p, ns, st, mo, q.E);
   } else if (avg <= 128) {

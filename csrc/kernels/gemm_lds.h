@@ -60,6 +60,74 @@ __device__ __forceinline__ void glds_n(bool nt, char* lds, int n, int lane, F sr
   if (lane < n) glds<SZ>(nt, src(lane), lds);
 }
 
+// The same DMA with the address split into a wave-uniform 64-bit base (SGPRs) and a per-lane
+// 32-bit byte offset (the saddr form): a stage's loads then cost one scalar base per instruction and
+// no per-lane 64-bit address arithmetic (v_mad_u64_u32 / v_lshl_add_u64 on the MFMA waves' VALU)
+template <int SZ>
+__device__ __forceinline__ void glds_s(bool nt, const void* sbase, uint32_t voff, char* lds) {
+  static_assert(SZ == 16 || SZ == 4, "glds_s: 16 or 4 bytes per lane");
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds));
+  if (nt) {
+    if constexpr (SZ == 16)
+      asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 nt" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+    else
+      asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1 nt" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+  } else {
+    if constexpr (SZ == 16)
+      asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+    else
+      asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+  }
+}
+// a wave-uniform pointer in SGPRs
+__device__ __forceinline__ const uint8_t* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const uint8_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+
+// Emitters of the per-type DMA schedules (W3<PT>::issue): instruction i moves SZ bytes for lanes
+// < n from src(lane) to lds + SZ * lane.
+//   EmitDirect: the DMA itself (64-bit per-lane addresses).
+//   EmitRecord: records lane offsets src(lane) - base at (sb, q) = (0, 0) and lane 0's, once per
+//               kernel: the schedule's addresses are (lane-independent stage delta) + (stage-
+//               independent lane offset).
+//   EmitSaddr:  the DMA from scalar base src(0)@(sb, q) - lane0 offset and the recorded lane offset.
+struct EmitDirect {
+  bool nt;
+  int lane;
+  template <int SZ, class F>
+  __device__ __forceinline__ void go(char* lds, int n, F src) { glds_n<SZ>(nt, lds, n, lane, src); }
+};
+template <int NI>
+struct EmitRecord {
+  const uint8_t* base;
+  int lane;
+  uint32_t* off;     // [NI] per-lane
+  uint32_t* off0;    // [NI] lane 0's (uniform)
+  int i = 0;
+  template <int SZ, class F>
+  __device__ __forceinline__ void go(char*, int n, F src) {
+    off[i] = (uint32_t)(reinterpret_cast<const uint8_t*>(src(min(lane, n - 1))) - base);
+    off0[i] = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<const uint8_t*>(src(0)) - base));
+    ++i;
+  }
+};
+template <int NI>
+struct EmitSaddr {
+  bool nt;
+  int lane;
+  const uint32_t* off;
+  const uint32_t* off0;
+  int i = 0;
+  template <int SZ, class F>
+  __device__ __forceinline__ void go(char* lds, int n, F src) {
+    const uint8_t* sb = uniform_ptr(reinterpret_cast<const uint8_t*>(src(0)) - off0[i]);
+    if (lane < n) glds_s<SZ>(nt, sb, off[i], lds);
+    ++i;
+  }
+};
+
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima), gfx9 encoding
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -154,12 +222,12 @@ template <> struct W3<P_Q4_K> {
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2]; };
   struct Prep { half2_t S2, M2; };
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
+    em.template go<16>(R, 32 * TW, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<16>(c.nt, R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16; });
+    em.template go<16>(R + TW * 512, 16 * TW, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -191,16 +259,16 @@ template <> struct W3<P_Q5_K> {
   static constexpr int NR(int TW) { return 5 * TW; }
   template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2], qh[TW][2]; };
   struct Prep { half2_t S2, M2; };
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
+    em.template go<16>(R, 32 * TW, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
     // 16-B entries = 4 rows' high-bit words: entry f -> (u, h, rows 4 (f & 3) ..)
-    glds_n<16>(c.nt, R + TW * 512, 8 * TW, lane, [&](int f) {
+    em.template go<16>(R + TW * 512, 8 * TW, [&](int f) {
       return c.chunk(f >> 3, CB) + 2048 + ((f >> 2) & 1) * 256 + (16 * c.q + 4 * (f & 3)) * 4;
     });
-    glds_n<16>(c.nt, R + TW * 640, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2560 + (e & 15) * 16; });
+    em.template go<16>(R + TW * 640, 16 * TW, [&](int e) { return c.chunk(e >> 4, CB) + 2560 + (e & 15) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -246,16 +314,16 @@ template <> struct W3<P_Q6_K> {
   static constexpr int NR(int TW) { return 6 * TW; }
   template <int TW> struct Raw { uint32_t sc[TW], d[TW], q[TW][2], qd[TW][2]; };
   struct Prep { uint32_t sc; f16 d; };
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
+    em.template go<16>(R, 32 * TW, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<16>(c.nt, R + TW * 512, 16 * TW, lane, [&](int f) {   // (u, h): 16 rows x 8 B contiguous
+    em.template go<16>(R + TW * 512, 16 * TW, [&](int f) {   // (u, h): 16 rows x 8 B contiguous
       return c.chunk(f >> 4, CB) + 2048 + ((f >> 3) & 1) * 512 + 16 * c.q * 8 + (f & 7) * 16;
     });
-    glds_n<4>(c.nt, R + TW * 768, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 3072 + (e & 15) * 16 + 4 * c.q; });
-    glds_n<16>(c.nt, R + TW * 832, 2 * TW, lane, [&](int f) { return c.chunk(f >> 1, CB) + 3328 + (f & 1) * 16; });
+    em.template go<4>(R + TW * 768, 16 * TW, [&](int e) { return c.chunk(e >> 4, CB) + 3072 + (e & 15) * 16 + 4 * c.q; });
+    em.template go<16>(R + TW * 832, 2 * TW, [&](int f) { return c.chunk(f >> 1, CB) + 3328 + (f & 1) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -303,12 +371,12 @@ template <> struct W3<P_Q8_0> {
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { uint32_t dd[TW]; u32x2 v[TW][2]; };
   struct Prep { uint32_t dd; };
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
 #pragma unroll
     for (int u = 0; u < TW; ++u)   // 64 entries of 16 B per tile: (h, r, half)
-      glds<16>(c.nt, c.chunk(u, CB) + (lane >> 5) * 2048 + (16 * c.q + ((lane >> 1) & 15)) * 32 + 16 * (lane & 1), R + u * 1024);
-    glds_n<4>(c.nt, R + TW * 1024, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 4096 + (e & 15) * 16 + 4 * c.q; });
+      em.template go<16>(R + u * 1024, 64, [&](int l) { return c.chunk(u, CB) + (l >> 5) * 2048 + (16 * c.q + ((l >> 1) & 15)) * 32 + 16 * (l & 1); });
+    em.template go<4>(R + TW * 1024, 16 * TW, [&](int e) { return c.chunk(e >> 4, CB) + 4096 + (e & 15) * 16 + 4 * c.q; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -342,12 +410,12 @@ template <> struct W3<P_Q4_0> {
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { uint32_t dd[TW], q[TW][2]; };
   struct Prep { uint32_t dd; };
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
-    glds_n<16>(c.nt, R, 32 * TW, lane, [&](int e) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
+    em.template go<16>(R, 32 * TW, [&](int e) {
       return c.chunk(e >> 5, CB) + ((e >> 4) & 1) * 1024 + (16 * c.q + (e & 15)) * 16;
     });
-    glds_n<4>(c.nt, R + TW * 512, 16 * TW, lane, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16 + 4 * c.q; });
+    em.template go<4>(R + TW * 512, 16 * TW, [&](int e) { return c.chunk(e >> 4, CB) + 2048 + (e & 15) * 16 + 4 * c.q; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -381,11 +449,11 @@ template <int PT> struct W3_16 {
   static constexpr int NR(int TW) { return 2 * TW; }
   template <int TW> struct Raw { u32x4 v[TW][2]; };
   struct Prep {};
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
 #pragma unroll
     for (int f = 0; f < 2 * TW; ++f)
-      glds<16>(c.nt, c.chunk(f >> 1, CB) + (4 * (f & 1) + (lane >> 4)) * 1024 + (16 * c.q + (lane & 15)) * 16, R + f * 1024);
+      em.template go<16>(R + f * 1024, 64, [&](int l) { return c.chunk(f >> 1, CB) + (4 * (f & 1) + (l >> 4)) * 1024 + (16 * c.q + (l & 15)) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {
@@ -416,11 +484,11 @@ template <> struct W3<P_I8> {
   static constexpr int NR(int TW) { return 2 * TW; }
   template <int TW> struct Raw { u32x4 v[TW][2]; };
   struct Prep {};
-  template <int TW>
-  __device__ static __forceinline__ void issue(char* R, const W3Src& c, int lane) {
+  template <int TW, class E>
+  __device__ static __forceinline__ void issue(char* R, const W3Src& c, E&& em) {
 #pragma unroll
     for (int f = 0; f < 2 * TW; ++f)
-      glds<16>(c.nt, c.chunk(f >> 1, CB) + ((2 * c.q + (f & 1)) * 64 + lane) * 16, R + f * 1024);
+      em.template go<16>(R + f * 1024, 64, [&](int l) { return c.chunk(f >> 1, CB) + ((2 * c.q + (f & 1)) * 64 + l) * 16; });
   }
   template <int TW>
   __device__ static __forceinline__ void load(const char* R, int lane, Raw<TW>& w) {

@@ -793,6 +793,69 @@ const char* mp_rccl_selftest(int device, const int64_t* sizes, int n_sizes, int 
   API_CATCH(nullptr)
 }
 
+// RCCL / compute CU-sharing proxy (1 rank): enqueue `iters` grouped self send/recv of `bytes` on a
+// side stream of `device` and return at once; the caller times its GEMMs on its own stream while
+// the RCCL kernels run, then mp_rccl_loop_wait reports the loop's wall time.  A 1-rank stand-in for
+// a pipeline stage whose activation send/recv shares the CUs with the next micro-batch's GEMMs
+// (tools/rccl_overlap_probe.py).
+namespace {
+struct RcclLoop {
+  void* comm = nullptr;
+  RcclLink* link = nullptr;
+  hipStream_t st = nullptr;
+  void *src = nullptr, *dst = nullptr;
+  size_t cap = 0;
+  hipEvent_t a = nullptr, b = nullptr;
+  int device = -1;
+};
+RcclLoop g_loop;
+}  // namespace
+
+int mp_rccl_loop_start(int device, int64_t bytes, int iters) {
+  API_TRY
+  HIP_OK(hipSetDevice(device));
+  if (g_loop.device != device) {
+    std::vector<void*> comms;
+    std::string err;
+    if (!rccl_init_all({device}, &comms, &err)) throw std::runtime_error("RCCL init failed: " + err);
+    g_loop.comm = comms[0];
+    g_loop.link = new RcclLink(g_loop.comm, 0, 0, device);
+    HIP_OK(hipStreamCreateWithFlags(&g_loop.st, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&g_loop.a));
+    HIP_OK(hipEventCreate(&g_loop.b));
+    g_loop.device = device;
+  }
+  if ((size_t)bytes > g_loop.cap) {
+    if (g_loop.src) (void)hipFree(g_loop.src);
+    if (g_loop.dst) (void)hipFree(g_loop.dst);
+    HIP_OK(hipMalloc(&g_loop.src, (size_t)bytes));
+    HIP_OK(hipMalloc(&g_loop.dst, (size_t)bytes));
+    HIP_OK(hipMemset(g_loop.src, 0x3c, (size_t)bytes));
+    g_loop.cap = (size_t)bytes;
+  }
+  HIP_OK(hipEventRecord(g_loop.a, g_loop.st));
+  for (int i = 0; i < iters; ++i) {
+    rccl_group_begin();
+    g_loop.link->send(g_loop.src, (size_t)bytes, g_loop.st);
+    g_loop.link->recv(g_loop.dst, (size_t)bytes, g_loop.st);
+    rccl_group_end();
+  }
+  HIP_OK(hipEventRecord(g_loop.b, g_loop.st));
+  return 0;
+  API_CATCH(-1)
+}
+
+double mp_rccl_loop_wait() {
+  API_TRY
+  if (g_loop.device < 0) throw std::runtime_error("mp_rccl_loop_wait: no loop started");
+  HIP_OK(hipSetDevice(g_loop.device));
+  HIP_OK(hipEventSynchronize(g_loop.b));
+  float ms = 0;
+  HIP_OK(hipEventElapsedTime(&ms, g_loop.a, g_loop.b));
+  return ms;
+  API_CATCH(-1.0)
+}
+
 // can RCCL put `n` ranks of one communicator on these devices (e.g. the same GPU twice)?
 const char* mp_rccl_probe_devices(const int* devices, int n) {
   API_TRY

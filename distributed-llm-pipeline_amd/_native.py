@@ -112,6 +112,8 @@ _SIGS = {
     "mp_engine_logits": ([c_void_p, c_int, c_void_p, c_int], c_int),
     "mp_rccl_unique_id": ([c_void_p], c_int),
     "mp_rccl_selftest": ([c_int, c_void_p, c_int, c_int], c_char_p),
+    "mp_rccl_loop_start": ([c_int, c_int64, c_int], c_int),
+    "mp_rccl_loop_wait": ([], c_double),
     "mp_rccl_probe_devices": ([c_void_p, c_int], c_char_p),
     "mp_set_gemv_tpw": ([c_int], None),
     "mp_init_packed": ([c_void_p, ctypes.c_size_t, c_int, c_float, ctypes.c_uint64, c_void_p], c_int),

@@ -47,6 +47,20 @@ def test_rccl_link_self_loop(cuda, native):
     print("RCCL_SELFTEST " + json.dumps(rep))
 
 
+def test_rccl_side_stream_loop(cuda, native):
+    """The CU-sharing proxy (mp_rccl_loop_start / wait, tools/gemv_bench.py --rccl-bytes): RCCL self
+    send/recv of a 256 x 8192 bf16 activation queued on a side stream runs while the caller's stream
+    computes, and reports its wall time."""
+    import torch
+    assert native.mp_rccl_loop_start(0, 256 * 8192 * 2, 20) == 0, native.mp_last_error()
+    a = torch.randn(4096, 4096, device="cuda")
+    for _ in range(4):
+        a = a @ a.T / 64.0
+    torch.cuda.synchronize()
+    ms = native.mp_rccl_loop_wait()
+    assert ms > 0, native.mp_last_error()
+
+
 def test_torch_nccl_world1_with_native_lib(cuda, native):
     """torch.distributed backend "nccl" (RCCL on ROCm) at world size 1, in the process that has
     libmipipe.so (sharing torch's HIP runtime and librccl): collectives work, then our own RCCL

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--g3", default="0,0,0", help="v3 GEMM tuning BM,BN,nsplit (0 = auto); ';'-separated list sweeps")
     ap.add_argument("--knob", action="append", default=[], metavar="NAME=V[,V..]",
                     help="tuning knob (csrc/runtime/tuning.h) swept per shape, e.g. GEMM3_PROBE=0,1,2")
+    ap.add_argument("--rccl-bytes", type=int, default=0,
+                    help="CU-sharing proxy: run each timed loop twice, the second time with a 1-rank RCCL self "
+                         "send/recv loop of this many bytes on a side stream (mp_rccl_loop_start)")
     a = ap.parse_args()
     L = N.lib()
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -134,17 +137,25 @@ def main():
                         for W in Ws[:2]:
                             run(W)
                         torch.cuda.synchronize()
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record()
-                        for i in range(a.iters):
-                            run(Ws[i % copies])
-                        e1.record()
-                        torch.cuda.synchronize()
-                        us = e0.elapsed_time(e1) * 1e3 / a.iters
-                        print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
-                                              GBps=round(nbytes / us / 1e3, 1),
-                                              TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
-                                              g3=g3 if a.gemm in (3, 4, 8) else None, sk=a.sk or None, knobs=dict(kn) or None)), flush=True)
+                        for with_rccl in ([False, True] if a.rccl_bytes else [False]):
+                            rccl_ms = None
+                            if with_rccl:   # side-stream RCCL kernels sharing the CUs for the whole timed loop
+                                N.check(L.mp_rccl_loop_start(torch.cuda.current_device(), a.rccl_bytes, 400), "rccl loop")
+                            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                            e0.record()
+                            for i in range(a.iters):
+                                run(Ws[i % copies])
+                            e1.record()
+                            torch.cuda.synchronize()
+                            if with_rccl:
+                                rccl_ms = round(L.mp_rccl_loop_wait(), 3)
+                            us = e0.elapsed_time(e1) * 1e3 / a.iters
+                            print(json.dumps(dict(shape=sname, type=tname, M=M, tpw=tpw, nsplit=nsplit, us=round(us, 2),
+                                                  GBps=round(nbytes / us / 1e3, 1),
+                                                  TFLOPs=round(2.0 * M * n * k / us / 1e6, 1), gemm=a.gemm,
+                                                  g3=g3 if a.gemm in (3, 4, 8) else None, sk=a.sk or None, knobs=dict(kn) or None,
+                                                  rccl_bytes=a.rccl_bytes if with_rccl else None,
+                                                  rccl_loop_ms=rccl_ms)), flush=True)
                 if a.gemm == 8:   # the per-row activation quantization the int8 GEMM needs first
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
