@@ -681,13 +681,9 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
-  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64) == 2) {
-    // 64-row tiles with 64 columns per wave (two column pairs share each A fragment): no padding
-    // rows at Mixtral's 64 rows per expert and the same MFMAs per stage as a full 128-row tile
-    const int n_cg4 = (q.ntiles + 31) / 32;
-    const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg4 * q.E, q.nsb * 4) : 1;
-    gemm4_go<PT, EPI, 64, true, 8, 4>(p, ns, st, mo, q.E);
-  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64) == 1) {   // opt-in: measured slower (r8i)
+  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64)) {   // opt-in: measured slower (r8i)
+    // (64-row tiles with 64 columns per wave, TW = 4, measured 33 % slower still: twice the Q4_K
+    // dequant per live MFMA, VALU-bound; profiles/r10c_moe_tile64x64.txt)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 64, true>(p, ns, st, mo, q.E);
   } else if (avg <= 128) {

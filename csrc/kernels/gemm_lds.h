@@ -93,11 +93,17 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const void* p) {
 //               kernel: the schedule's addresses are (lane-independent stage delta) + (stage-
 //               independent lane offset).
 //   EmitSaddr:  the DMA from scalar base src(0)@(sb, q) - lane0 offset and the recorded lane offset.
+// A schedule entry of n > 64 lanes (TW = 4: 128 quant pieces) is ceil(n / 64) wave instructions,
+// entries 64 k .. 64 k + 63 to lds + 64 k SZ (W3<PT>::NI counts them so).
 struct EmitDirect {
   bool nt;
   int lane;
   template <int SZ, class F>
-  __device__ __forceinline__ void go(char* lds, int n, F src) { glds_n<SZ>(nt, lds, n, lane, src); }
+  __device__ __forceinline__ void go(char* lds, int n, F src) {
+#pragma unroll
+    for (int k = 0; 64 * k < n; ++k)
+      glds_n<SZ>(nt, lds + 64 * k * SZ, n - 64 * k, lane, [&](int e) { return src(64 * k + e); });
+  }
 };
 template <int NI>
 struct EmitRecord {
@@ -108,9 +114,13 @@ struct EmitRecord {
   int i = 0;
   template <int SZ, class F>
   __device__ __forceinline__ void go(char*, int n, F src) {
-    off[i] = (uint32_t)(reinterpret_cast<const uint8_t*>(src(min(lane, n - 1))) - base);
-    off0[i] = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<const uint8_t*>(src(0)) - base));
-    ++i;
+#pragma unroll
+    for (int k = 0; 64 * k < n; ++k) {
+      const int nk = min(64, n - 64 * k);
+      off[i] = (uint32_t)(reinterpret_cast<const uint8_t*>(src(64 * k + min(lane, nk - 1))) - base);
+      off0[i] = __builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<const uint8_t*>(src(64 * k)) - base));
+      ++i;
+    }
   }
 };
 template <int NI>
@@ -122,11 +132,16 @@ struct EmitSaddr {
   int i = 0;
   template <int SZ, class F>
   __device__ __forceinline__ void go(char* lds, int n, F src) {
-    const uint8_t* sb = uniform_ptr(reinterpret_cast<const uint8_t*>(src(0)) - off0[i]);
-    if (lane < n) glds_s<SZ>(nt, sb, off[i], lds);
-    ++i;
+#pragma unroll
+    for (int k = 0; 64 * k < n; ++k) {
+      const uint8_t* sb = uniform_ptr(reinterpret_cast<const uint8_t*>(src(64 * k)) - off0[i]);
+      if (lane < n - 64 * k) glds_s<SZ>(nt, sb, off[i], lds + 64 * k * SZ);
+      ++i;
+    }
   }
 };
+// wave instructions of a schedule entry of n lanes
+constexpr int wi(int n) { return (n + 63) / 64; }
 
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima), gfx9 encoding
 template <int N>
@@ -218,7 +233,7 @@ __device__ __forceinline__ void wait_lgkm() {
 template <> struct W3<P_Q4_K> {
   static constexpr int CB = chunk_bytes(P_Q4_K);
   static constexpr int RAW(int TW) { return TW * 768; }
-  static constexpr int NI(int) { return 2; }
+  static constexpr int NI(int TW) { return wi(32 * TW) + wi(16 * TW); }
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2]; };
   struct Prep { half2_t S2, M2; };
@@ -255,7 +270,7 @@ template <> struct W3<P_Q4_K> {
 template <> struct W3<P_Q5_K> {
   static constexpr int CB = chunk_bytes(P_Q5_K);
   static constexpr int RAW(int TW) { return TW * 896; }
-  static constexpr int NI(int) { return 3; }
+  static constexpr int NI(int TW) { return wi(32 * TW) + wi(8 * TW) + wi(16 * TW); }
   static constexpr int NR(int TW) { return 5 * TW; }
   template <int TW> struct Raw { u32x4 hdr[TW]; uint32_t q[TW][2], qh[TW][2]; };
   struct Prep { half2_t S2, M2; };
@@ -310,7 +325,7 @@ template <> struct W3<P_Q5_K> {
 template <> struct W3<P_Q6_K> {
   static constexpr int CB = chunk_bytes(P_Q6_K);
   static constexpr int RAW(int TW) { return TW * 896; }
-  static constexpr int NI(int) { return 4; }
+  static constexpr int NI(int TW) { return wi(32 * TW) + wi(16 * TW) + wi(16 * TW) + wi(2 * TW); }
   static constexpr int NR(int TW) { return 6 * TW; }
   template <int TW> struct Raw { uint32_t sc[TW], d[TW], q[TW][2], qd[TW][2]; };
   struct Prep { uint32_t sc; f16 d; };
@@ -367,7 +382,7 @@ template <> struct W3<P_Q6_K> {
 template <> struct W3<P_Q8_0> {
   static constexpr int CB = chunk_bytes(P_Q8_0);
   static constexpr int RAW(int TW) { return TW * 1088; }
-  static constexpr int NI(int TW) { return TW + 1; }
+  static constexpr int NI(int TW) { return TW + wi(16 * TW); }
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { uint32_t dd[TW]; u32x2 v[TW][2]; };
   struct Prep { uint32_t dd; };
@@ -406,7 +421,7 @@ template <> struct W3<P_Q8_0> {
 template <> struct W3<P_Q4_0> {
   static constexpr int CB = chunk_bytes(P_Q4_0);
   static constexpr int RAW(int TW) { return TW * 576; }
-  static constexpr int NI(int) { return 2; }
+  static constexpr int NI(int TW) { return wi(32 * TW) + wi(16 * TW); }
   static constexpr int NR(int TW) { return 3 * TW; }
   template <int TW> struct Raw { uint32_t dd[TW], q[TW][2]; };
   struct Prep { uint32_t dd; };

@@ -46,7 +46,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM4_NW", 0, 0, 8, nw4_ok},
     {"GEMM4_SPREAD", 0, 0, 2, nullptr},
     {"GEMM4_WNT", 0, 0, 2, nullptr},
-    {"GEMM4_MOE64", 0, 0, 2, nullptr},
+    {"GEMM4_MOE64", 0, 0, 1, nullptr},
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},

@@ -30,7 +30,7 @@ enum Knob : int {
   KNOB_GEMM4_NW,            // gemm4: compute waves per workgroup of unsplit launches (0 auto, 7, 8)
   KNOB_GEMM4_SPREAD,        // gemm4: LDS-DMA issue after the stage barrier (0 burst, 1 spread over MFMA steps, 2 spread + waves 4-7 two steps later)
   KNOB_GEMM4_WNT,           // gemm4: non-temporal LDS-DMA of the weights (0 auto: one row block per column group, 1 on, 2 off)
-  KNOB_GEMM4_MOE64,         // gemm4 MoE mode when the mean rows per expert <= 64: 0 128-row tiles, 1 64-row tiles x 32 columns per wave, 2 64-row tiles x 64 columns per wave
+  KNOB_GEMM4_MOE64,         // gemm4 MoE mode: 64-row tiles when the mean rows per expert <= 64 (0 / 1)
   KNOB_GEMM3_BM,            // gemm3: force rows per workgroup (0 auto, 128, 256); A/B runs only
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)

@@ -53,7 +53,7 @@ def experts(native):
     return gu, dn, gu_all, dn_all
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["tile128", "tile64", "tile64x64"])
+@pytest.fixture(params=[0, 1], ids=["tile128", "tile64"])
 def moe64(request, native):
     from mipipe import _native as N
     N.check(N.lib().mp_set_knob(b"GEMM4_MOE64", request.param), "knob")
