@@ -733,10 +733,10 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // prefill_gemm_v=4, ran 70B mb256 at 5953-5970 vs 5764 tok/s but 8B mb256 at 27.3k vs 29.4k, prompt
   // processing 2-5 % slower, and missed the 70B-width oracle at row 128 after two decode rounds
   // (NMSE 1.1e-3): profiles/r8s_v4_everywhere.txt -- not the default)
-  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v
-                 : is16(m.ptype)         ? 3
-                 : epi == EPI_ATOMIC     ? 2
-                                         : 4;
+  // round 5: with the tail-stage hazard gone (tools/isa_lint.py) and the saddr DMA, gemm4 takes the
+  // split-K shapes too: 70B mb256 a tie (5797 / 5786 vs 5800 / 5776), 8B mb256 30401 vs 29709
+  // (profiles/r10d_splitk_ab_and_prof.txt)
+  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v : is16(m.ptype) ? 3 : 4;
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
   const bool v3 = gv == 3;
   const bool v2 = gv == 2 && !is16(m.ptype);
