@@ -382,6 +382,32 @@ int mp_op_gemvs(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   API_CATCH(-1)
 }
 
+// chained o -> gate/up -> down of one row (launch_gemvs_chain): attn f16 [Ko_pad] -> x f32 [d] += o;
+// h f16 = SwiGLU(gate/up(rmsnorm(x) * gamma)); x += down(h).  cnt: 16 device ints (zeroed once;
+// [8] = the error flag).  Returns the workgroups launched, 0 when the chain does not apply.
+int mp_op_gemvs_chain3(int pt_o, const void* Wo, int nt_o, int nsb_o, const void* attn, int ld_attn, int pt_gu,
+                       const void* Wgu, int nt_gu, int nsb_gu, void* x, int d, const void* gamma, float eps, void* h,
+                       int ldh, int F, int pt_dn, const void* Wdn, int nt_dn, int nsb_dn, void* cnt, void* stream) {
+  API_TRY
+  GemvsChainPhase ph[3];
+  for (auto& q : ph) q.p = GemvParams{};
+  ph[0].ptype = pt_o; ph[0].epi = EPI_ATOMIC;
+  ph[0].p.W = (const uint8_t*)Wo; ph[0].p.ntiles = nt_o; ph[0].p.nsb = nsb_o; ph[0].p.X = (const f16*)attn;
+  ph[0].p.ldx = ld_attn; ph[0].p.M = 1; ph[0].p.Y = (float*)x; ph[0].p.ldy = d; ph[0].p.n_valid = d;
+  ph[1].ptype = pt_gu; ph[1].epi = EPI_SWIGLU;
+  ph[1].p.W = (const uint8_t*)Wgu; ph[1].p.ntiles = nt_gu; ph[1].p.nsb = nsb_gu; ph[1].p.M = 1;
+  ph[1].p.H = (f16*)h; ph[1].p.ldh = ldh; ph[1].p.n_valid = F;
+  ph[1].p.Xf = (const float*)x; ph[1].p.ldxf = d; ph[1].p.gamma = (const float*)gamma; ph[1].p.eps = eps; ph[1].p.d_norm = d;
+  ph[2].ptype = pt_dn; ph[2].epi = EPI_ATOMIC;
+  ph[2].p.W = (const uint8_t*)Wdn; ph[2].p.ntiles = nt_dn; ph[2].p.nsb = nsb_dn; ph[2].p.X = (const f16*)h;
+  ph[2].p.ldx = ldh; ph[2].p.M = 1; ph[2].p.Y = (float*)x; ph[2].p.ldy = d; ph[2].p.n_valid = d;
+  int wgs = 0;
+  if (!launch_gemvs_chain(ph, 3, (int32_t*)cnt, (int32_t*)cnt + 8, (hipStream_t)stream, &wgs)) return 0;
+  HIP_OK(hipGetLastError());
+  return wgs;
+  API_CATCH(-1)
+}
+
 int mp_op_rmsnorm(const void* x, int ldx, const void* w, int d, float eps, void* out, int ldo, int M, void* stream) {
   API_TRY
   launch_rmsnorm((const float*)x, ldx, (const float*)w, d, eps, (f16*)out, ldo, M, nullptr, 0, (hipStream_t)stream);

@@ -498,6 +498,7 @@ void HipStage::alloc_runtime() {
     ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
   }
   attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
+  chain_cnt_ = (int32_t*)zalloc(16 * 4);
   if (opt_.prefill_flash && opt_.max_ctx > 256) {   // prefill KV-split partials (attn_prefill.hip)
     pf_opart_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * Dp_ * 4);
     pf_ml_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * 2 * 4);
@@ -952,6 +953,8 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     }
     if (!(decode && attention_o(li, M, pos, slot, x, st))) {
       attention(li, M, pos, kvlen, slot, decode, st, false);
+      // o -> gate/up -> down as one chained launch (knob GEMVS_CHAIN; falls back when unsupported)
+      if (knob(KNOB_GEMVS_CHAIN) && chain_layer(L, M, x, st)) return;
       gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
     }
     if (L.moe) {
@@ -1145,6 +1148,26 @@ void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen
     }
     }
   }
+}
+
+bool HipStage::chain_layer(const LayerW& L, int M, float* x, hipStream_t st) {
+  if (M != 1 || L.moe || !L.fused_gateup || opt_.deterministic || !chain_cnt_) return false;
+  const int d = cfg_.d_model;
+  GemvsChainPhase ph[3];
+  auto mat = [](GemvParams& p, const PackedMat& m) {
+    p.W = m.d; p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb;
+  };
+  ph[0] = GemvsChainPhase{L.wo.ptype, EPI_ATOMIC, GemvParams{}};
+  mat(ph[0].p, L.wo);
+  ph[0].p.X = attn_; ph[0].p.ldx = Ko_; ph[0].p.M = M; ph[0].p.Y = x; ph[0].p.ldy = d; ph[0].p.n_valid = d;
+  ph[1] = GemvsChainPhase{L.gateup.ptype, EPI_SWIGLU, GemvParams{}};
+  mat(ph[1].p, L.gateup);
+  ph[1].p.M = M; ph[1].p.H = h_; ph[1].p.ldh = Kff_; ph[1].p.n_valid = cfg_.d_ff;
+  ph[1].p.Xf = x; ph[1].p.ldxf = d; ph[1].p.gamma = L.ffn_norm; ph[1].p.eps = cfg_.eps; ph[1].p.d_norm = d;
+  ph[2] = GemvsChainPhase{L.down.ptype, EPI_ATOMIC, GemvParams{}};
+  mat(ph[2].p, L.down);
+  ph[2].p.X = h_; ph[2].p.ldx = Kff_; ph[2].p.M = M; ph[2].p.Y = x; ph[2].p.ldy = d; ph[2].p.n_valid = d;
+  return launch_gemvs_chain(ph, 3, chain_cnt_, chain_cnt_ + 8, st);
 }
 
 void HipStage::gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, const float* Xf, const float* gamma,

@@ -209,6 +209,8 @@ class HipStage : public Stage {
   float* sk_defer_ = nullptr;   // gemv(): ATOMIC GEMMs into this buffer defer their reduction
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
   int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
+  int32_t* chain_cnt_ = nullptr;  // chained o -> gate/up -> down (launch_gemvs_chain): [0..3] counters, [8] error flag
+  bool chain_layer(const LayerW& L, int M, float* x, hipStream_t st);
   // MoE scratch
   float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
   float* moe_w_ = nullptr; f16* moe_h_ = nullptr;

@@ -54,6 +54,22 @@ bool gemvs2_supported(int pt, int pt2);
 void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st);
 void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G = 0,
                   int force_split = 0);
+// Chained single-stream GEMVs (gemvs.hip gemvs_chain_kernel): 2 or 3 consecutive gemvs launches as
+// ONE launch whose phases hand off through sc1 stores + agent counters, each phase's weights in
+// flight before it waits for the previous one.  Supported chain: [EPI_ATOMIC (Q4_K) ->] EPI_SWIGLU
+// (Q4_K, fused RMSNorm) -> EPI_ATOMIC (Q4_K | Q6_K), M == 1 -- the o -> gate/up -> down of a decode
+// layer.  cnt: 4 device ints, zero before the first launch (the kernel re-arms them); err: a device
+// int set to 1 if a poll gave up (bounded spin).  Returns false (nothing launched) when the shape is
+// not supported or the phases cannot all be resident at once.
+struct GemvsChainArgs {
+  GemvParams p[3];
+  int start[4];          // phase i owns blocks [start[i], start[i+1])
+  int32_t* cnt;
+  int32_t* err;
+};
+struct GemvsChainPhase { int ptype, epi; GemvParams p; };
+bool launch_gemvs_chain(const GemvsChainPhase* ph, int n, int32_t* cnt, int32_t* err, hipStream_t st,
+                        int* wgs_out = nullptr);
 void set_gemv_tpw(int tiles_per_wave);    // M > 32 tiles per wave: 0 = auto, 1, 2 (tuning knob)
 int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)

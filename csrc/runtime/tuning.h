@@ -34,6 +34,7 @@ enum Knob : int {
   KNOB_GEMM3_BM,            // gemm3: force rows per workgroup (0 auto, 128, 256); A/B runs only
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
+  KNOB_GEMVS_CHAIN,         // single stream: o -> gate/up -> down as one chained launch (0 / 1)
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes that skip work (wrong results): only in a `make PROBES=1` build, never in the
   // default library, so no environment variable can corrupt a serving or bench run

@@ -83,6 +83,9 @@ _SIGS = {
                           c_void_p, c_int64, c_void_p], c_int),
     "mp_op_gemvs": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                      c_int, c_void_p, c_int, c_void_p, c_float, c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
+    "mp_op_gemvs_chain3": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                            c_int, c_void_p, c_float, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                            c_void_p], c_int),
     "mp_op_penalize": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float, c_void_p], c_int),
     "mp_op_hist_push": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_sample": ([c_void_p, c_int, c_int, c_int, c_float, c_int, c_float, c_float, ctypes.c_uint64, c_void_p,

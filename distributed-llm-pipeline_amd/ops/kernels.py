@@ -55,6 +55,21 @@ class PackedWeight:
         self.host = pack_t16(raw, ggml_type, n, k, gateup)
         self.dev = torch.from_numpy(self.host).to(device)
 
+    @classmethod
+    def random(cls, ggml_type: int, n: int, k: int, seed: int = 0, scale: float | None = None, device="cuda"):
+        """Random-init blocks of the type generated on the device (mp_init_packed, the synthetic
+        models' weights): no host copy."""
+        self = cls.__new__(cls)
+        self.ggml_type, self.n, self.k = ggml_type, n, k
+        self.ptype = pack_type(ggml_type)
+        self.n_pad, self.k_pad, self.ntiles, self.nsb = packed_dims(ggml_type, n, k)
+        self.host = None
+        nbytes = N.lib().mp_packed_bytes(ggml_type, n, k)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        N.check(N.lib().mp_init_packed(_ptr(self.dev), nbytes, self.ptype, scale if scale else 1.0 / k ** 0.5, seed,
+                                       _stream()), "init_packed")
+        return self
+
     def unpack(self) -> torch.Tensor:
         out = torch.zeros(self.n_pad, self.k_pad, dtype=torch.float16, device=self.dev.device)
         N.check(N.lib().mp_op_unpack(self.ptype, _ptr(self.dev), self.ntiles, self.nsb, _ptr(out), self.k_pad,
@@ -147,6 +162,19 @@ def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4, m
     return N.check(N.lib().mp_op_gemm4_splitk(w.ptype, _ptr(w.dev), w.ntiles, w.nsb, _ptr(x), w.k_pad, M, _ptr(y),
                                                y.stride(0), w.n, _ptr(scratch), scratch.numel(), _stream()),
                    "gemm_splitk")
+
+
+def gemvs_chain3(wo: PackedWeight, wgu: PackedWeight, wdn: PackedWeight, attn: torch.Tensor, x: torch.Tensor,
+                 gamma: torch.Tensor, eps: float, h: torch.Tensor, cnt: torch.Tensor) -> int:
+    """One decode row's o -> gate/up -> down as ONE chained launch (gemvs.hip gemvs_chain_kernel):
+    x += o(attn); h = SwiGLU(gate/up(rmsnorm(x) gamma)); x += down(h).  attn f16 [1][wo.k_pad], x f32
+    [1][d] (updated in place), h f16 [1][wdn.k_pad], cnt int32 [16] zeroed once ([8]: the poll
+    give-up flag).  Returns the workgroups launched (0: the chain does not apply)."""
+    d, F = x.shape[1], wgu.n // 2
+    return N.check(N.lib().mp_op_gemvs_chain3(wo.ptype, _ptr(wo.dev), wo.ntiles, wo.nsb, _ptr(attn), attn.stride(0),
+                                               wgu.ptype, _ptr(wgu.dev), wgu.ntiles, wgu.nsb, _ptr(x), d, _ptr(gamma),
+                                               eps, _ptr(h), h.stride(0), F, wdn.ptype, _ptr(wdn.dev), wdn.ntiles,
+                                               wdn.nsb, _ptr(cnt), _stream()), "gemvs_chain3")
 
 
 def moe_route(logits: torch.Tensor, k: int, list_cap: int | None = None):

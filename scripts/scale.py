@@ -101,7 +101,8 @@ def main():
             p["efficiency"] = round(p["value"] / (p["n_gpus"] * base["value"]), 3)
     out = {"metric": "decode tokens/sec (whole node) + p50/token", "launcher": a.launcher, "scaling": "weak",
            "visible_gpus": have, "points": points}
-    rec = last_bench_record()
+    # the driver's BENCH record is the default (headline) configuration: compare only that one
+    rec = last_bench_record() if not any(x in a.bench_args for x in ("--model", "--ftype", "--mb-size")) else None
     if rec and base:
         out["n1_vs_bench_record"] = dict(rec, n1_value=base["value"],
                                          ratio=round(base["value"] / rec["value"], 3) if rec.get("value") else None)

@@ -1,0 +1,90 @@
+"""Chained single-stream GEMVs (gemvs.hip gemvs_chain_kernel, launch_gemvs_chain): a decode row's
+o -> gate/up -> down as ONE launch whose phases hand off through sc1 stores and agent-scope
+counters.  Checked against the same three GEMVs launched one by one (the engine's unchained path)
+and against a plain PyTorch fp32 reference, at the Llama-3-8B and 70B widths, with the Q4_K and the
+Q6_K down projection; the counters must re-arm (several launches back to back, bitwise repeatable)
+and the poll's give-up flag must stay clear."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def nmse(a, b):
+    a, b = a.double(), b.double()
+    return float(((a - b) ** 2).sum() / ((b ** 2).sum() + 1e-30))
+
+
+SHAPES = {"8b": (4096, 14336), "70b": (8192, 28672)}
+
+
+@pytest.mark.parametrize("shape", ["8b", "70b"])
+@pytest.mark.parametrize("down_qt", ["Q4_K", "Q6_K"])
+def test_chain_matches_separate_launches(cuda, native, shape, down_qt):
+    from mipipe.ops.kernels import PackedWeight, gemv_small, gemvs_chain3, EPI_ATOMIC, EPI_SWIGLU
+    from mipipe.utils import quants as Q
+    d, F = SHAPES[shape]
+    dq = Q.Q6_K if down_qt == "Q6_K" else Q.Q4_K
+    wo = PackedWeight.random(Q.Q4_K, d, d, seed=1)
+    wgu = PackedWeight.random(Q.Q4_K, 2 * F, d, seed=2)
+    wdn = PackedWeight.random(dq, d, F, seed=3)
+    g = torch.Generator().manual_seed(5)
+    x0 = (torch.randn(1, d, generator=g) * 2).cuda()
+    attn = torch.randn(1, wo.k_pad, generator=g).half().cuda()
+    gamma = (torch.rand(d, generator=g) + 0.5).cuda()
+    eps = 1e-5
+
+    # unchained: the engine's three gemvs launches
+    x1 = x0.clone()
+    gemv_small(wo, EPI_ATOMIC, x=attn, y=x1)
+    h1 = torch.zeros(1, wdn.k_pad, dtype=torch.float16, device="cuda")
+    gemv_small(wgu, EPI_SWIGLU, xf=x1, gamma=gamma, eps=eps, y=h1[:, :F])
+    gemv_small(wdn, EPI_ATOMIC, x=h1, y=x1)
+
+    cnt = torch.zeros(16, dtype=torch.int32, device="cuda")
+    outs = []
+    for _ in range(3):   # the counters re-arm between launches
+        x2 = x0.clone()
+        h2 = torch.zeros(1, wdn.k_pad, dtype=torch.float16, device="cuda")
+        wgs = gemvs_chain3(wo, wgu, wdn, attn, x2, gamma, eps, h2, cnt)
+        assert wgs > 0, "chain did not launch"
+        torch.cuda.synchronize()
+        outs.append((x2.cpu(), h2.cpu()))
+    assert int(cnt[8]) == 0, "a chain poll gave up"
+    assert int(cnt[:4].abs().sum()) == 0, f"counters not re-armed: {cnt[:4].tolist()}"
+    for xo, ho in outs[1:]:
+        assert torch.equal(xo, outs[0][0]) and torch.equal(ho, outs[0][1])
+    x2, h2 = outs[0]
+    # same arithmetic up to the in-workgroup k-split (the chain may pick other tiles per workgroup)
+    assert nmse(h2[:, :F].float(), h1[:, :F].float().cpu()) < 1e-5
+    assert nmse(x2 - x0.cpu(), (x1 - x0).cpu()) < 1e-5
+
+    # fp32 reference of the whole block
+    wo_d, wgu_d, wdn_d = wo.unpack().float(), wgu.unpack().float(), wdn.unpack().float()
+    xr = x0 + attn[:, :d].float() @ wo_d.T
+    xn = (xr * torch.rsqrt((xr * xr).mean(-1, keepdim=True) + eps) * gamma).half().float()
+    gu = xn @ wgu_d.T
+    gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(F)], device="cuda")
+    hr = (torch.nn.functional.silu(gu[:, gi]) * gu[:, gi + 8]).half().float()
+    xr = xr + hr @ wdn_d.T
+    assert nmse(x2 - x0.cpu(), (xr - x0).cpu()) < 1e-4
+
+
+def test_chain_in_engine_matches_unchained(cuda, native, model_dir):
+    """The engine with the knob on (GEMVS_CHAIN=1) generates what it generates without it."""
+    import numpy as np
+    from conftest import make_model
+    from mipipe import _native as N
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
+    rng = np.random.default_rng(3)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, 7)]]
+    with Engine(gguf=path, max_ctx=128) as eng:
+        ref, _ = eng.generate(prompts, 12)
+    N.check(N.lib().mp_set_knob(b"GEMVS_CHAIN", 1), "knob")
+    try:
+        with Engine(gguf=path, max_ctx=128) as eng:
+            out, _ = eng.generate(prompts, 12)
+    finally:
+        N.lib().mp_set_knob(b"GEMVS_CHAIN", 0)
+    assert out == ref
