@@ -514,8 +514,8 @@ bool gemm4_supported(int ptype);
 
 // K splits of a gemm4 launch: enough workgroups for one round over the 256 CUs (one 8-wave
 // workgroup per CU: the 3-stage LDS ring takes ~130 KB), >= 16 stages (1024 k) per split
-static int g4_splits(int wgs, int n_stages) {
-  const int target = knob(KNOB_GEMM2_SPLIT_WG);
+static int g4_splits(int wgs, int n_stages, int per_cu = 1) {
+  const int target = knob(KNOB_GEMM2_SPLIT_WG) * per_cu;
   if (wgs >= target) return 1;
   return std::max(1, std::min(target / wgs, n_stages / 16));
 }
@@ -564,6 +564,7 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
 static int g4_bm(int ptype, int M, int ntiles) {
   if (is16(ptype)) return 128;
   if (knob(KNOB_GEMM3_BM)) return knob(KNOB_GEMM3_BM);
+  if (M <= 64 && knob(KNOB_GEMM4_M64)) return 64;   // 64-row micro-batches on the GEMM (opt-in)
   if (M <= 128) return 128;
   const int cgs = (ntiles + 15) / 16;
   return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;
@@ -587,6 +588,9 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  } else if (bm == 64) {   // 60 KB of LDS: two workgroups per CU
+    if (nw7) gemm4_go<PT, EPI, 64, false, 7>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 64>(p, nsplit, st);
   } else if (bm == 128) {
     if (nw7) gemm4_go<PT, EPI, 128, false, 7>(p, nsplit, st);
     else gemm4_go<PT, EPI, 128>(p, nsplit, st);
@@ -607,7 +611,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
     const int n_stages = p.nsb * 4;
     int ns = 1;
     if (scratch) {   // split-K partial stores: split s writes scratch + s * M * ldp
-      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
       const int per = (n_stages + ns - 1) / ns;
       ns = (n_stages + per - 1) / per;
       const int ldp = p.ntiles * 16;
@@ -617,7 +621,8 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
       gemm4_bm<PT, EPI_STORE>(p, ns, st);
       return true;
     }
-    if (epi == EPI_ATOMIC && allow_split) ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+    if (epi == EPI_ATOMIC && allow_split)
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
     switch (epi) {
       case EPI_STORE: gemm4_bm<PT, EPI_STORE>(p, 1, st); break;
       case EPI_ATOMIC: gemm4_bm<PT, EPI_ATOMIC>(p, ns, st); break;
@@ -645,7 +650,7 @@ int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
   const int bm = g4_bm(ptype, M, ntiles);
   const int wgs = (ntiles + 15) / 16 * ((M + bm - 1) / bm);
   const int n_stages = nsb * 4;
-  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages);
+  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
   ns = std::max(1, std::min(ns, n_stages));
   const int per = (n_stages + ns - 1) / ns;
   return (n_stages + per - 1) / per;

@@ -509,7 +509,7 @@ void HipStage::alloc_runtime() {
     auto acc = [&](const PackedMat& m) {
       if (!m.d || is16(m.ptype)) return;
       for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
-        if (M <= 64) continue;
+        if (M <= (knob(KNOB_GEMM4_M64) ? 32 : 64)) continue;
         int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
         if (opt_.prefill_gemm_v == 4 || opt_.prefill_gemm_v == 0)
           ns = std::max(ns, gemm4_splits(m.ptype, (int)m.dims.ntiles, (int)m.dims.nsb, M));
@@ -756,7 +756,11 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     launch_gemm3(P_I8, epi, p, st, allow_split && !opt_.deterministic);
     return;
   }
-  if (M > 64 && opt_.prefill_gemm && gv == 4 && gemm4_supported(m.ptype)) {
+  // (opt-in, knob GEMM4_M64: 33-64 row micro-batches on gemm4's 64-row tiles, where the GEMV's MFMA
+  // time is exposed -- PERFORMANCE.md 'Why the 70B mb64 GEMV did not move further')
+  const bool g4m64 = M > 32 && M <= 64 && !extras && !is16(m.ptype) && knob(KNOB_GEMM4_M64) && opt_.prefill_gemm &&
+                     opt_.prefill_gemm_v == 0 && gemm4_supported(m.ptype);
+  if ((M > 64 || g4m64) && opt_.prefill_gemm && gv == 4 && gemm4_supported(m.ptype)) {
     // v4 GEMM (gemm4.hip: 32x32x16 MFMA): split-K shapes store per-split partials like v2 (into the
     // residual x: absorbed by the next RMSNorm), the rest run whole-K
     GemvParams p{};

@@ -35,6 +35,7 @@ enum Knob : int {
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
   KNOB_GEMVS_CHAIN,         // single stream: o -> gate/up -> down as one chained launch (0 / 1)
+  KNOB_GEMM4_M64,           // decode micro-batches of 33-64 rows on gemm4's 64-row tiles instead of the GEMV (0 / 1)
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes that skip work (wrong results): only in a `make PROBES=1` build, never in the
   // default library, so no environment variable can corrupt a serving or bench run
