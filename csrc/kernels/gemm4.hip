@@ -41,6 +41,14 @@ __device__ __forceinline__ f32x16 mma32(half8_t a, half8_t b, f32x16 c) {
   else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// dword P of a B fragment register
+template <int P>
+__device__ __forceinline__ void set_dw(half8_t& f, uint32_t v) {
+  u32x4 u = __builtin_bit_cast(u32x4, f);
+  u[P] = v;
+  f = __builtin_bit_cast(half8_t, u);
+}
+
 // Per-type reads of one wave's raw stage image (W3<PT>::issue layout, TW tiles) in the 32x32
 // mapping: column pair `pair` = tiles 2 pair, 2 pair + 1 (32 columns, one MFMA B operand).
 template <int PT> struct W4;
@@ -65,6 +73,17 @@ template <> struct W4<P_Q4_K> {
     const int kk = t >> 1, e = t & 1;
     return nib8(w.q[kk][e], kk ? h2hi(p.S2) : h2lo(p.S2), kk ? h2hi(p.M2) : h2lo(p.M2), k);
   }
+  // dword P of frag() (nib8's four independent pairs), so a fragment's dequant can be spread over
+  // the gaps between one wave's MFMAs instead of one 13-instruction VALU burst
+  static constexpr bool kParts = true;
+  template <int P>
+  __device__ static __forceinline__ uint32_t fragp(const Raw& w, const Prep& p, int t, int, const Consts& k) {
+    const int kk = t >> 1, e = t & 1;
+    const uint32_t v = P >= 2 ? w.q[kk][e] >> 8 : w.q[kk][e];
+    const half2_t S = kk ? h2hi(p.S2) : h2lo(p.S2), Mh = kk ? h2hi(p.M2) : h2lo(p.M2);
+    if constexpr (P & 1) return as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mhi, k.mag_lo)) - h2c(64.f), S, Mh));
+    else return as_u32(__builtin_elementwise_fma(as_h2(and_or(v, k.mlo, k.mag_hi)) - h2c(1024.f), S, Mh));
+  }
 };
 
 // Q6_K: quants [u][h][r] 16 B (dwords 2h, 2h+1 = one b64), high bits [u][kk][r] 8 B (the 2-bit
@@ -72,6 +91,7 @@ template <> struct W4<P_Q4_K> {
 // [u][r] (dword q), d [u][r]
 template <> struct W4<P_Q6_K> {
   static constexpr int NR = 6;
+  static constexpr bool kParts = true;
   struct Raw { uint32_t sc, d; u32x2 q[2]; uint32_t qd[2]; };
   struct Prep { uint32_t sc; f16 d; };
   template <int TW>
@@ -105,11 +125,31 @@ template <> struct W4<P_Q6_K> {
                  as_u32((as_h2(and_or(tt, k.mlo, h2)) - h2c(1056.f)) * S),
                  as_u32((as_h2(and_or(tt, k.mhi, h3)) - h2c(96.f)) * S));
   }
+  // dword P of frag() (the scale and high-bit words are shared: the compiler keeps them between steps)
+  template <int P>
+  __device__ static __forceinline__ uint32_t fragp(const Raw& w, const Prep& p, int t, int h, const Consts& k) {
+    const int kk = t >> 1, e = t & 1;
+    const uint32_t h16 = (w.qd[kk] >> (16 * e)) & 0xFFFFu;
+    const uint32_t sb = (p.sc >> (8 * (2 * kk + h))) & 0xFFu;
+    const f16 sf = (as_h2(0x6400u | sb).x - (f16)1152.f) * p.d;
+    const half2_t S = half2_t{sf, sf};
+    const uint32_t x = h16 | (h16 << 8);
+    const uint32_t v = P >= 2 ? w.q[kk][e] >> 8 : w.q[kk][e];
+    if constexpr (P == 0) return as_u32((as_h2(and_or(v, k.mlo, ((x << 4) & 0x00300030u) | k.mag_hi)) - h2c(1056.f)) * S);
+    if constexpr (P == 1) return as_u32((as_h2(and_or(v, k.mhi, ((x << 6) & 0x03000300u) | k.mag_lo)) - h2c(96.f)) * S);
+    if constexpr (P == 2) return as_u32((as_h2(and_or(v, k.mlo, (x & 0x00300030u) | k.mag_hi)) - h2c(1056.f)) * S);
+    return as_u32((as_h2(and_or(v, k.mhi, ((x << 2) & 0x03000300u) | k.mag_lo)) - h2c(96.f)) * S);
+  }
 };
 
 // Q5_K: quants as Q4_K, high-bit dword [u][kk][r] (byte g = dword g's 8 high bits), header [u][r]
 template <> struct W4<P_Q5_K> {
   static constexpr int NR = 5;
+  static constexpr bool kParts = false;
+  template <int P, class RW, class PR>   // (unused: kParts false) the whole fragment's dword P
+  __device__ static __forceinline__ uint32_t fragp(const RW& w, const PR& p, int t, int h, const Consts& k) {
+    return __builtin_bit_cast(u32x4, frag(w, p, t, h, k))[P];
+  }
   struct Raw { u32x4 hdr; u32x2 q[2]; uint32_t qh[2]; };
   struct Prep { half2_t S2, M2; };
   template <int TW>
@@ -146,6 +186,11 @@ template <> struct W4<P_Q5_K> {
 // dwords g = 2h, 2h+1 of the 16x16 map (one b128 per kk); block scales [u][r] = (d(2q), d(2q+1))
 template <> struct W4<P_Q8_0> {
   static constexpr int NR = 3;
+  static constexpr bool kParts = false;
+  template <int P, class RW, class PR>   // (unused: kParts false) the whole fragment's dword P
+  __device__ static __forceinline__ uint32_t fragp(const RW& w, const PR& p, int t, int h, const Consts& k) {
+    return __builtin_bit_cast(u32x4, frag(w, p, t, h, k))[P];
+  }
   struct Raw { uint32_t dd; u32x4 v[2]; };
   struct Prep { uint32_t dd; };
   template <int TW>
@@ -173,6 +218,11 @@ template <> struct W4<P_Q8_0> {
 // (h, c) of MFMA t needs piece g = 2h + e of (u, kk, r)
 template <int PT> struct W4_16 {
   static constexpr int NR = 4;
+  static constexpr bool kParts = false;
+  template <int P, class RW, class PR>   // (unused: kParts false) the whole fragment's dword P
+  __device__ static __forceinline__ uint32_t fragp(const RW& w, const PR& p, int t, int h, const Consts& k) {
+    return __builtin_bit_cast(u32x4, frag(w, p, t, h, k))[P];
+  }
   struct Raw { u32x4 v[4]; };
   struct Prep {};
   template <int TW>
@@ -345,8 +395,12 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   // A fragments read AD steps ahead (8; half the stage's NA fragments for the 64-row MoE tile)
   constexpr int NA = 4 * FR, AD = NA >= 16 ? 8 : NA / 2, NR = Q::NR * NPR, JB = NA - AD - 1;
   // B fragment t + 1 is dequantized at step i = IB of fragment t (behind the first MFMAs of t)
-  constexpr int IB = FR >= 4 ? FR / 2 : 0;
+  // B fragment t + 1 is dequantized right behind fragment t's first MFMA (FR - 1 steps of slack
+  // for its VALU chain), and the next stage's scales + first B fragment three steps after its raw
+  // bytes were read (JP), not on the last step: the stage's first MFMA no longer waits for them
+  constexpr int IB = FR >= 4 ? 1 : 0;
   static_assert(JB > FR / 2 && NA - AD > JB, "gemm4: barrier step");
+  constexpr int JP = JB + 3 < NA - 2 ? JB + 3 : NA - 2;   // next stage's prep step (bf[.][0] of this stage: last use at FR - 1 < JB)
   static_assert(JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
   using RawT = typename Q::Raw;
   using PrepT = typename Q::Prep;
@@ -404,7 +458,16 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], b);
       // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
       // stage's value was FR steps ago)
-      if constexpr (i == IB && t < 3) {
+      if constexpr (Q::kParts && t < 3) {
+        // fragment t + 1 one dword per step (steps 0-3 of fragment t; 0, 0, 1, 1 at two row fragments)
+        static_for<4>([&](auto pc) {
+          constexpr int P = decltype(pc)::value;
+          if constexpr (i == (FR >= 4 ? P : P / 2)) {
+#pragma unroll
+            for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][t + 1], Q::template fragp<P>(raw[pp], pr[pp], t + 1, h, kc));
+          }
+        });
+      } else if constexpr (i == IB && t < 3) {
 #pragma unroll
         for (int pp = 0; pp < NPR; ++pp) bf[pp][t + 1] = Q::frag(raw[pp], pr[pp], t + 1, h, kc);
       }
@@ -430,13 +493,19 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
           }
         }
         if constexpr (j > JB) read_a(std::integral_constant<int, j - JB - 1>{}, af_n[j - JB - 1], b1);
-        if constexpr (j == NA - 2) {   // stage s+1's raw bytes are older than its last fragment read
+        constexpr bool split0 = Q::kParts && JP + 4 < NA;   // bf[.][0] of stage s+1 one dword per step after JP
+        if constexpr (j == JP) {   // stage s+1's raw bytes: the j - JB fragment reads after them may be in flight
           wait_lgkm<(j - JB < 15 ? j - JB : 15)>();
 #pragma unroll
           for (int pp = 0; pp < NPR; ++pp) {   // (bf[.][0] of stage s: last use at j = FR - 1)
             pr_n[pp] = Q::prep(raw_n[pp], (s + 1) & 3);
-            bf[pp][0] = Q::frag(raw_n[pp], pr_n[pp], 0, h, kc);
+            if constexpr (!split0) bf[pp][0] = Q::frag(raw_n[pp], pr_n[pp], 0, h, kc);
           }
+        }
+        if constexpr (split0 && j > JP && j <= JP + 4) {
+          constexpr int P = j - JP - 1;
+#pragma unroll
+          for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][0], Q::template fragp<P>(raw_n[pp], pr_n[pp], 0, h, kc));
         }
       }
     });

@@ -47,6 +47,10 @@ def test_chain_matches_separate_launches(cuda, native, shape, down_qt):
         x2 = x0.clone()
         h2 = torch.zeros(1, wdn.k_pad, dtype=torch.float16, device="cuda")
         wgs = gemvs_chain3(wo, wgu, wdn, attn, x2, gamma, eps, h2, cnt)
+        if wgs == 0 and shape == "70b":
+            # 70B's gate/up alone needs 448 workgroups of 8 tiles: the three phases do not fit the
+            # resident budget (2 per CU), so the launcher declines and the engine runs three launches
+            pytest.skip("70B phases exceed the resident budget: chain declined (engine falls back)")
         assert wgs > 0, "chain did not launch"
         torch.cuda.synchronize()
         outs.append((x2.cpu(), h2.cpu()))
