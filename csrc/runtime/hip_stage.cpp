@@ -60,6 +60,9 @@ HipStage::HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOpt
 HipStage::~HipStage() {
   (void)hipSetDevice(spec_.device);
   destroy_graphs();
+  if (pf_st_) (void)hipStreamDestroy(pf_st_);
+  if (pf_fork_) (void)hipEventDestroy(pf_fork_);
+  if (pf_join_) (void)hipEventDestroy(pf_join_);
   for (void* p : allocs_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -499,6 +502,7 @@ void HipStage::alloc_runtime() {
   }
   attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
   chain_cnt_ = (int32_t*)zalloc(16 * 4);
+  pf_sink_ = (uint32_t*)zalloc(64 * 4);
   if (opt_.prefill_flash && opt_.max_ctx > 256) {   // prefill KV-split partials (attn_prefill.hip)
     pf_opart_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * Dp_ * 4);
     pf_ml_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * 2 * 4);
@@ -933,6 +937,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
   if (small_path(M)) {
+    if (decode) prefetch_layer(li, st);
     // gemvs: RMSNorms fused into the qkv / gate-up GEMVs, complete outputs per workgroup (q|k|v
     // stored with its bias, o / down added into the residual by their single owner)
     const bool two = knob(KNOB_GEMVS2) != 0;
@@ -1287,9 +1292,50 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
   dec_slot0_ = slot_of(mb, 0);   // slot_[mb] holds slot_of(mb, b) = dec_slot0_ + b
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
+  prefetch_join(st);
   flush_sk(st);
   if (spec_.last()) head(mb, B, x, tok_[mb], (uint64_t)mb + 1, st);
   launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
+}
+
+// The single stream's GEMVs are latency-bound except gate/up and down, and those read up to ~25 %
+// faster from the 256 MiB Infinity Cache (profiles/r2w_gemv_mall_hot_cold.txt): while qkv,
+// attention and o leave HBM idle, a side stream reads this layer's o / gate-up / down and the next
+// layer's qkv into the MALL.  Layers over 160 MB (70B: 0.43 GB) would evict themselves: no prefetch.
+// The side stream is forked per layer (an event on the compute stream) and joined once per decode
+// step (prefetch_join), so a captured graph holds it as a parallel branch.
+void HipStage::prefetch_layer(int li, hipStream_t st) {
+  const int grid = knob(KNOB_PREFETCH);
+  const LayerW& L = layers_[li];
+  if (grid <= 0 || L.moe || !L.fused_gateup || !pf_sink_) return;
+  PrefetchArgs a{};
+  auto add = [&](const PackedMat& m) {
+    if (m.d && a.n < 6) { a.p[a.n] = m.d; a.bytes[a.n] = m.bytes(); ++a.n; }
+  };
+  add(L.wo);
+  add(L.gateup);
+  add(L.down);
+  if (li + 1 < (int)layers_.size())
+    for (const MatSeg& sg : layers_[li + 1].qkv) add(sg.m);
+  uint64_t total = 0;
+  for (int i = 0; i < a.n; ++i) total += a.bytes[i];
+  if (total > ((uint64_t)160 << 20)) return;
+  if (!pf_st_) {
+    HIP_OK(hipStreamCreateWithFlags(&pf_st_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&pf_fork_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&pf_join_, hipEventDisableTiming));
+  }
+  HIP_OK(hipEventRecord(pf_fork_, st));
+  HIP_OK(hipStreamWaitEvent(pf_st_, pf_fork_, 0));
+  launch_prefetch(a, grid, pf_sink_, pf_st_);
+  pf_open_ = true;
+}
+
+void HipStage::prefetch_join(hipStream_t st) {
+  if (!pf_open_) return;
+  HIP_OK(hipEventRecord(pf_join_, pf_st_));
+  HIP_OK(hipStreamWaitEvent(st, pf_join_, 0));
+  pf_open_ = false;
 }
 
 void HipStage::capture_graphs() {

@@ -211,6 +211,14 @@ class HipStage : public Stage {
   int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
   int32_t* chain_cnt_ = nullptr;  // chained o -> gate/up -> down (launch_gemvs_chain): [0..3] counters, [8] error flag
   bool chain_layer(const LayerW& L, int M, float* x, hipStream_t st);
+  // MALL prefetch (knob PREFETCH, single stream): a side stream forked at each layer's start reads
+  // that layer's o / gate-up / down and the next layer's qkv while qkv / attention / o run
+  hipStream_t pf_st_ = nullptr;
+  hipEvent_t pf_fork_ = nullptr, pf_join_ = nullptr;
+  uint32_t* pf_sink_ = nullptr;
+  bool pf_open_ = false;   // a fork not yet joined back into the compute stream
+  void prefetch_layer(int li, hipStream_t st);
+  void prefetch_join(hipStream_t st);
   // MoE scratch
   float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
   float* moe_w_ = nullptr; f16* moe_h_ = nullptr;

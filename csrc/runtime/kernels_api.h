@@ -273,6 +273,14 @@ void launch_penalize(const PenaltyParams& p, hipStream_t st);
 // append tokens[m] to row m's ring: hist[m][cnt[m] % last_n] = tokens[m]; ++cnt[m]
 void launch_hist_push(int32_t* hist, int32_t* cnt, int last_n, const int32_t* tokens, int M, hipStream_t st);
 
+// read up to 6 byte ranges into the Infinity Cache (MALL); sink: >= 64 device u32 (never read)
+struct PrefetchArgs {
+  const void* p[6];
+  uint64_t bytes[6];
+  int n;
+};
+void launch_prefetch(const PrefetchArgs& a, int grid, uint32_t* sink, hipStream_t st);
+
 // pos[i] += 1, kvlen[i] = pos[i] + 1 for i < M (graph-resident decode step advance)
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st);
 
