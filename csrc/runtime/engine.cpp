@@ -163,6 +163,17 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   } else {
     S_ = std::max(1, j.get_int("stages", 1));
   }
+  // gpu_layers (llama-cli -ngl N, n_gpu_layers) below the layer count: like llama.cpp, the LAST N
+  // layers (and the head) are offloaded -- to the `stages` GPU stages, partitioned as usual -- and
+  // the first n_layer - N layers with the embedding run on a CPU stage in front of them (one more
+  // stage; host links on both of its ends).  N <= 0 keeps the engine-wide backend, N >= n_layer
+  // is the all-GPU engine (the reference's -ngl 99).
+  const int ngl = j.get_int("gpu_layers", -1);
+  hybrid_ = !cpu_ && ngl > 0 && ngl < cfg_.n_layer;
+  if (hybrid_ && mode_ == "mp") throw std::runtime_error("gpu_layers < n_layer (hybrid CPU/GPU split) needs mode local");
+  const int S_gpu = S_;
+  if (hybrid_) S_ = S_gpu + 1;
+  const int g0 = hybrid_ ? 1 : 0;   // first GPU stage
   // default prompt chunk: 2048 rows for a single GPU stage (the 128-row GEMM tiles then run 16 row
   // blocks per weight tile group: 8B 41.6k -> 59.0k, 70B 6.3k -> 6.9k prompt tok/s at 64 x 512
   // prompts), 512 when stages pipeline the chunks (finer chunks overlap the stages) or on CPU
@@ -175,34 +186,52 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   kv_fp8_ = kv_fp8;
   if (kv_fp8 && (j.get_str("backend", "hip") == "cpu" || !j.get_bool("fused_attn", true) || !j.get_bool("prefill_flash", true)))
     throw std::runtime_error("kv_dtype fp8 needs the HIP backend with fused_attn and prefill_flash");
+  // devices of the GPU stages (a hybrid split's CPU stage 0 carries the first GPU's id, unused)
   std::vector<int> devices(S_);
-  for (int s = 0; s < S_; ++s) devices[s] = s;
+  for (int s = g0; s < S_; ++s) devices[s] = s - g0;
   if (j.has("devices")) {
     auto& a = j["devices"].arr();
-    for (int s = 0; s < S_; ++s) devices[s] = (int)a[s % a.size()].num();
+    for (int s = g0; s < S_; ++s) devices[s] = (int)a[(s - g0) % a.size()].num();
   }
+  if (hybrid_) devices[0] = devices[1];
   if (mode_ == "mp") devices[rank_] = j.get_int("device", devices[rank_]);
   // per-stage speed for the cost partitioner: given (device_speed: [..]), or measured
   // (device_speed: "probe", Halda-style; mp mode: every rank must pass the same list, which
   // mipipe.parallel.init_from_torchrun(device_speed="probe") gathers over torch.distributed)
-  std::vector<double> speed(S_, 1.0);
+  // (hybrid: the speeds of the GPU stages, which split the offloaded layers among themselves)
+  std::vector<double> speed(S_gpu, 1.0);
   if (j.has("device_speed") && j["device_speed"].is_str()) {
     if (j["device_speed"].str() != "probe") throw std::runtime_error("device_speed: a list or \"probe\"");
     if (mode_ == "mp") throw std::runtime_error("device_speed probe in mp mode: gather the list across ranks first");
     std::map<int, DeviceProfile> seen;
-    for (int s = 0; s < S_; ++s) {
-      if (!seen.count(devices[s])) seen[devices[s]] = cpu_ ? probe_host() : probe_device(devices[s]);
-      speed[s] = seen[devices[s]].speed();
+    for (int s = 0; s < S_gpu; ++s) {
+      const int dv = devices[s + g0];
+      if (!seen.count(dv)) seen[dv] = cpu_ ? probe_host() : probe_device(dv);
+      speed[s] = seen[dv].speed();
     }
     // stages sharing one device (single-GPU emulation) split its speed
     std::map<int, int> share;
-    for (int s = 0; s < S_; ++s) share[devices[s]]++;
-    for (int s = 0; s < S_; ++s) speed[s] /= share[devices[s]];
+    for (int s = 0; s < S_gpu; ++s) share[devices[s + g0]]++;
+    for (int s = 0; s < S_gpu; ++s) speed[s] /= share[devices[s + g0]];
   } else if (j.has("device_speed")) {
-    for (int s = 0; s < S_ && s < (int)j["device_speed"].arr().size(); ++s) speed[s] = j["device_speed"].arr()[s].num();
+    for (int s = 0; s < S_gpu && s < (int)j["device_speed"].arr().size(); ++s) speed[s] = j["device_speed"].arr()[s].num();
   }
   device_speed_ = speed;
-  specs_ = partition_layers(layer_cost, embd_cost, head_cost, speed, parse_split_mode(j.get_str("split", "cost")));
+  const SplitMode split_mode = parse_split_mode(j.get_str("split", "cost"));
+  if (hybrid_) {
+    const int Lc = cfg_.n_layer - ngl;   // layers kept on the CPU
+    std::vector<double> gcost(layer_cost.begin() + Lc, layer_cost.end());
+    std::vector<StageSpec> g = partition_layers(gcost, 0.0, head_cost, speed, split_mode);
+    StageSpec c;
+    c.stage = 0; c.n_stages = S_; c.layer_begin = 0; c.layer_end = Lc;
+    specs_.assign(1, c);
+    for (StageSpec sp : g) {
+      sp.stage += 1; sp.n_stages = S_; sp.layer_begin += Lc; sp.layer_end += Lc;
+      specs_.push_back(sp);
+    }
+  } else {
+    specs_ = partition_layers(layer_cost, embd_cost, head_cost, speed, split_mode);
+  }
   for (int s = 0; s < S_; ++s) specs_[s].device = devices[s];
   // --gpu-mem (prima.cpp): per-GPU memory budget in GiB; caps the auto KV sizing and
   // is checked against every stage's weights + KV below (--force downgrades the failure to a warning)
@@ -233,7 +262,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li] + layer_extra[li];
       if (sp.first()) w += embd_bytes;
       if (sp.last()) w += head_cost;
-      const int key = mode_ == "mp" ? sp.stage : devices[sp.stage];
+      const int key = stage_cpu(sp.stage) && hybrid_ ? -1 : mode_ == "mp" ? sp.stage : devices[sp.stage];   // -1: host
       dev_w[key] += w;
       dev_l[key] += sp.layer_end - sp.layer_begin;
       dev_n[key] += 1;
@@ -242,11 +271,12 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     double per_tok = 0;
     int lmax = 1;
     for (auto& e : dev_w) {
+      const bool host = cpu_ || e.first == -1;   // CPU stages: f32 KV in host memory
       const int layers = std::max(1, dev_l[e.first]);
-      const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (cpu_ ? 4.0 : kv_fp8 ? 1.0 : 2.0);
+      const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (host ? 4.0 : kv_fp8 ? 1.0 : 2.0);
       const double reserve =
           dev_n[e.first] * (4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4);
-      const double budget = frac * cap_bytes - e.second - reserve;
+      const double budget = frac * (host ? 64.0 * (1 << 30) : cap_bytes) - e.second - reserve;
       // paged KV: the pool holds the LIVE tokens of all slots (not n_slots x max_ctx)
       const long c = budget > 0 ? (long)(budget / pt) : 0;
       if (c < ctx) { ctx = c; per_tok = pt; lmax = layers; }
@@ -276,7 +306,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     std::map<int, std::pair<double, double>> need;   // device -> (weights, kv)
     std::map<int, std::string> who;
     for (auto& sp : specs_) {
-      if (mode_ == "mp" && sp.stage != rank_) continue;
+      if ((mode_ == "mp" && sp.stage != rank_) || (hybrid_ && stage_cpu(sp.stage))) continue;   // per GPU
       double w = 0;
       for (int li = sp.layer_begin; li < sp.layer_end; ++li) w += layer_cost[li] + layer_extra[li];
       if (sp.first()) w += embd_b;
@@ -350,7 +380,8 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     if (mode_ == "mp" && s != rank_) continue;
     auto w = std::make_unique<Worker>();
     w->device = specs_[s].device;
-    if (cpu_) {
+    w->cpu = stage_cpu(s);
+    if (w->cpu) {
       w->stage.reset(new CpuStage(cfg_, specs_[s], so));
     } else {
       HIP_OK(hipSetDevice(w->device));
@@ -363,7 +394,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
                            (float)j.get_num("min_p", 0.0), seed);
     w->stage->set_penalties(j.get_int("repeat_last_n", 64), (float)j.get_num("repeat_penalty", 1.0),
                             (float)j.get_num("frequency_penalty", 0.0), (float)j.get_num("presence_penalty", 0.0));
-    if (cpu_) {
+    if (w->cpu) {
       w->ring_pending.assign(M_, false);
       workers_.push_back(std::move(w));
       continue;
@@ -396,7 +427,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     else if (ad == "f16") act_dtype_ = ACT_F16;
     else if (ad == "bf16") act_dtype_ = ACT_BF16;
     else throw std::runtime_error("act_dtype must be auto, f32, f16 or bf16");
-    if (cpu_) act_dtype_ = ACT_F32;
+    if (cpu_ || hybrid_) act_dtype_ = ACT_F32;   // host links carry the f32 residual
     if (act_dtype_ != ACT_F32 && S_ > 1) {
       const size_t wb = (size_t)std::max(chunk_, B_) * cfg_.d_model * 2;
       for (auto& w : workers_) {
@@ -422,6 +453,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     out_host_ = out_vec_.data();
   } else {
     for (auto& w : workers_) {
+      if (w->cpu) continue;
       HIP_OK(hipSetDevice(w->device));
       w->stage->capture_graphs();
     }
@@ -439,7 +471,7 @@ Engine::~Engine() {
   } catch (...) {
   }
   for (auto& w : workers_) {
-    if (cpu_) {
+    if (w->cpu) {
       w->stage.reset();
       continue;
     }
@@ -476,7 +508,8 @@ void Engine::build_links(const Json& j) {
     // thread per GPU).  RCCL refuses a communicator with two ranks on one GPU, and may be unusable
     // on a box; then the link falls back to the peer-copy LocalLink and says so (info()["links"]).
     // "auto": rccl when every stage has its own GPU, local otherwise.
-    std::string kind = cpu_ ? "host" : j.get_str("link", "local");
+    // (a hybrid split: host links everywhere; the GPU ends copy through host memory)
+    std::string kind = cpu_ || hybrid_ ? "host" : j.get_str("link", "local");
     if (kind == "auto") {
       std::vector<int> d;
       for (auto& sp : specs_) d.push_back(sp.device);
@@ -485,7 +518,7 @@ void Engine::build_links(const Json& j) {
     }
     for (int i = 0; i < S_; ++i) {
       const int a = i, b = (i + 1) % S_;
-      if (cpu_) {
+      if (kind == "host") {
         links_.emplace_back(new HostLink(std::max(4, M_ + 2)));
         workers_[a]->out = links_.back().get();
         workers_[b]->in = links_.back().get();
@@ -615,7 +648,7 @@ void Engine::span(Worker& w, hipStream_t s, int tid, const std::string& name, co
   Worker::TraceRecT r;
   r.name = name;
   r.tid = tid;
-  if (cpu_) {
+  if (w.cpu) {
     r.ta = now_ms();
     body();
     r.tb = now_ms();
@@ -696,7 +729,7 @@ void Engine::run_items_cpu(Worker& w, const std::vector<Item>& items) {
 }
 
 void Engine::run_items(Worker& w, const std::vector<Item>& items) {
-  if (cpu_) return run_items_cpu(w, items);
+  if (w.cpu) return run_items_cpu(w, items);
   HIP_OK(hipSetDevice(w.device));
   Stage& st = *w.stage;
   hipStream_t cs = st.stream();
@@ -834,7 +867,7 @@ void Engine::collect_trace() {
     const int pid = w.stage->spec().stage;
     for (auto& r : w.tr) {
       double ta = r.ta, tb = r.tb;
-      if (!cpu_) {
+      if (!w.cpu) {
         float ea = 0, eb = 0;
         HIP_OK(hipEventElapsedTime(&ea, w.tr_base, r.a));
         HIP_OK(hipEventElapsedTime(&eb, w.tr_base, r.b));
@@ -992,6 +1025,7 @@ void Engine::sync_all() {
   if (cpu_) return;
   const double deadline = now_ms() + watchdog_s_ * 1e3;
   for (auto& w : workers_) {
+    if (w->cpu) continue;
     HIP_OK(hipSetDevice(w->device));
     for (hipStream_t s : {w->stage->stream(), w->send_st, w->recv_st}) {
       for (;;) {
@@ -1030,7 +1064,7 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
   std::vector<Item> items;
   for (auto& w : workers_) {
     Stage& st = *w->stage;
-    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    if (!w->cpu) HIP_OK(hipSetDevice(w->device));
     for (int mb = 0; mb < M_; ++mb) {
       std::vector<int32_t> pos(B_, 0);
       for (int b = 0; b < B_; ++b) {
@@ -1049,7 +1083,7 @@ void Engine::start(const std::vector<std::vector<int32_t>>& prompts) {
     if (st.spec().first()) {
       for (size_t i = 0; i < prompts.size(); ++i) {
         if (prompts[i].empty() || (int)prompts[i].size() >= max_ctx_) throw std::runtime_error("bad prompt length");
-        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4);
+        if (w->cpu) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4);
         else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts[i].data(), prompts[i].size() * 4,
                               hipMemcpyHostToDevice));
       }
@@ -1112,7 +1146,7 @@ Json Engine::save_state(const std::string& dir) {
   size_t total = 0;
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
-    if (!cpu_) HIP_OK(hipSetDevice(wp->device));
+    if (!wp->cpu) HIP_OK(hipSetDevice(wp->device));
     Json h = Json::object();
     h["magic"] = "mipipe-stage-state"; h["version"] = 1; h["fingerprint"] = fp;
     h["stage"] = st.spec().stage; h["layer_begin"] = st.spec().layer_begin; h["layer_end"] = st.spec().layer_end;
@@ -1124,7 +1158,7 @@ Json Engine::save_state(const std::string& dir) {
       Json toks = Json::array();
       std::vector<int32_t> t(B_);
       for (int mb = 0; mb < M_; ++mb) {
-        if (cpu_) std::memcpy(t.data(), st.tokens(mb), (size_t)B_ * 4);
+        if (wp->cpu) std::memcpy(t.data(), st.tokens(mb), (size_t)B_ * 4);
         else HIP_OK(hipMemcpy(t.data(), st.tokens(mb), (size_t)B_ * 4, hipMemcpyDeviceToHost));
         for (int b = 0; b < B_; ++b) toks.push(t[b]);
       }
@@ -1228,7 +1262,7 @@ Json Engine::load_state(const std::string& dir) {
   kv_sync();
   for (auto& wp : workers_) {
     Stage& st = *wp->stage;
-    if (!cpu_) HIP_OK(hipSetDevice(wp->device));
+    if (!wp->cpu) HIP_OK(hipSetDevice(wp->device));
     const std::string path = dir + "/stage" + std::to_string(st.spec().stage) + ".bin";
     const std::string raw = slurp(path);
     const size_t nl = raw.find('\n');
@@ -1278,15 +1312,15 @@ Json Engine::load_state(const std::string& dir) {
           t[b] = (int32_t)toks[(size_t)mb * B_ + b].num();
           if (t[b] < 0 || t[b] >= cfg_.vocab) throw std::runtime_error("load_state: token id out of range");
         }
-        if (cpu_) std::memcpy(st.tokens(mb), t.data(), (size_t)B_ * 4);
+        if (wp->cpu) std::memcpy(st.tokens(mb), t.data(), (size_t)B_ * 4);
         else HIP_OK(hipMemcpy(st.tokens(mb), t.data(), (size_t)B_ * 4, hipMemcpyHostToDevice));
       }
       for (size_t i = 0; i < prompts_.size(); ++i) {
-        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
+        if (wp->cpu) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
         else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4,
                               hipMemcpyHostToDevice));
       }
-      if (cpu_) std::fill(wp->ring_pending.begin(), wp->ring_pending.end(), false);
+      if (wp->cpu) std::fill(wp->ring_pending.begin(), wp->ring_pending.end(), false);
     }
     if (st.spec().last()) {   // penalty windows: prompt + accepted tokens
       for (int mb = 0; mb < M_; ++mb) {
@@ -1365,7 +1399,7 @@ void Engine::push_positions(int mb) {
   std::vector<int32_t> pos(B_);
   for (int b = 0; b < B_; ++b) pos[b] = slot_pos((size_t)mb * B_ + b);
   for (auto& w : workers_) {
-    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    if (!w->cpu) HIP_OK(hipSetDevice(w->device));
     w->stage->set_positions(mb, pos);
   }
 }
@@ -1386,7 +1420,7 @@ void Engine::kv_grant(size_t slot, int n_tokens) {
 void Engine::kv_sync() {
   if (!pager_.dirty()) return;
   for (auto& w : workers_) {
-    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    if (!w->cpu) HIP_OK(hipSetDevice(w->device));
     w->stage->set_block_table(pager_.table());
   }
   pager_.clean();
@@ -1418,10 +1452,10 @@ void Engine::admit(const std::vector<int>& slots, const std::vector<std::vector<
   kv_sync();
   for (auto& w : workers_) {
     Stage& st = *w->stage;
-    if (!cpu_) HIP_OK(hipSetDevice(w->device));
+    if (!w->cpu) HIP_OK(hipSetDevice(w->device));
     if (st.spec().first())
       for (size_t i : seqs) {
-        if (cpu_) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
+        if (w->cpu) std::memcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4);
         else HIP_OK(hipMemcpy(st.prompt_buf() + i * max_ctx_, prompts_[i].data(), prompts_[i].size() * 4,
                               hipMemcpyHostToDevice));
       }
@@ -1470,7 +1504,7 @@ StepStats Engine::decode_steps(int k) {
     if (i < active_.size() && active_[i]) kv_grant(i, slot_pos(i) + k + 1);
   kv_sync();
   for (auto& w : workers_)
-    if (w->stage->spec().last() && cpu_) {
+    if (w->stage->spec().last() && w->cpu) {
       w->tok_t.clear();
     } else if (w->stage->spec().last()) {
       HIP_OK(hipSetDevice(w->device));
@@ -1491,7 +1525,7 @@ StepStats Engine::decode_steps(int k) {
   StepStats ss;
   ss.wall_ms = now_ms() - t0;
   for (auto& w : workers_)
-    if (w->stage->spec().last() && cpu_) {
+    if (w->stage->spec().last() && w->cpu) {
       for (size_t i = M_; i < w->tok_t.size(); ++i) ss.token_ms.push_back(w->tok_t[i] - w->tok_t[i - M_]);
     } else if (w->stage->spec().last()) {
       for (int r = 1; r < k; ++r)
@@ -1624,7 +1658,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
         kv_grant(i, pos + (int)chunk[i].size());
         drafted += (long)d.size();
         if (!wf) {
-        } else if (cpu_) {
+        } else if (wf->cpu) {
           std::memcpy(wf->stage->prompt_buf() + i * max_ctx_ + pos, chunk[i].data(), chunk[i].size() * 4);
         } else {
           HIP_OK(hipSetDevice(wf->device));
@@ -1650,7 +1684,7 @@ Json Engine::spec_generate(const std::vector<std::vector<int32_t>>& prompts, int
     if (wl) {
       size_t off = 0;
       for (const Item& it : items) {
-        if (!cpu_) HIP_OK(hipSetDevice(wl->device));
+        if (!wl->cpu) HIP_OK(hipSetDevice(wl->device));
         wl->stage->copy_verify_tokens(it.mb, all.data() + off, it.T);
         off += (size_t)it.T;
       }
@@ -1728,7 +1762,7 @@ int Engine::copy_logits(int mb, float* out, int rows) {
   (void)mb;
   for (auto& w : workers_)
     if (w->stage->spec().last()) {
-      if (cpu_) {
+      if (w->cpu) {
         for (int r = 0; r < rows; ++r)
           std::memcpy(out + (size_t)r * cfg_.vocab, w->stage->logits_ptr() + (size_t)r * w->stage->logits_ld(),
                       (size_t)cfg_.vocab * 4);
@@ -1757,7 +1791,7 @@ Json Engine::info() const {
   }
   j["kv_free_pages"] = pager_.free_pages();
   j["mode"] = mode_;
-  j["backend"] = cpu_ ? "cpu" : "hip";
+  j["backend"] = cpu_ ? "cpu" : hybrid_ ? "hybrid" : "hip";
   j["load_ms"] = load_ms_;
   Json st = Json::array();
   for (auto& s : specs_) {

@@ -133,6 +133,7 @@ class Engine {
     hipEvent_t tr_base = nullptr;
     double tr_base_ms = 0;
     int device = 0;
+    bool cpu = false;   // CpuStage (backend "cpu", or the host stage of a hybrid -ngl split)
     // act_dtype != f32: per micro-batch device staging of the 2-byte wire format
     std::vector<void*> wire_out, wire_in;
   };
@@ -165,7 +166,9 @@ class Engine {
   std::vector<std::vector<int32_t>> gen_;          // generated tokens per sequence
   int32_t* out_host_ = nullptr;                    // pinned [rounds_cap][M*B]
   std::vector<int32_t> out_vec_;                   // CPU backend storage of out_host_
-  bool cpu_ = false;
+  bool cpu_ = false;          // every stage on the CPU backend
+  bool hybrid_ = false;       // gpu_layers (-ngl N) < n_layer: stage 0 on the CPU, the rest on GPUs
+  bool stage_cpu(int s) const { return cpu_ || (hybrid_ && s == 0); }
   bool kv_fp8_ = false;      // kv_dtype "fp8" (checkpoint fingerprint: the KV bytes' element type)
   bool trace_ = false, failed_ = false;
   bool packed_prefill_ = true;   // several sequences per prefill chunk (config "packed_prefill")

@@ -288,8 +288,17 @@ void TcpLink::recv(void* buf, size_t bytes, hipStream_t st) {
 namespace mp {
 
 // ---------------------------------------------------------------- HostLink
-void HostLink::send(const void* buf, size_t bytes, hipStream_t) {
-  std::vector<uint8_t> m((const uint8_t*)buf, (const uint8_t*)buf + bytes);
+// A stream means a GPU end (the hybrid CPU/GPU split): buf is device memory, copied through the
+// host message on that stream (blocking the caller's host thread, like a CPU stage's transfers).
+void HostLink::send(const void* buf, size_t bytes, hipStream_t st) {
+  std::vector<uint8_t> m;
+  if (st) {
+    m.resize(bytes);
+    HIP_OK(hipMemcpyAsync(m.data(), buf, bytes, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  } else {
+    m.assign((const uint8_t*)buf, (const uint8_t*)buf + bytes);
+  }
   std::unique_lock<std::mutex> l(mu_);
   if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || q_.size() < max_q_; }))
     throw std::runtime_error("HostLink: send timed out (peer stalled)");
@@ -300,15 +309,24 @@ void HostLink::send(const void* buf, size_t bytes, hipStream_t) {
   cv_.notify_all();
 }
 
-void HostLink::recv(void* buf, size_t bytes, hipStream_t) {
-  std::unique_lock<std::mutex> l(mu_);
-  if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !q_.empty(); }))
-    throw std::runtime_error("HostLink: recv timed out (peer stalled)");
-  if (aborted_) throw std::runtime_error("HostLink: aborted");
-  if (q_.front().size() != bytes) throw std::runtime_error("HostLink: message size mismatch");
-  std::memcpy(buf, q_.front().data(), bytes);
-  q_.pop_front();
-  cv_.notify_all();
+void HostLink::recv(void* buf, size_t bytes, hipStream_t st) {
+  std::vector<uint8_t> m;
+  {
+    std::unique_lock<std::mutex> l(mu_);
+    if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || !q_.empty(); }))
+      throw std::runtime_error("HostLink: recv timed out (peer stalled)");
+    if (aborted_) throw std::runtime_error("HostLink: aborted");
+    if (q_.front().size() != bytes) throw std::runtime_error("HostLink: message size mismatch");
+    m = std::move(q_.front());
+    q_.pop_front();
+    cv_.notify_all();
+  }
+  if (st) {
+    HIP_OK(hipMemcpyAsync(buf, m.data(), bytes, hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+  } else {
+    std::memcpy(buf, m.data(), bytes);
+  }
 }
 
 void HostLink::abort() {

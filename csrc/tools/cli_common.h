@@ -20,7 +20,7 @@ struct CliOptions {
   Json eng = Json::object();  // engine config
   std::string prompt = "Once upon a time";
   int n_predict = 200;        // reference: -n 200 (main.rs:44)
-  int ngl = 99;               // reference: -ngl 99 (main.rs:50); 0 = CPU backend
+  int ngl = 99;               // reference: -ngl 99 (main.rs:50); 0 = CPU backend; < n_layer: hybrid
   bool verbose = false;
   bool echo_prompt = true;
   bool bench = false;
@@ -82,7 +82,8 @@ inline void print_common_usage(FILE* f) {
           "  --draft-max K             speculative decoding by prompt lookup: up to K drafted tokens per\n"
           "                            verify round (greedy; --lookup-ngram N, default 3)\n"
           "placement / pipeline:\n"
-          "  -ngl, --n-gpu-layers N    0 = CPU backend, otherwise all layers on GPUs (default 99)\n"
+          "  -ngl, --n-gpu-layers N    layers offloaded to the GPU stages (default 99 = all); 0 = CPU backend;\n"
+          "                            0 < N < n_layer: the first n_layer - N layers run on a CPU stage in front\n"
           "  --stages N, --pp N        pipeline stages (one GPU each)\n"
           "  --devices 0,1,..          GPU of each stage (repeat a GPU to emulate PP on one device)\n"
           "  --micro-batches M         micro-batches in flight;  --mb-size B sequences per micro-batch\n"
@@ -176,6 +177,7 @@ inline CliOptions parse_cli(int argc, char** argv,
   if (!synthetic.empty()) e["synthetic"] = synthetic_arch(synthetic);
   if (!e.has("gguf") && !e.has("synthetic")) throw std::runtime_error("need -m FILE or --synthetic NAME");
   if (o.ngl == 0) e["backend"] = "cpu";
+  else if (o.ngl > 0) e["gpu_layers"] = o.ngl;   // >= n_layer: every layer on the GPUs
   if (stages > 0) e["stages"] = stages;
   if (!devices.empty()) {
     Json d = Json::array();

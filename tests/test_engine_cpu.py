@@ -550,3 +550,11 @@ def test_fp8_kv_needs_hip_backend(native, model_dir):
         Engine(gguf=path, backend="cpu", max_ctx=128, kv_dtype="fp8")
     with pytest.raises(RuntimeError, match="kv_dtype must be"):
         Engine(gguf=path, backend="cpu", max_ctx=128, kv_dtype="int4")
+
+
+def test_hybrid_split_needs_local_mode(model_dir):
+    """gpu_layers < n_layer (a CPU stage in front of the GPU stages) is a single-process layout."""
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
+    with pytest.raises(Exception, match="needs mode local"):
+        Engine(gguf=path, max_ctx=64, mode="mp", world=2, rank=0, gpu_layers=2)
