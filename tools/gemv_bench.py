@@ -84,11 +84,12 @@ def main():
                     name, vals = kv.split("=", 1)
                     knobs = [k + [(name, int(v))] for k in knobs for v in vals.split(",")]
                 for tpw, g3, kn in [(int(t), g, k) for t in a.tpw.split(",") for g in a.g3.split(";") for k in knobs]:
-                    for name, v in kn:
-                        N.check(L.mp_set_knob(name.encode(), v), "set_knob")
                     L.mp_set_gemv_tpw(tpw)
                     bm, bn, g3s = [int(v) for v in g3.split(",")]
+                    # (0 arguments reset GEMM3_BM / BN / SPLIT to their defaults: --knob values go after)
                     L.mp_set_gemm3_tuning(bm, bn, g3s, 0)
+                    for name, v in kn:
+                        N.check(L.mp_set_knob(name.encode(), v), "set_knob")
                     waves = (ntiles + max(tpw, 1) - 1) // max(tpw, 1)
                     if a.gemm or epi == EPI_SWIGLU or (epi != EPI_ATOMIC and a.splits == "auto"):
                         splits = [1]
