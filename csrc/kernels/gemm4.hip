@@ -277,7 +277,9 @@ struct G4Geom {
   static constexpr int A_INSTR = (NP + NWV - 1) / NWV;        // per wave (uniform: vmcnt accounting)
 };
 
-// FL (compile-time flags): bits 0-1 LDS-DMA spread mode, bit 2 non-temporal weights.  Compile-time
+// FL (compile-time flags): bits 0-1 LDS-DMA spread mode, bit 2 non-temporal weights; bits 3-5 timing
+// probes (probe builds only, wrong results): 3 raw bits as B fragments (no dequant VALU), 4 no MFMAs
+// (operands kept live), 5 no LDS-DMA (the stage images keep stale bytes).  Compile-time
 // because every weight DMA of a stage branched on them at run time: the 2-stage loop body of the MoE
 // gate/up kernel carried 485 scalar instructions (36 of them 64-bit compares, 44 s_nop) against 32
 // MFMAs.
@@ -292,6 +294,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   using Q3 = W3<PT>;
   using Q = W4<PT>;
   using G = G4Geom<PT, BM, NWV, TW>;
+  constexpr bool PR_NODQ = (FL & 8) != 0, PR_NOMMA = (FL & 16) != 0, PR_NODMA = (FL & 32) != 0;
   constexpr int NB = G::NB, FR = BM / 32, BN = 16 * TW * NWV;
   constexpr bool BF = PT == P_BF16;
   static_assert(NB >= 3 && NB <= 5, "gemm4: 3-5 stage buffers");
@@ -350,11 +353,13 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   }
   const uint8_t* const xbase = reinterpret_cast<const uint8_t*>(p.X);
   auto issue_a = [&](int s, int b) {
+    if constexpr (PR_NODMA) return;
     const uint8_t* sb = uniform_ptr(xbase + (size_t)s * 128);
 #pragma unroll
     for (int i = 0; i < G::A_INSTR; ++i) glds_s<16>(false, sb, xoff[i], stage_a(b) + apc[i] * 1024);
   };
   auto issue_a1 = [&](int i, int s, int b) {
+    if constexpr (PR_NODMA) return;
     const uint8_t* sb = uniform_ptr(xbase + (size_t)s * 128);
 #pragma unroll
     for (int ii = 0; ii < G::A_INSTR; ++ii)
@@ -374,6 +379,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
     Q3::template issue<TW>(smem, c0, EmitRecord<NIB>{Wbase, lane, boff, boff0});
   }
   auto issue_b = [&](int s, int b) {
+    if constexpr (PR_NODMA) return;
     src.sb = s / 4; src.q = s % 4;
     Q3::template issue<TW>(stage_r(b), src, EmitSaddr<NIB>{src.nt, lane, boff, boff0});
   };
@@ -404,6 +410,22 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   static_assert(JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
   using RawT = typename Q::Raw;
   using PrepT = typename Q::Prep;
+  // probes: a raw dword / raw fragment instead of the dequantized one
+  struct RawDw { uint32_t d[sizeof(RawT) / 4]; };
+  auto raw_dw = [&](const RawT& w, int k) { return __builtin_bit_cast(RawDw, w).d[k % (sizeof(RawT) / 4)]; };
+  auto fragx = [&](const RawT& w, const PrepT& prp, int t) -> half8_t {
+    if constexpr (PR_NODQ) {
+      const u32x4 u = {raw_dw(w, t), raw_dw(w, t + 1), raw_dw(w, t + 2), raw_dw(w, t + 3)};
+      return __builtin_bit_cast(half8_t, u);
+    } else {
+      return Q::frag(w, prp, t, h, kc);
+    }
+  };
+  auto fragpx = [&](auto pc, const RawT& w, const PrepT& prp, int t) -> uint32_t {
+    constexpr int P = decltype(pc)::value;
+    if constexpr (PR_NODQ) return raw_dw(w, t + P);
+    else return Q::template fragp<P>(w, prp, t, h, kc);
+  };
   RawT raw[NPR];
   PrepT pr[NPR];
   half8_t bf[NPR][4];
@@ -430,7 +452,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 #pragma unroll
   for (int pp = 0; pp < NPR; ++pp) {
     pr[pp] = Q::prep(raw[pp], s_begin & 3);
-    bf[pp][0] = Q::frag(raw[pp], pr[pp], 0, h, kc);
+    bf[pp][0] = fragx(raw[pp], pr[pp], 0);
   }
 
   // One stage.  LAST (the split's final stage, compile-time) issues nothing for a next stage: no
@@ -453,7 +475,10 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
       if (i == 0 || !MOE || i < fr_live) {
         const half8_t a = x_op<BF>(__builtin_bit_cast(half8_t, af[j]));
 #pragma unroll
-        for (int pp = 0; pp < NPR; ++pp) acc[i][pp] = mma32<BF>(a, bf[pp][t], acc[i][pp]);
+        for (int pp = 0; pp < NPR; ++pp) {
+          if constexpr (PR_NOMMA) asm volatile("" :: "v"(a), "v"(bf[pp][t]));
+          else acc[i][pp] = mma32<BF>(a, bf[pp][t], acc[i][pp]);
+        }
       }
       if constexpr (j + AD < NA) read_a(std::integral_constant<int, j + AD>{}, af[j + AD], b);
       // B fragment t + 1, behind the first MFMAs of fragment t (its last use of the previous
@@ -464,12 +489,12 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
           constexpr int P = decltype(pc)::value;
           if constexpr (i == (FR >= 4 ? P : P / 2)) {
 #pragma unroll
-            for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][t + 1], Q::template fragp<P>(raw[pp], pr[pp], t + 1, h, kc));
+            for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][t + 1], fragpx(pc, raw[pp], pr[pp], t + 1));
           }
         });
       } else if constexpr (i == IB && t < 3) {
 #pragma unroll
-        for (int pp = 0; pp < NPR; ++pp) bf[pp][t + 1] = Q::frag(raw[pp], pr[pp], t + 1, h, kc);
+        for (int pp = 0; pp < NPR; ++pp) bf[pp][t + 1] = fragx(raw[pp], pr[pp], t + 1);
       }
       if constexpr (!LAST) {
         if constexpr (j == JB) {
@@ -499,13 +524,13 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
 #pragma unroll
           for (int pp = 0; pp < NPR; ++pp) {   // (bf[.][0] of stage s: last use at j = FR - 1)
             pr_n[pp] = Q::prep(raw_n[pp], (s + 1) & 3);
-            if constexpr (!split0) bf[pp][0] = Q::frag(raw_n[pp], pr_n[pp], 0, h, kc);
+            if constexpr (!split0) bf[pp][0] = fragx(raw_n[pp], pr_n[pp], 0);
           }
         }
         if constexpr (split0 && j > JP && j <= JP + 4) {
           constexpr int P = j - JP - 1;
 #pragma unroll
-          for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][0], Q::template fragp<P>(raw_n[pp], pr_n[pp], 0, h, kc));
+          for (int pp = 0; pp < NPR; ++pp) set_dw<P>(bf[pp][0], fragpx(std::integral_constant<int, P>{}, raw_n[pp], pr_n[pp], 0));
         }
       }
     });
@@ -611,6 +636,22 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   const dim3 grid(n_cg * n_mb, nsplit, E), block(64 * NWV);
 #define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F, TW>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
 #ifdef MIPIPE_TIMING_PROBES
+  // timing probes (knob GEMM4_PROBE): Q4_K dense gate/up (SwiGLU, 256 rows) and split-K stores
+  if constexpr (PT == P_Q4_K && !MOE && ((EPI == EPI_SWIGLU && BM == 256) || (EPI == EPI_STORE && BM == 128))) {
+    const int pk = knob(KNOB_GEMM4_PROBE);
+    if (pk) {
+      const int w4 = wnt ? 4 : 0;
+      switch (pk) {
+        case 1: if (w4) G4_LAUNCH(4 | 8); else G4_LAUNCH(8); return;
+        case 2: if (w4) G4_LAUNCH(4 | 16); else G4_LAUNCH(16); return;
+        case 3: if (w4) G4_LAUNCH(4 | 24); else G4_LAUNCH(24); return;
+        case 4: if (w4) G4_LAUNCH(4 | 32); else G4_LAUNCH(32); return;
+        case 5: if (w4) G4_LAUNCH(4 | 40); else G4_LAUNCH(40); return;
+        case 6: if (w4) G4_LAUNCH(4 | 48); else G4_LAUNCH(48); return;
+        default: if (w4) G4_LAUNCH(4 | 56); else G4_LAUNCH(56); return;
+      }
+    }
+  }
   // the LDS-DMA spread schedules (knob GEMM4_SPREAD, measured no faster: PERFORMANCE.md) exist in
   // the probe build only
   switch (knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0)) {

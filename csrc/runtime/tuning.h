@@ -43,6 +43,7 @@ enum Knob : int {
   // default library, so no environment variable can corrupt a serving or bench run
   KNOB_GEMM3_PROBE,         // gemm3 timing probes (Q4_K SwiGLU 256x256 only; 0 = the real kernel)
   KNOB_ATTN_PROBE,          // decode attention timing probes (1: no V append, 2: no K append; 0 = real)
+  KNOB_GEMM4_PROBE,         // gemm4 timing probes (Q4_K, dense): bit 0 no dequant, 1 no MFMA, 2 no LDS-DMA
 #endif
   KNOB_COUNT
 };
