@@ -287,7 +287,7 @@ struct G4Geom {
 // share every A fragment; the 64-row MoE tile, where 32-column waves left half the MFMAs of a
 // 128-row tile on padding rows)
 template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0, int TW = 2>
-__global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
+__global__ __launch_bounds__(64 * NWV) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages, const G4Moe mo) {
   static_assert(TW == 2 || TW == 4, "gemm4: 2 or 4 tiles per wave");
   constexpr int NPR = TW / 2;   // 32-column pairs per wave
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemvParams p, const in
   constexpr int IB = FR >= 4 ? 1 : 0;
   static_assert(JB > FR / 2 && NA - AD > JB, "gemm4: barrier step");
   constexpr int JP = JB + 3 < NA - 2 ? JB + 3 : NA - 2;   // next stage's prep step (bf[.][0] of this stage: last use at FR - 1 < JB)
-  static_assert(JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
+  static_assert((FL & 3) == 0 || JB + G::A_INSTR + 2 < NA, "gemm4: the spread LDS-DMA issue must end inside the stage");
   using RawT = typename Q::Raw;
   using PrepT = typename Q::Prep;
   // probes: a raw dword / raw fragment instead of the dequantized one
@@ -698,6 +698,11 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  } else if ((knob(KNOB_GEMM4_TW4) == 1 && bm == 256) || (knob(KNOB_GEMM4_TW4) == 2 && bm >= 128)) {
+    // 4 waves of 64 columns (one per SIMD): every A fragment read from LDS feeds two MFMAs (half the
+    // LDS A traffic of 8 waves x 32 columns); the same 256-column workgroup tile and grid
+    if (bm == 128) gemm4_go<PT, EPI, 128, false, 4, 4>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 256, false, 4, 4>(p, nsplit, st);
   } else if (bm == 64) {   // 60 KB of LDS: two workgroups per CU
     if (nw7) gemm4_go<PT, EPI, 64, false, 7>(p, nsplit, st);
     else gemm4_go<PT, EPI, 64>(p, nsplit, st);
