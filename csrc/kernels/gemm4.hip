@@ -698,7 +698,7 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
-  } else if ((knob(KNOB_GEMM4_TW4) == 1 && bm == 256) || (knob(KNOB_GEMM4_TW4) == 2 && bm >= 128)) {
+  } else if (((knob(KNOB_GEMM4_TW4) & 1) && bm == 256) || (knob(KNOB_GEMM4_TW4) == 2 && bm >= 128)) {
     // 4 waves of 64 columns (one per SIMD): every A fragment read from LDS feeds two MFMAs (half the
     // LDS A traffic of 8 waves x 32 columns); the same 256-column workgroup tile and grid
     if (bm == 128) gemm4_go<PT, EPI, 128, false, 4, 4>(p, nsplit, st);
@@ -810,7 +810,8 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
     // the down projection unsplit: Mixtral at 256 tokens 10225-10246 vs 10091-10093 tok/s with the
     // 2 K splits that fill the 256 CUs (half the float atomics into the residual; r9i)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot && knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : 1;
-    gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
+    if (knob(KNOB_GEMM4_TW4) == 3) gemm4_go<PT, EPI, 128, true, 4, 4>(p, ns, st, mo, q.E);   // 4 waves x 64 columns
+    else gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
   } else {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 255) / 256), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 256, true>(p, ns, st, mo, q.E);
