@@ -287,7 +287,7 @@ struct G4Geom {
 // share every A fragment; the 64-row MoE tile, where 32-column waves left half the MFMAs of a
 // 128-row tile on padding rows)
 template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0, int TW = 2>
-__global__ __launch_bounds__(64 * NWV) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 && TW == 2 ? 2 : 1))) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages, const G4Moe mo) {
   static_assert(TW == 2 || TW == 4, "gemm4: 2 or 4 tiles per wave");
   constexpr int NPR = TW / 2;   // 32-column pairs per wave
@@ -680,6 +680,11 @@ static int g4_bm(int ptype, int M, int ntiles) {
   return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;
 }
 
+// workgroups resident per CU: 2 for the 64-row tiles and for 4-wave 128-row tiles (GEMM4_NW=4)
+static int g4_per_cu(int ptype, int bm) {
+  return bm == 64 || (bm == 128 && !is16(ptype) && knob(KNOB_GEMM4_NW) == 4) ? 2 : 1;
+}
+
 // compute waves per workgroup for an unsplit launch: 7 (224 columns) when that fills more of the
 // 256 CUs in whole rounds (70B gate/up at M = 256: 224 -> 256 workgroups), else 8; knob GEMM4_NW
 static int g4_nwv(int ntiles, int n_mb) {
@@ -707,7 +712,10 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
     if (nw7) gemm4_go<PT, EPI, 64, false, 7>(p, nsplit, st);
     else gemm4_go<PT, EPI, 64>(p, nsplit, st);
   } else if (bm == 128) {
-    if (nw7) gemm4_go<PT, EPI, 128, false, 7>(p, nsplit, st);
+    // GEMM4_NW=4: 4 waves x 32 columns (64 KB of LDS, <= 256 registers): two independent workgroups
+    // per CU, so one's stage barrier and DMA waits overlap the other's MFMAs
+    if (knob(KNOB_GEMM4_NW) == 4) gemm4_go<PT, EPI, 128, false, 4>(p, nsplit, st);
+    else if (nw7) gemm4_go<PT, EPI, 128, false, 7>(p, nsplit, st);
     else gemm4_go<PT, EPI, 128>(p, nsplit, st);
   } else {
     if (nw7) gemm4_go<PT, EPI, 256, false, 7>(p, nsplit, st);
@@ -722,11 +730,12 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
     return false;
   } else {
     const int bm = g4_bm(PT, p.M, p.ntiles);
-    const int wgs = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
+    const int tpc = g4_per_cu(PT, bm) == 2 && bm == 128 ? 8 : 16;   // T16 tiles per column group
+    const int wgs = (p.ntiles + tpc - 1) / tpc * ((p.M + bm - 1) / bm);
     const int n_stages = p.nsb * 4;
     int ns = 1;
     if (scratch) {   // split-K partial stores: split s writes scratch + s * M * ldp
-      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(PT, bm));
       const int per = (n_stages + ns - 1) / ns;
       ns = (n_stages + per - 1) / per;
       const int ldp = p.ntiles * 16;
@@ -737,7 +746,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
       return true;
     }
     if (epi == EPI_ATOMIC && allow_split)
-      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(PT, bm));
     switch (epi) {
       case EPI_STORE: gemm4_bm<PT, EPI_STORE>(p, 1, st); break;
       case EPI_ATOMIC: gemm4_bm<PT, EPI_ATOMIC>(p, ns, st); break;
@@ -763,9 +772,10 @@ static bool gemm4_dispatch(int ptype, int epi, const GemvParams& p, bool allow_s
 int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
   if (!gemm4_supported(ptype)) return 1;
   const int bm = g4_bm(ptype, M, ntiles);
-  const int wgs = (ntiles + 15) / 16 * ((M + bm - 1) / bm);
+  const int tpc = g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;
+  const int wgs = (ntiles + tpc - 1) / tpc * ((M + bm - 1) / bm);
   const int n_stages = nsb * 4;
-  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, bm == 64 ? 2 : 1);
+  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(ptype, bm));
   ns = std::max(1, std::min(ns, n_stages));
   const int per = (n_stages + ns - 1) / ns;
   return (n_stages + per - 1) / per;

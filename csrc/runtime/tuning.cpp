@@ -22,7 +22,7 @@ bool ns_ok(int v) { return v == 2 || v == 3 || v == 4; }
 bool nw_ok(int v) { return v == 4 || v == 8; }
 bool g_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; }
 bool bm_ok(int v) { return v == 0 || v == 128 || v == 256; }
-bool nw4_ok(int v) { return v == 0 || v == 7 || v == 8; }
+bool nw4_ok(int v) { return v == 0 || v == 4 || v == 7 || v == 8; }
 
 const KnobDef kDefs[KNOB_COUNT] = {
     {"ATTN_PF_MAXWG", 512, 0, 1 << 30, nullptr},   // r7v: mb256 np 61.3 vs PF 65.3 us/layer

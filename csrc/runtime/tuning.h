@@ -27,7 +27,8 @@ enum Knob : int {
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
   KNOB_ATTN_WAVE,           // decode attention: the wave-per-item kernel (0 off, 1 on, 2 auto)
   KNOB_ATTN_WAVE_MIN,       // auto: (token, kv head, split) items at or above which it is taken
-  KNOB_GEMM4_NW,            // gemm4: compute waves per workgroup of unsplit launches (0 auto, 7, 8)
+  KNOB_GEMM4_NW,            // gemm4: compute waves per workgroup of unsplit launches (0 auto, 7, 8; 4 = 128-row
+                            // tiles of 4 waves, two workgroups per CU, split-K included)
   KNOB_GEMM4_SPREAD,        // gemm4: LDS-DMA issue after the stage barrier (0 burst, 1 spread over MFMA steps, 2 spread + waves 4-7 two steps later)
   KNOB_GEMM4_WNT,           // gemm4: non-temporal LDS-DMA of the weights (0 auto: one row block per column group, 1 on, 2 off)
   KNOB_GEMM4_MOE64,         // gemm4 MoE mode: 64-row tiles when the mean rows per expert <= 64 (0 / 1)
