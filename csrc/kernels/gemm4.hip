@@ -550,6 +550,11 @@ __global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV ==
     stage(F_{}, s + 1, b, afB, af, rawB, raw, prB, pr);
     b = b + 1 == NB ? 0 : b + 1;
   }
+  // every LDS read retired BEFORE the even / odd exits join: with the accumulators in AGPRs (TW = 4)
+  // the register allocator puts their AGPR -> VGPR copies for the epilogue at the top of the join
+  // block, ahead of a wait placed there -- onto the destinations of the even exit's dead
+  // next-stage reads (tools/isa_lint.py "clobber").  (The odd tail over-waits for its first reads.)
+  wait_lgkm<0>();
   if (s < s_end) stage(T_{}, s, b, af, afB, raw, rawB, pr, prB);
   wait_vmcnt<0>();   // the clamped tail loads: drained before the workgroup's LDS is released
   wait_lgkm<0>();
