@@ -42,7 +42,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
     {"ATTN_WAVE", 2, 0, 2, nullptr},
-    {"ATTN_WAVE_MIN", 1024, 1, 1 << 30, nullptr},
+    {"ATTN_WAVE_MIN", 512, 1, 1 << 30, nullptr},   // r10ac: mb64 at 8 kv heads (512 items) +2.5-3 %, mb32 (256) -2.3 %
     {"GEMM4_NW", 0, 0, 8, nw4_ok},
     {"GEMM4_SPREAD", 0, 0, 2, nullptr},
     {"GEMM4_WNT", 0, 0, 2, nullptr},

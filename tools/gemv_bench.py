@@ -19,7 +19,7 @@ SHAPES = {  # name: (N, K, epi)
     "8b.qkv": (6144, 4096, EPI_ATOMIC), "8b.o": (4096, 4096, EPI_ATOMIC),
     "8b.gateup": (28672, 4096, EPI_SWIGLU), "8b.down": (4096, 14336, EPI_ATOMIC),
 }
-TYPES = {"Q4_K": Q.Q4_K, "Q6_K": Q.Q6_K, "Q8_0": Q.Q8_0, "Q5_K": Q.Q5_K, "F16": Q.F16}
+TYPES = {"Q4_K": Q.Q4_K, "Q6_K": Q.Q6_K, "Q8_0": Q.Q8_0, "Q5_K": Q.Q5_K, "F16": Q.F16, "BF16": Q.BF16}
 
 
 def main():
