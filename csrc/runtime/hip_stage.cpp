@@ -513,6 +513,10 @@ void HipStage::alloc_runtime() {
     auto acc = [&](const PackedMat& m) {
       if (!m.d || is16(m.ptype)) return;
       for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
+        if (M > 4 && M <= 64 && knob(KNOB_GEMV_SKSTORE)) {   // the GEMV's partial stores (gemv)
+          const int ns = det_splits((int)m.dims.ntiles, (int)m.dims.nsb, M, EPI_ATOMIC);
+          if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
+        }
         if (M <= (knob(KNOB_GEMM4_M64) ? 32 : 64)) continue;
         int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
         if (opt_.prefill_gemm_v == 4 || opt_.prefill_gemm_v == 0)
@@ -823,6 +827,21 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     p.n_valid = n_valid;
     const int nsplit = allow_split ? gemv_auto_split(p.ntiles, p.nsb, p.M, epi) : 1;
     const int ns = det_splits(p.ntiles, p.nsb, p.M, epi, allow_split);
+    // split-K through per-split partial stores instead of float atomics (knob GEMV_SKSTORE; 5-64
+    // rows, one slice): the o / down partials go to the next RMSNorm of x (norm_x), the qkv ones
+    // through one reduction -- the same scheme as the M > 64 GEMMs
+    if (!opt_.deterministic && knob(KNOB_GEMV_SKSTORE) && opt_.gemm_splitk_store && sk_part_ && epi == EPI_ATOMIC &&
+        ns > 1 && M <= 64 && !extras && (size_t)ns * p.M * p.ntiles * 16 <= sk_part_n_) {
+      const int ldp = p.ntiles * 16;
+      const bool defer = Y == sk_defer_;
+      flush_sk(st);   // the scratch is about to be overwritten
+      GemvParams q = p;
+      q.Y = sk_part_; q.ldy = ldp; q.split_stride = (int64_t)p.M * ldp;
+      launch_gemv(m.ptype, EPI_STORE, q, ns, st);
+      if (defer) sk_pend_ = SkPending{Y, p.M, n_valid, ldy, ns, ldp, (int64_t)p.M * ldp};
+      else launch_splitk_reduce(sk_part_, ns, (int64_t)p.M * ldp, ldp, p.M, n_valid, p.Y, ldy, st);
+      continue;
+    }
     if (opt_.deterministic && epi == EPI_ATOMIC && ns > 1) {
       // split s stores its partial to det_part_[s]; then one fixed-order reduction adds them into Y
       const int ldp = p.ntiles * 16;

@@ -52,6 +52,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
     {"GEMVS_CHAIN", 0, 0, 1, nullptr},
     {"GEMM4_M64", 0, 0, 1, nullptr},
+    {"GEMV_SKSTORE", 0, 0, 1, nullptr},
     {"GEMM4_TW4", 1, 0, 3, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
     {"PREFETCH", 0, 0, 4096, nullptr},
 #ifdef MIPIPE_TIMING_PROBES

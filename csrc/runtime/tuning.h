@@ -37,6 +37,8 @@ enum Knob : int {
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
   KNOB_GEMVS_CHAIN,         // single stream: o -> gate/up -> down as one chained launch (0 / 1)
   KNOB_GEMM4_M64,           // decode micro-batches of 33-64 rows on gemm4's 64-row tiles instead of the GEMV (0 / 1)
+  KNOB_GEMV_SKSTORE,        // decode GEMV at 5-64 rows: split-K partial stores + the next norm's reduction instead of
+                            // atomics (0 / 1; r10af: 8B mb64 +2 %, 70B mb16-32 -6-8 %)
   KNOB_GEMM4_TW4,           // gemm4 dense: 4 waves x 64 columns (two MFMAs per A fragment) instead of 8 x 32
                             // (0 off, 1 the 256-row tiles only, 2 also the 128-row tiles, 3 = 1 + the 128-row MoE tiles)
   KNOB_PREFETCH,            // single stream: side-stream MALL prefetch of each layer's o / gate-up / down and the next
