@@ -306,6 +306,14 @@ int mp_set_knob(const char* name, int value) {
   API_CATCH(-1)
 }
 
+// back to the knob's MIPIPE_* environment value, else its default
+int mp_reset_knob(const char* name) {
+  API_TRY
+  reset_knob(name);
+  return 0;
+  API_CATCH(-1)
+}
+
 int mp_op_gemv(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
                int ldy, void* H, int ldh, int n_valid, int nsplit, void* stream) {
   API_TRY

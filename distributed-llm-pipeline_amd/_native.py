@@ -66,6 +66,7 @@ _SIGS = {
     "mp_op_gemm3_i8": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                         c_void_p, c_void_p, c_int, c_void_p], c_int),
     "mp_set_knob": ([c_char_p, c_int], c_int),
+    "mp_reset_knob": ([c_char_p], c_int),
     "mp_op_unpack": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_rmsnorm": ([c_void_p, c_int, c_void_p, c_int, c_float, c_void_p, c_int, c_int, c_void_p], c_int),
     "mp_op_embed": ([c_int, c_void_p, c_int64, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),

@@ -173,6 +173,39 @@ def test_gemm4_seven_wave_tiles(cuda, native, qt, nw, M):
         N.lib().mp_set_knob(b"GEMM4_NW", 0)
 
 
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
+@pytest.mark.parametrize("form", ["tw4", "nw4"])
+@pytest.mark.parametrize("k", [2048, 2304])
+@pytest.mark.parametrize("M", [65, 256])
+def test_gemm4_four_wave_tiles(cuda, tuning, qt, form, k, M):
+    """The 4-wave forms on every tile: 64 columns per wave with the accumulators in AGPRs
+    (GEMM4_TW4=2; the AGPR -> VGPR epilogue copies once landed on in-flight LDS reads at the loop's
+    even exit) and 32 columns per wave at two workgroups per CU (GEMM4_NW=4).  An even (32) and an
+    odd (36) stage count, STORE / SwiGLU / split-K ATOMIC over a non-zero residual."""
+    from mipipe import _native as N
+    from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
+    name, val = (b"GEMM4_TW4", 2) if form == "tw4" else (b"GEMM4_NW", 4)
+    N.check(N.lib().mp_set_knob(name, val), "knob")
+    try:
+        n = 640
+        raw, deq = _weights(qt, n, k, 900 + qt + M + k)
+        w = PackedWeight(raw, qt, n, k)
+        xh = _x(M, k, w.k_pad, M + 11)
+        ref = _ref(xh, k, deq, qt)
+        y = gemm(w, xh.cuda(), EPI_STORE, v=4)
+        assert torch.isfinite(y).all() and nmse(y.cpu(), ref) < 1e-5
+        h = gemm(w, xh.cuda(), EPI_SWIGLU, v=4)
+        gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
+        href = torch.nn.functional.silu(ref[:, gi]) * ref[:, gi + 8]
+        assert nmse(h.float().cpu(), href) < 1e-4
+        tuning(0, 0, 3, 0)   # 3 K splits: per-split stage counts 11 / 11 / 10 or 12 / 12 / 12
+        base = torch.randn(M, n)
+        y2 = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4)
+        assert nmse(y2.cpu() - base, ref) < 1e-5
+    finally:
+        N.lib().mp_reset_knob(name)
+
+
 def _ref_gpu(xh, k, deq, qt):
     """fp32 reference on the GPU (the 70B-width shapes are ~20 GFLOP each)."""
     xa = xh[:, :k].float()
