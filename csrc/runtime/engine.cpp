@@ -924,6 +924,7 @@ void Engine::write_trace(const std::string& path) const {
 Json Engine::health() const {
   Json j = Json::object();
   j["ok"] = !failed_;
+  j["backend"] = cpu_ ? "cpu" : hybrid_ ? "hybrid" : "hip";
   j["prefix_reused_tokens"] = (int64_t)reused_tokens_;
   if (failed_stage_ >= 0) {
     j["failed_stage"] = failed_stage_;
@@ -957,9 +958,13 @@ Json Engine::health() const {
 Json Engine::failover_config(const Json& cfg, const Json& health) {
   Json c = cfg;
   c["fault"] = Json::object();   // an injected fault does not follow the engine across a rebuild
-  const int S = cfg.get_int("stages", 1);
+  const int S = cfg.get_int("stages", 1);   // GPU stages (a hybrid split puts its CPU stage 0 in front)
   if (!health.has("failed_stage") || S <= 1 || cfg.get_str("mode", "local") == "mp") return c;
-  const int bad = health.get_int("failed_stage", 0);
+  int bad = health.get_int("failed_stage", 0);
+  if (health.get_str("backend", "") == "hybrid") {
+    if (bad == 0) return c;   // the CPU stage: rebuilt in place
+    bad -= 1;                 // index among the GPU stages
+  }
   Json devs = Json::array();
   if (cfg.has("devices") && cfg["devices"].is_arr() && !cfg["devices"].arr().empty()) {
     const auto& a = cfg["devices"].arr();
