@@ -642,7 +642,8 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
 #define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F, TW>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes (knob GEMM4_PROBE): Q4_K dense gate/up (SwiGLU, 256 rows) and split-K stores
-  if constexpr (PT == P_Q4_K && !MOE && ((EPI == EPI_SWIGLU && BM == 256) || (EPI == EPI_STORE && BM == 128))) {
+  if constexpr (PT == P_Q4_K && ((!MOE && ((EPI == EPI_SWIGLU && BM == 256) || (EPI == EPI_STORE && BM == 128))) ||
+                                 (MOE && EPI == EPI_SWIGLU && BM == 128 && NWV == 8))) {
     const int pk = knob(KNOB_GEMM4_PROBE);
     if (pk) {
       const int w4 = wnt ? 4 : 0;
@@ -659,12 +660,14 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   }
   // the LDS-DMA spread schedules (knob GEMM4_SPREAD, measured no faster: PERFORMANCE.md) exist in
   // the probe build only
-  switch (knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0)) {
-    case 1: G4_LAUNCH(1); return;
-    case 2: G4_LAUNCH(2); return;
-    case 5: G4_LAUNCH(5); return;
-    case 6: G4_LAUNCH(6); return;
-    default: break;
+  if constexpr (NWV >= 7) {   // (the 4-wave forms issue more DMA per wave than a stage's spread slots)
+    switch (knob(KNOB_GEMM4_SPREAD) | (wnt ? 4 : 0)) {
+      case 1: G4_LAUNCH(1); return;
+      case 2: G4_LAUNCH(2); return;
+      case 5: G4_LAUNCH(5); return;
+      case 6: G4_LAUNCH(6); return;
+      default: break;
+    }
   }
 #endif
   if (wnt) G4_LAUNCH(4);
