@@ -4,7 +4,8 @@
     out, stats = eng.generate([[1, 15, 27], [1, 99]], n_predict=32)
 
 Config keys mirror the C++ Engine (see engine.h): gguf | synthetic+ftype, mode ("local" or "mp"),
-stages, devices, link ("local" | "rccl" | "tcp"), backend ("hip" | "cpu"), n_mb, mb_size, max_ctx,
+stages, devices, link ("local" | "rccl" | "tcp"), backend ("hip" | "cpu"), gpu_layers (llama-cli -ngl N:
+0 < N < n_layer puts the first n_layer - N layers on a CPU stage in front of the GPU stages), n_mb, mb_size, max_ctx,
 prefill_chunk, split ("even" | "mem" | "cost"), graphs, fused_attn, prefill_gemm, attn_split_len,
 temp/top_k/top_p/min_p/seed (sampling; llama.cpp chain order), repeat_penalty/repeat_last_n/
 frequency_penalty/presence_penalty (penalties over the last n tokens, prompt included), world/rank/hosts/next_host/base_port/rccl_ids (mp mode),
