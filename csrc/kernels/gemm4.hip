@@ -829,6 +829,7 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
     // 2 K splits that fill the 256 CUs (half the float atomics into the residual; r9i)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot && knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : 1;
     if (knob(KNOB_GEMM4_TW4) == 3) gemm4_go<PT, EPI, 128, true, 4, 4>(p, ns, st, mo, q.E);   // 4 waves x 64 columns
+    else if (knob(KNOB_GEMM4_NW) == 7) gemm4_go<PT, EPI, 128, true, 7>(p, ns, st, mo, q.E);   // 224-column tiles
     else gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
   } else {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 255) / 256), q.nsb * 4) : 1;
