@@ -15,6 +15,13 @@
 #include "pack.h"
 #include "qtypes.h"
 
+// host-only multiversioning (hipcc also runs a device pass over this file, which has no clones)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MP_HOST_AVX2_CLONES
+#else
+#define MP_HOST_AVX2_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+
 namespace mp {
 
 namespace {
@@ -242,6 +249,17 @@ void CpuStage::set_positions(int mb, const std::vector<int32_t>& pos) {
   for (size_t i = 0; i < pos.size() && i < pos_[mb].size(); ++i) pos_[mb][i] = pos[i];
 }
 
+// dot product with 8 fixed-order partial sums (one AVX2 vector; no FMA contraction in either clone, so
+// the AVX2 and baseline builds give the same bits)
+MP_HOST_AVX2_CLONES static float dot8(const float* w, const float* x, int64_t K) {
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t k = 0;
+  for (; k + 8 <= K; k += 8)
+    for (int j = 0; j < 8; ++j) s[j] += w[k + j] * x[k + j];
+  for (; k < K; ++k) s[0] += w[k] * x[k];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
 void CpuStage::matmul(const CpuMat& W, const float* X, int ldx, int M, float* Y, int ldy, bool accumulate) {
   const int64_t K = W.K;
   pool_->parallel_for(W.N, [&](int64_t n0, int64_t n1) {
@@ -249,14 +267,7 @@ void CpuStage::matmul(const CpuMat& W, const float* X, int ldx, int M, float* Y,
     for (int64_t n = n0; n < n1; ++n) {
       dequant_row(W.type, W.data + n * W.rb, w.data(), K);
       for (int m = 0; m < M; ++m) {
-        const float* x = X + (size_t)m * ldx;
-        float s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        int64_t k = 0;
-        for (; k + 4 <= K; k += 4) {
-          s0 += w[k] * x[k]; s1 += w[k + 1] * x[k + 1]; s2 += w[k + 2] * x[k + 2]; s3 += w[k + 3] * x[k + 3];
-        }
-        for (; k < K; ++k) s0 += w[k] * x[k];
-        const float s = (s0 + s1) + (s2 + s3);
+        const float s = dot8(w.data(), X + (size_t)m * ldx, K);
         float& y = Y[(size_t)m * ldy + n];
         y = accumulate ? y + s : s;
       }

@@ -6,6 +6,13 @@
 #include <thread>
 #include <vector>
 
+// host-only multiversioning (hipcc also runs a device pass over this file, which has no clones)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MP_HOST_AVX2_CLONES
+#else
+#define MP_HOST_AVX2_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+
 namespace mp {
 
 float f16_to_f32(uint16_t h) {
@@ -219,7 +226,9 @@ int pack_t16_tiles(int t, int64_t N, int64_t K, const RowFn& row, uint8_t* dst, 
   return pt;
 }
 
-void dequant_row(int t, const uint8_t* src, float* dst, int64_t K) {
+// (host code: an AVX2 clone chosen at load time where the CPU has it -- no FMA, so both clones round
+// alike -- and the baseline x86-64 one elsewhere)
+MP_HOST_AVX2_CLONES void dequant_row(int t, const uint8_t* src, float* dst, int64_t K) {
   switch (t) {
     case T_F32: std::memcpy(dst, src, K * 4); return;
     case T_F16: for (int64_t i = 0; i < K; ++i) dst[i] = f16_to_f32(rd16(src + 2 * i)); return;
@@ -242,14 +251,31 @@ void dequant_row(int t, const uint8_t* src, float* dst, int64_t K) {
       }
       return;
     case T_Q4_K: case T_Q5_K:
+      // per 64-element group: two sub-block scales hoisted out of the element loop (the same float
+      // arithmetic as the per-element form: (d * sc) * q - dmin * m)
       for (int64_t b = 0; b < K / 256; ++b) {
         const uint8_t* blk = src + (t == T_Q4_K ? 144 : 176) * b;
         const float d = f16_to_f32(rd16(blk)), dmin = f16_to_f32(rd16(blk + 2));
-        for (int w = 0; w < 256; ++w) {
-          int sc, m;
-          get_scale_min_k4(w / 32, blk + 4, sc, m);
-          const int q = t == T_Q4_K ? q4k_nib(blk, w) : q5k_val(blk, w);
-          dst[256 * b + w] = d * sc * q - dmin * m;
+        const uint8_t* __restrict__ qh = blk + 16;             // Q5_K high bits
+        const uint8_t* __restrict__ qs = blk + (t == T_Q4_K ? 16 : 48);
+        float* __restrict__ o = dst + 256 * b;   // (restrict: the byte loads may not alias the stores)
+        for (int c = 0; c < 4; ++c) {
+          int s0, m0, s1, m1;
+          get_scale_min_k4(2 * c, blk + 4, s0, m0);
+          get_scale_min_k4(2 * c + 1, blk + 4, s1, m1);
+          const float d0 = d * s0, n0 = dmin * m0, d1 = d * s1, n1 = dmin * m1;
+          const uint8_t* __restrict__ q = qs + 32 * c;
+          if (t == T_Q4_K) {
+            for (int l = 0; l < 32; ++l) {
+              o[64 * c + l] = d0 * (q[l] & 15) - n0;
+              o[64 * c + 32 + l] = d1 * (q[l] >> 4) - n1;
+            }
+          } else {
+            for (int l = 0; l < 32; ++l) {
+              o[64 * c + l] = d0 * ((q[l] & 15) | (((qh[l] >> (2 * c)) & 1) << 4)) - n0;
+              o[64 * c + 32 + l] = d1 * ((q[l] >> 4) | (((qh[l] >> (2 * c + 1)) & 1) << 4)) - n1;
+            }
+          }
         }
       }
       return;
@@ -258,7 +284,21 @@ void dequant_row(int t, const uint8_t* src, float* dst, int64_t K) {
         const uint8_t* blk = src + 210 * b;
         const float d = f16_to_f32(rd16(blk + 208));
         const int8_t* sc = reinterpret_cast<const int8_t*>(blk + 192);
-        for (int w = 0; w < 256; ++w) dst[256 * b + w] = d * sc[w / 16] * (float)(q6k_val(blk, w) - 32);
+        float* __restrict__ o = dst + 256 * b;
+        for (int n = 0; n < 2; ++n) {
+          const uint8_t* __restrict__ ql = blk + 64 * n;
+          const uint8_t* __restrict__ qh = blk + 128 + 32 * n;
+          for (int k = 0; k < 4; ++k) {
+            const int w0 = 128 * n + 32 * k;
+            const float ds0 = d * sc[w0 / 16], ds1 = d * sc[w0 / 16 + 1];
+            const uint8_t* __restrict__ qq = ql + (k & 1) * 32;
+            for (int l = 0; l < 32; ++l) {
+              const int lo = (k < 2) ? (qq[l] & 15) : (qq[l] >> 4);
+              const int v = lo | (((qh[l] >> (2 * k)) & 3) << 4);
+              o[w0 + l] = (l < 16 ? ds0 : ds1) * (float)(v - 32);
+            }
+          }
+        }
       }
       return;
   }

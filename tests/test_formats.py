@@ -45,6 +45,19 @@ def test_native_dequant_row_matches_numpy(native, qt):
 
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q5_K, Q.Q6_K, Q.Q8_0])
+def test_native_dequant_row_random_bits(native, qt):
+    """Every quant / scale / high-bit field exercised (random block bytes, 6-bit scales up to 63):
+    the native row dequantizer (CPU backend, per-sub-block scales hoisted) against numpy."""
+    rng = np.random.default_rng(11 + qt)
+    K = 1024
+    b = Q.random_blocks(rng, qt, 1, K, 0.05)
+    ref = Q.dequantize(b, qt).reshape(-1)
+    out = np.zeros(K, np.float32)
+    assert native.mp_dequant_row(qt, b.ctypes.data, out.ctypes.data, K) == 0
+    np.testing.assert_allclose(out, ref, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q5_K, Q.Q6_K, Q.Q8_0])
 def test_random_blocks_finite(qt):
     rng = np.random.default_rng(1)
     b = Q.random_blocks(rng, qt, 4, 512, 0.05)
