@@ -273,7 +273,8 @@ __device__ __forceinline__ half8_t softmax_chunk(f32x4 (&sc)[2], bool mask, int 
                  (f16)pv[1][0], (f16)pv[1][1], (f16)pv[1][2], (f16)pv[1][3]};
 }
 
-template <int KK>
+// ROT = false: q is already rotated (the qkv GEMV's append epilogue, DecodeAttnParams::pre)
+template <int KK, bool ROT = true>
 __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const float* row, const float2* cs, float nrs,
                                                int kvh, int G, int q4, int col, half8_t (&qf)[KK]) {
   const int g = col;
@@ -305,7 +306,7 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
         const float4* xs = reinterpret_cast<const float4*>(row + hs * p.hd + dl);
         const float4* cp = reinterpret_cast<const float4*>(cs + dl / 2);
         xa[kh][0] = xs[0]; xa[kh][1] = xs[1];
-        ca[kh][0] = cp[0]; ca[kh][1] = cp[1];
+        if constexpr (ROT) { ca[kh][0] = cp[0]; ca[kh][1] = cp[1]; }
         if constexpr (HB) {
           const float4* bs = reinterpret_cast<const float4*>(p.bias + hs * p.hd + dl);
           ba[kh][0] = bs[0]; ba[kh][1] = bs[1];
@@ -317,7 +318,12 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
         const int d0 = 32 * kk + 8 * q4;
         const bool ok = rvalid && d0 < p.hd;
         float x[8] = {xa[kh][0].x, xa[kh][0].y, xa[kh][0].z, xa[kh][0].w, xa[kh][1].x, xa[kh][1].y, xa[kh][1].z, xa[kh][1].w};
-        const float c[8] = {ca[kh][0].x, ca[kh][0].y, ca[kh][0].z, ca[kh][0].w, ca[kh][1].x, ca[kh][1].y, ca[kh][1].z, ca[kh][1].w};
+        float c[8] = {};
+        if constexpr (ROT) {
+          const float cc[8] = {ca[kh][0].x, ca[kh][0].y, ca[kh][0].z, ca[kh][0].w, ca[kh][1].x, ca[kh][1].y, ca[kh][1].z, ca[kh][1].w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) c[j] = cc[j];
+        }
         if constexpr (HB) {
           const float b[8] = {ba[kh][0].x, ba[kh][0].y, ba[kh][0].z, ba[kh][0].w, ba[kh][1].x, ba[kh][1].y, ba[kh][1].z, ba[kh][1].w};
 #pragma unroll
@@ -329,8 +335,13 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
         half8_t v = {};
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-          v[j] = ok ? (f16)((x[j] * c[j] - x[j + 1] * c[j + 1]) * qsc) : (f16)0.f;
-          v[j + 1] = ok ? (f16)((x[j] * c[j + 1] + x[j + 1] * c[j]) * qsc) : (f16)0.f;
+          if constexpr (ROT) {
+            v[j] = ok ? (f16)((x[j] * c[j] - x[j + 1] * c[j + 1]) * qsc) : (f16)0.f;
+            v[j + 1] = ok ? (f16)((x[j] * c[j + 1] + x[j + 1] * c[j]) * qsc) : (f16)0.f;
+          } else {
+            v[j] = ok ? (f16)(x[j] * qsc) : (f16)0.f;
+            v[j + 1] = ok ? (f16)(x[j + 1] * qsc) : (f16)0.f;
+          }
         }
         qf[kk] = v;
       }
@@ -350,7 +361,7 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
           const int d = d0 + j;
           if (d < p.hd) {
             const float x0 = qkv_at(qr + d), x1 = qkv_at(qr + d + 1);
-            const float2 c = cs[d >> 1];
+            const float2 c = ROT ? cs[d >> 1] : make_float2(1.f, 0.f);
             v[j] = (f16)((x0 * c.x - x1 * c.y) * qsc);
             v[j + 1] = (f16)((x0 * c.y + x1 * c.x) * qsc);
           }
@@ -366,7 +377,9 @@ __device__ __forceinline__ void decode_q_frags(const DecodeAttnParams& p, const 
 __device__ int g_attn_probe_calls = 0;
 #endif
 
-template <int DP, bool F8, bool PF, int NW = 4>
+// PRE: q arrives rotated and the new token's K / V are already in the cache (the qkv GEMV's append
+// epilogue, DecodeAttnParams::pre): no append, no RoPE, and no dependent position -> page chain
+template <int DP, bool F8, bool PF, int NW = 4, bool PRE = false>
 __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, const int t, const int kvh, const int z,
                                                  f16* xo = nullptr) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;   // raw fragment: 8 elements
@@ -452,7 +465,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
   // global round trip per call: the single-stream fixed cost, profiles/r8d_attn_ctx_sweep.txt)
   __shared__ __attribute__((aligned(16))) f16 sm_kn[DP];
   __shared__ f16 sm_vn[DP];
-  const bool owns = start <= pos && pos < end;
+  const bool owns = !PRE && start <= pos && pos < end;
   const int nch = (end - start + 31) / 32;
   if (PF && !pre && wv < nch) load(wv, kA, vA);   // in flight during the q build and the append
   const int j = threadIdx.x;   // the append: one K pair and one V element per thread (DP <= 256 threads)
@@ -477,7 +490,7 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
 
   // 2. q fragments with RoPE applied in registers (decode_q_frags)
   half8_t qf[KK];
-  decode_q_frags<KK>(p, row, cs, nrs, kvh, G, q4, col, qf);
+  decode_q_frags<KK, !PRE>(p, row, cs, nrs, kvh, G, q4, col, qf);
   ATT_STAMP(2);
 
   // 3. append the new token's K (rotated) and V to the cache.  The split that reads the new token
@@ -701,16 +714,16 @@ __device__ __forceinline__ void attn_decode_body(const DecodeAttnParams& p, cons
     __hip_atomic_store(p.counters + (size_t)t * p.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int DP, bool F8>
+template <int DP, bool F8, bool PRE = false>
 __global__ __launch_bounds__(256) void attn_decode_kernel(const DecodeAttnParams p) {
-  attn_decode_body<DP, F8, true>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+  attn_decode_body<DP, F8, true, 4, PRE>(p, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 // single stream / tiny micro-batches (few (token, kv head) workgroups, short contexts): 8 waves, so
 // every 32-key chunk of a context up to 256 keys has its own wave (with 4, wave 0 computed chunks 0
 // and 4 one after the other: the ~2.8 us chunk phase of profiles/r8j_attn_stamps.txt)
-template <int DP, bool F8>
+template <int DP, bool F8, bool PRE = false>
 __global__ __launch_bounds__(512) void attn_decode_kernel8(const DecodeAttnParams p) {
-  attn_decode_body<DP, F8, true, 8>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+  attn_decode_body<DP, F8, true, 8, PRE>(p, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 // many-split long contexts: 3 workgroups per CU (occupancy, not per-wave latency, is what they need)
 template <int DP, bool F8>
@@ -1149,16 +1162,12 @@ void launch_attn_combine(const AttnParams& p, hipStream_t st) {
   else hipLaunchKernelGGL(mpk::attn_combine_kernel<64>, dim3(p.M * p.Hq), dim3(64), 0, st, p);
 }
 
-template <bool F8, bool PF>
+// many splits / many workgroups: the 3-per-CU variant without the next-chunk prefetch
+template <bool F8>
 static void attn_decode_go(const DecodeAttnParams& p, hipStream_t st) {
   dim3 grid(p.M, p.Hkv, p.n_split);
-  if constexpr (PF) {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, F8>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, F8>), grid, dim3(256), 0, st, p);
-  } else {
-    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel_np<128, F8>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((mpk::attn_decode_kernel_np<64, F8>), grid, dim3(256), 0, st, p);
-  }
+  if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel_np<128, F8>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((mpk::attn_decode_kernel_np<64, F8>), grid, dim3(256), 0, st, p);
 }
 
 constexpr int kAttnOTpw = 8;   // output tiles per workgroup: 8B's W_o -> 32 x 8 = 256 workgroups
@@ -1196,7 +1205,28 @@ bool attn_decode_wave_selected(const DecodeAttnParams& p) {
   return (int64_t)p.M * p.Hkv * p.n_split >= knob(KNOB_ATTN_WAVE_MIN);
 }
 
+bool attn_decode_pre_ok(const DecodeAttnParams& p) {
+  return !attn_decode_wave_selected(p) && p.n_split == 1 && p.M * p.Hkv <= knob(KNOB_ATTN_PF_MAXWG) && !p.ssq &&
+         (p.Dp == 128 || p.Dp == 64);
+}
+
+template <bool F8, bool PRE>
+static void attn_decode_pf(const DecodeAttnParams& p, hipStream_t st) {
+  const dim3 grid(p.M, p.Hkv, 1);
+  if (p.M * p.Hkv <= knob(KNOB_ATTN_NW8_MAXWG)) {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel8<128, F8, PRE>), grid, dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel8<64, F8, PRE>), grid, dim3(512), 0, st, p);
+  } else {
+    if (p.Dp == 128) hipLaunchKernelGGL((mpk::attn_decode_kernel<128, F8, PRE>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((mpk::attn_decode_kernel<64, F8, PRE>), grid, dim3(256), 0, st, p);
+  }
+}
+
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
+  if (p.pre) {   // q rotated and K / V appended by the qkv GEMV (gemvs QkvAppend)
+    if (!attn_decode_pre_ok(p)) throw std::runtime_error("launch_attn_decode: pre-appended inputs need the one-split kernel");
+    return p.kv_fp8 ? attn_decode_pf<true, true>(p, st) : attn_decode_pf<false, true>(p, st);
+  }
   if (attn_decode_wave_selected(p)) {
     const int items = p.M * p.Hkv * p.n_split;
     const dim3 grid((items + 3) / 4);
@@ -1223,19 +1253,8 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
   // MIPIPE_ATTN_PF_MAXWG) need occupancy more than per-wave latency: the 3-per-CU variant
   const int pf_max = knob(KNOB_ATTN_PF_MAXWG);
   const bool pf = p.n_split == 1 && p.M * p.Hkv <= pf_max;
-  if (pf && p.M * p.Hkv <= knob(KNOB_ATTN_NW8_MAXWG)) {
-    const dim3 grid(p.M, p.Hkv, 1);
-    if (p.Dp == 128) {
-      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_kernel8<128, true>), grid, dim3(512), 0, st, p);
-      else hipLaunchKernelGGL((mpk::attn_decode_kernel8<128, false>), grid, dim3(512), 0, st, p);
-    } else {
-      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_kernel8<64, true>), grid, dim3(512), 0, st, p);
-      else hipLaunchKernelGGL((mpk::attn_decode_kernel8<64, false>), grid, dim3(512), 0, st, p);
-    }
-    return;
-  }
-  if (p.kv_fp8) pf ? attn_decode_go<true, true>(p, st) : attn_decode_go<true, false>(p, st);
-  else pf ? attn_decode_go<false, true>(p, st) : attn_decode_go<false, false>(p, st);
+  if (pf) return p.kv_fp8 ? attn_decode_pf<true, false>(p, st) : attn_decode_pf<false, false>(p, st);
+  p.kv_fp8 ? attn_decode_go<true>(p, st) : attn_decode_go<false>(p, st);
 }
 
 }  // namespace mp

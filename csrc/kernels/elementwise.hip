@@ -457,26 +457,6 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* __restric
   if (acc == 0x9E3779B9u) out[blockIdx.x] = (float)acc;   // keeps the loads; practically never stores
 }
 
-// MALL prefetch (HipStage knob PREFETCH): read up to 6 byte ranges with plain (allocating) 16 B
-// loads, 4 in flight per lane, so the GEMVs that follow find their weights in the 256 MiB Infinity
-// Cache.  Runs on a side stream while the latency-bound qkv / attention / o phases leave HBM idle.
-__global__ __launch_bounds__(256) void prefetch_kernel(const PrefetchArgs a, uint32_t magic, uint32_t* sink) {
-  uint32_t acc = 0;
-  const size_t stride = (size_t)gridDim.x * 256 * 4;
-  for (int r = 0; r < a.n; ++r) {
-    const u32x4* __restrict__ b = reinterpret_cast<const u32x4*>(a.p[r]);
-    const size_t n16 = a.bytes[r] / 16;
-    for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
-      u32x4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = i + 256 * u < n16 ? b[i + 256 * u] : u32x4{0, 0, 0, 0};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    }
-  }
-  if (acc == magic) sink[blockIdx.x & 63] = acc;   // keeps the loads (magic: a value never matched in practice)
-}
-
 // one thread per row of the micro-batch (mb_size up to 1024: a 64-thread single block advanced only
 // rows 0-63, so wide micro-batches decoded rows >= 64 at a frozen position)
 __global__ __launch_bounds__(256) void advance_kernel(int32_t* pos, int32_t* kvlen, int M, int32_t* step) {
@@ -607,12 +587,6 @@ void launch_moe_combine(const float* Yslot, int ld_slot, int k, int M, int n, fl
 void launch_stream_read(const void* buf, size_t bytes, float* out, hipStream_t st) {
   hipLaunchKernelGGL(mpk::stream_read_kernel, dim3(4096), dim3(256), 0, st, reinterpret_cast<const u32x4*>(buf),
                      bytes / 16, out);
-}
-
-void launch_prefetch(const PrefetchArgs& a, int grid, uint32_t* sink, hipStream_t st) {
-  if (a.n <= 0) return;
-  if (a.n > 6 || !sink || grid <= 0) throw std::runtime_error("launch_prefetch: 1-6 ranges, a sink and a grid");
-  hipLaunchKernelGGL(mpk::prefetch_kernel, dim3(grid), dim3(256), 0, st, a, 0x9E3779B9u, sink);
 }
 
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st) {

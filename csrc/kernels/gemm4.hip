@@ -682,7 +682,6 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
 static int g4_bm(int ptype, int M, int ntiles) {
   if (is16(ptype)) return 128;
   if (knob(KNOB_GEMM3_BM)) return knob(KNOB_GEMM3_BM);
-  if (M <= 64 && knob(KNOB_GEMM4_M64)) return 64;   // 64-row micro-batches on the GEMM (opt-in)
   if (M <= 128) return 128;
   const int cgs = (ntiles + 15) / 16;
   return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;

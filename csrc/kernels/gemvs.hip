@@ -42,67 +42,11 @@ using namespace mp;
 
 constexpr int GS_NW = 8;
 constexpr int GS_NT = GS_NW * 64;
+constexpr int EPI_QKV = 3;   // STORE with the RoPE + KV-append epilogue (GemvParams::qa)
 
-// ---- chained launches (gemvs_chain_kernel): consecutive single-stream GEMVs in ONE launch, each
-// phase's workgroups issuing their first weight loads before they wait for the previous phase, so a
-// phase's ramp (launch, first HBM round trip) hides under the previous phase's tail instead of
-// following a kernel boundary.  Hand-off (MI355X_MICROARCH.md 'Valid forms', first row of the sc1
-// table; cdna_hip_programming.md Guideline 16): every byte a later phase reads is stored sc1 (agent
-// relaxed) and drained (vmcnt(0)) by every storing wave, after the workgroup barrier one lane adds
-// to the phase's counter (agent atomic); a consumer workgroup's lane 0 polls that counter with sc1
-// loads, the others pass a barrier it joins, and EVERY load of handed-off bytes is an sc1 load.
-// CH bit 0: this phase consumes a previous phase's outputs; bit 1: its outputs are consumed later in
-// the launch.
-struct ChainWait {
-  const int32_t* cnt = nullptr;   // the previous phase's completion counter
-  int target = 0;                 // its workgroup count
-  int32_t* err = nullptr;         // set to 1 by a poll that gave up (bounded spin)
-};
-__device__ __forceinline__ float ld_sc1f(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1u(const void* p) {
-  return __hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<void*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1f(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_sc1u(void* p, uint32_t v) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool SC>
-__device__ __forceinline__ float4 ld_f4(const float* p) {
-  if constexpr (SC) return make_float4(ld_sc1f(p), ld_sc1f(p + 1), ld_sc1f(p + 2), ld_sc1f(p + 3));
-  else return *reinterpret_cast<const float4*>(p);
-}
-template <bool SC>
-__device__ __forceinline__ u32x4 ld_u4(const void* p) {
-  if constexpr (SC) {
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-    return u32x4{ld_sc1u(q), ld_sc1u(q + 1), ld_sc1u(q + 2), ld_sc1u(q + 3)};
-  } else {
-    return *reinterpret_cast<const u32x4*>(p);
-  }
-}
-// the consumer's wait: lane 0 polls (relaxed sc1, s_sleep between polls, bounded), the workgroup joins
-__device__ __forceinline__ void chain_wait(const ChainWait& cw) {
-  if (threadIdx.x == 0) {
-    int spins = 0;
-    while (__hip_atomic_load(const_cast<int32_t*>(cw.cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cw.target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 22)) {   // ~0.1 s: a broken hand-off ends in a flagged wrong result, not a hang
-        __hip_atomic_store(cw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// bx: this workgroup's tile-group index (blockIdx.x, or its offset inside a segment of gemvs2 or a
-// phase of a chain); by: its k-split (blockIdx.y of a plain launch)
-template <int PT, int EPI, int G, bool NORM, int NSO = 0, int CH = 0>
-__device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx, const int by = -1,
-                                           const ChainWait cw = ChainWait{}) {
-  constexpr bool SCL = (CH & 1) != 0, SCS = (CH & 2) != 0;   // sc1 loads of inputs / stores of outputs
+// bx: this workgroup's tile-group index (blockIdx.x, or its offset inside a segment of gemvs2)
+template <int PT, int EPI, int G, bool NORM, int NSO = 0>
+__device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx) {
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr bool BF = PT == P_BF16;
@@ -116,7 +60,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r = lane & 15;
   const int M = p.M;
-  const int split = by >= 0 ? by : (int)blockIdx.y;
+  const int split = blockIdx.y;
   const int sbA = split * p.sb_per_split;
   const int sbB = min(sbA + p.sb_per_split, p.nsb);
   if (sbA >= sbB) return;   // uniform over the workgroup
@@ -130,13 +74,39 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   const bool live = tile < p.ntiles;
   const __amdgpu_buffer_rsrc_t wsrc =
       make_rsrc(p.W + ((size_t)min(tile, p.ntiles - 1) * p.nsb + wA) * CB, (uint32_t)(live ? (wB - wA) * CB : 0));
+#ifdef MIPIPE_TIMING_PROBES
+  const int probe = p.probe;
+#else
+  constexpr int probe = 0;
+#endif
+  // the single owner's residual (ATOMIC, one split): loaded first, so the epilogue is a plain store
+  // instead of a read-modify-write round trip after the reduction.  Epilogue wave e < G owns tile
+  // bx * G + e; lane (m = lane >> 4, column r)
+  float resid = 0.f;
+  if constexpr (EPI == EPI_ATOMIC) {
+    const int et0 = bx * G + wave, nc0 = et0 * 16 + r;
+    if (nsplit == 1 && p.rpf && wave < G && et0 < p.ntiles && (lane >> 4) < M && nc0 < p.n_valid)
+      resid = p.Y[(size_t)(lane >> 4) * p.ldy + nc0];
+  }
   typename D::Raw ring[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) D::load(ring[s], BufSrc{wsrc, s * CB}, lane);   // past the range: zeros, no traffic
-  if constexpr (SCL) chain_wait(cw);   // weights in flight while the previous phase finishes
+  // QKV epilogue: position, cache page and this lane's (cos, sin), loaded under the weight stream
+  int qa_pos = 0, qa_page = 0;
+  float2 qa_cs = make_float2(1.f, 0.f);
+  if constexpr (EPI == EPI_QKV) {
+    const QkvAppend& q = p.qa;
+    const int m = lane >> 4, c = q.col0 + (bx * G + wave) * 16 + r;
+    if (wave < G && m < M) {
+      qa_pos = q.pos[m];
+      qa_page = q.block_table[(size_t)(q.slot0 + m) * q.max_pages + (qa_pos >> 6)];
+      if (c < (q.Hq + q.Hkv) * q.hd) qa_cs = q.rope_cs[(size_t)qa_pos * (q.hd >> 1) + ((c % q.hd) >> 1)];
+    }
+  }
 
   // ---- prologue: x of rows [0, M), k in [sbA*256, sbB*256) -> LDS as f16
-  if constexpr (NORM) {
+  if (probe & 2) {
+  } else if constexpr (NORM) {
     const int d4 = p.d_norm >> 2;
     const int k0 = sbA * 256, k1 = min(sbB * 256, p.d_norm);   // this workgroup's k-range (valid part)
     if (M == 1 && d4 <= 4 * GS_NT) {
@@ -148,7 +118,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
       for (int u = 0; u < 4; ++u) {
         const int c = tid + u * GS_NT;
         const bool in = c < d4, mine = in && 4 * c >= k0 && 4 * c < k1;
-        v[u] = in ? ld_f4<SCL>(p.Xf + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[u] = in ? *reinterpret_cast<const float4*>(p.Xf + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
         gm[u] = mine ? reinterpret_cast<const float4*>(p.gamma)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
@@ -182,7 +152,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int c = c0 + tid + u * GS_NT;
-              v[u] = c < d4 ? ld_f4<SCL>(reinterpret_cast<const float*>(xr + c)) : make_float4(0.f, 0.f, 0.f, 0.f);
+              v[u] = c < d4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) ss[m] += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
@@ -209,7 +179,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
         u32x4 o = {0u, 0u, 0u, 0u};
         if (kg < p.d_norm) {
           const float* xr = p.Xf + (size_t)m * p.ldxf + kg;
-          const float4 a = ld_f4<SCL>(xr), b = ld_f4<SCL>(xr + 4);
+          const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
           const float4 ga = *reinterpret_cast<const float4*>(p.gamma + kg), gb = *reinterpret_cast<const float4*>(p.gamma + kg + 4);
           const float sc = rs_s[m];
           o = x8_pack<BF>(a.x * sc * ga.x, a.y * sc * ga.y, a.z * sc * ga.z, a.w * sc * ga.w, b.x * sc * gb.x,
@@ -227,7 +197,7 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
       for (int u = 0; u < 4; ++u) {
         const int c = c0 + tid + u * GS_NT;
         const int m = c / k8, kl = (c - m * k8) * 8;
-        if (c < tot) v[u] = ld_u4<SCL>(p.X + (size_t)m * p.ldx + (size_t)sbA * 256 + kl);
+        if (c < tot) v[u] = *reinterpret_cast<const u32x4*>(p.X + (size_t)m * p.ldx + (size_t)sbA * 256 + kl);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -245,6 +215,10 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   const f16* xrow = xs + (size_t)r * krange + t16_xoff(g, 0);   // valid for r < M only
   const bool xr_ok = r < M;
   auto step = [&](const int s, const int sbl) {   // sbl: super-block index relative to sbA
+    if (probe & 1) {   // timing probe: consume the loads, no dequant / MFMA
+      acc[0] += __uint_as_float(*reinterpret_cast<const uint32_t*>(&ring[s]) & 1u);
+      return;
+    }
     half8_t b[4];
     D::template dequant<0>(ring[s], b, lane, kc);
 #pragma unroll
@@ -305,13 +279,36 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   if constexpr (EPI == EPI_SWIGLU) {
     const float up = __shfl_xor(val, 8);
     const int o = et * 8 + r;
-    if constexpr (SCS) {
-      // 4-B sc1 stores: lane r (even) writes its f16 and lane r + 1's (the chain needs n_valid even)
-      const uint32_t bits = (uint32_t)__builtin_bit_cast(uint16_t, sat_f16(silu(val) * up));
-      const uint32_t nb = (uint32_t)__shfl_down((int)bits, 1);
-      if (r < 8 && !(r & 1) && m < M && o < p.n_valid) st_sc1u(p.H + (size_t)m * p.ldh + o, bits | (nb << 16));
-    } else {
-      if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(val) * up);
+    if (r < 8 && m < M && o < p.n_valid) p.H[(size_t)m * p.ldh + o] = sat_f16(silu(val) * up);
+  } else if constexpr (EPI == EPI_QKV) {
+    // q / k: rotate the adjacent pair (c, c ^ 1) (lanes r, r ^ 1); q -> Y (f32), k and v -> the cache
+    const QkvAppend& q = p.qa;
+    const int nc = et * 16 + r;
+    const float out = val + (p.bias ? p.bias[nc] : 0.f);
+    const float oth = __shfl_xor(out, 1);
+    const int c = q.col0 + nc;
+    const int qn = q.Hq * q.hd, kn = q.Hkv * q.hd;
+    const bool odd = r & 1;
+    const float x0 = odd ? oth : out, x1 = odd ? out : oth;
+    const float rot = odd ? x0 * qa_cs.y + x1 * qa_cs.x : x0 * qa_cs.x - x1 * qa_cs.y;
+    const float rp = __shfl_xor(rot, 1);   // the pair's other rotated value
+    if (m < M && nc < p.n_valid) {
+      const int idx = qa_pos & 63;
+      if (c < qn) {
+        p.Y[(size_t)m * p.ldy + nc] = rot;
+      } else if (c < qn + kn) {
+        const int h = (c - qn) / q.hd, d = (c - qn) % q.hd;
+        const size_t ko = (((size_t)qa_page * q.Hkv + h) * 64 + idx) * q.Dp + d;
+        if (!odd) {
+          if (q.kv_fp8) *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(q.k_cache) + ko) = (uint16_t)f8x2_pack(rot, rp);
+          else *reinterpret_cast<half2_t*>(q.k_cache + ko) = half2_t{(f16)rot, (f16)rp};
+        }
+      } else {
+        const int h = (c - qn - kn) / q.hd, d = (c - qn - kn) % q.hd;
+        const size_t vo = (((size_t)qa_page * q.Hkv + h) * q.Dp + d) * 64 + idx;
+        if (q.kv_fp8) reinterpret_cast<uint8_t*>(q.v_cache)[vo] = (uint8_t)f8x2_pack(out, 0.f);
+        else q.v_cache[vo] = (f16)out;
+      }
     }
   } else {
     const int nc = et * 16 + r;
@@ -319,11 +316,11 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
       const float out = val + ((p.bias && split == 0) ? p.bias[nc] : 0.f);
       float* dst = p.Y + (size_t)m * p.ldy + nc;
       if constexpr (EPI == EPI_ATOMIC) {
-        if constexpr (CH != 0) st_sc1f(dst, ld_sc1f(dst) + out);   // chain: single owner, sc1 both ways
-        else if (nsplit == 1) *dst += out;   // single owner: plain read-modify-write (deterministic)
+        if (nsplit == 1) {   // single owner: deterministic
+          if (p.rpf != 0 || (probe & 4) != 0) *dst = resid + out;
+          else *dst += out;
+        }
         else unsafeAtomicAdd(dst, out);
-      } else if constexpr (SCS) {
-        st_sc1f(dst, out);
       } else {
         *dst = out;
       }
@@ -339,58 +336,10 @@ __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const 
 // two weight segments with different quant types over the same normed input in ONE launch (the
 // q+k and v projections of a mixed-type layer, e.g. Q4_K_M's Q6_K attn_v): workgroups [0, nwg1)
 // take segment 1, the rest segment 2.  STORE epilogue, RMSNorm fused, no k-split.
-template <int PT, int PT2, int G>
+template <int PT, int PT2, int G, int EPI = EPI_STORE>
 __global__ __launch_bounds__(GS_NT) void gemvs2_kernel(const GemvParams p, const GemvParams p2, const int nwg1) {
-  if ((int)blockIdx.x < nwg1) gemvs_body<PT, EPI_STORE, G, true>(p, 1, blockIdx.x);
-  else gemvs_body<PT2, EPI_STORE, G, true>(p2, 1, blockIdx.x - nwg1);
-}
-
-template <int PT, int EPI, int G, bool NORM>
-struct GemvsPhase {
-  template <int CH>
-  __device__ static __forceinline__ void run(const GemvParams& p, int bx, const ChainWait& cw) {
-    gemvs_body<PT, EPI, G, NORM, 2, CH>(p, 1, bx, 0, cw);   // NS 2 (the default), no k-split
-  }
-};
-
-// phases P0 .. P(NPH-1) (P2 = void: two); phase i owns blocks [start[i], start[i+1]).  Every
-// workgroup of the grid must be resident at once (the host sizes the phases for that).
-template <class P0, class P1, class P2>
-__global__ __launch_bounds__(GS_NT) void gemvs_chain_kernel(const GemvsChainArgs a) {
-  constexpr int NPH = std::is_void<P2>::value ? 2 : 3;
-  const int b = blockIdx.x;
-  const int ph = b < a.start[1] ? 0 : (NPH == 2 || b < a.start[2]) ? 1 : 2;
-  const int bx = b - a.start[ph];
-  ChainWait cw;
-  cw.err = a.err;
-  if (ph > 0) {
-    cw.cnt = a.cnt + ph - 1;
-    cw.target = a.start[ph] - a.start[ph - 1];
-  }
-  if (ph == 0) {
-    P0::template run<2>(a.p[0], bx, cw);
-  } else if (ph == NPH - 1) {
-    if constexpr (NPH == 3) P2::template run<1>(a.p[2], bx, cw);
-    else P1::template run<1>(a.p[1], bx, cw);
-  } else {
-    P1::template run<3>(a.p[1], bx, cw);
-  }
-  // publish: every wave drains its (sc1) stores, then one lane counts the workgroup; the last
-  // workgroup of the last phase re-arms the counters for the next launch (every earlier phase has
-  // finished counting by then: each phase waited for all of the one before)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (ph < NPH - 1) {
-      __hip_atomic_fetch_add(a.cnt + ph, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const int n_last = a.start[NPH] - a.start[NPH - 1];
-      if (__hip_atomic_fetch_add(a.cnt + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_last - 1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) __hip_atomic_store(a.cnt + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
+  if ((int)blockIdx.x < nwg1) gemvs_body<PT, EPI, G, true>(p, 1, blockIdx.x);
+  else gemvs_body<PT2, EPI, G, true>(p2, 1, blockIdx.x - nwg1);
 }
 
 }  // namespace mpk
@@ -467,21 +416,28 @@ template <int PT>
 static void gemvs_pt(int epi, const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   const bool norm = p.Xf != nullptr;
   switch (epi) {
-    case EPI_STORE: return norm ? gemvs_g<PT, EPI_STORE, true>(p, pl, st) : gemvs_g<PT, EPI_STORE, false>(p, pl, st);
+    case EPI_STORE:
+      if (p.qa.pos) return gemvs_g<PT, mpk::EPI_QKV, true>(p, pl, st);   // norm required (launch_gemvs checks)
+      return norm ? gemvs_g<PT, EPI_STORE, true>(p, pl, st) : gemvs_g<PT, EPI_STORE, false>(p, pl, st);
     case EPI_ATOMIC: return norm ? gemvs_g<PT, EPI_ATOMIC, true>(p, pl, st) : gemvs_g<PT, EPI_ATOMIC, false>(p, pl, st);
     case EPI_SWIGLU: return norm ? gemvs_g<PT, EPI_SWIGLU, true>(p, pl, st) : gemvs_g<PT, EPI_SWIGLU, false>(p, pl, st);
   }
 }
 
-template <int PT, int PT2, int G>
-static void gemvs2_go(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
+template <int PT, int PT2, int G, int EPI>
+static void gemvs2_go_e(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
   static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs2_kernel<PT, PT2, G>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs2_kernel<PT, PT2, G, EPI>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
   }();
   if (!attr && lds > 60 * 1024) throw std::runtime_error("gemvs2: cannot raise the dynamic LDS limit");
   const int nwg1 = (p.ntiles + G - 1) / G, nwg2 = (p2.ntiles + G - 1) / G;
-  hipLaunchKernelGGL((mpk::gemvs2_kernel<PT, PT2, G>), dim3(nwg1 + nwg2), dim3(mpk::GS_NT), lds, st, p, p2, nwg1);
+  hipLaunchKernelGGL((mpk::gemvs2_kernel<PT, PT2, G, EPI>), dim3(nwg1 + nwg2), dim3(mpk::GS_NT), lds, st, p, p2, nwg1);
+}
+template <int PT, int PT2, int G>
+static void gemvs2_go(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
+  if (p.qa.pos) gemvs2_go_e<PT, PT2, G, mpk::EPI_QKV>(p, p2, lds, st);
+  else gemvs2_go_e<PT, PT2, G, EPI_STORE>(p, p2, lds, st);
 }
 
 template <int PT, int PT2>
@@ -502,12 +458,17 @@ bool gemvs2_supported(int pt, int pt2) {
 void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st) {
   if (!gemvs2_supported(pt, pt2)) throw std::runtime_error("launch_gemvs2: unsupported type pair");
   if (p.M < 1 || p.M > 4 || p2.M != p.M) throw std::runtime_error("launch_gemvs2: M must be 1..4 and equal");
+  if ((p.qa.pos != nullptr) != (p2.qa.pos != nullptr) || (p.qa.pos && (p.qa.hd % 16 || p.qa.col0 % 16 || p2.qa.col0 % 16)))
+    throw std::runtime_error("launch_gemvs2: both segments take the q|k|v append epilogue or neither");
   if (!p.Xf || !p2.Xf || p.nsb != p2.nsb || p.d_norm != p2.d_norm || (p.d_norm & 7) || p.d_norm > p.nsb * 256)
     throw std::runtime_error("launch_gemvs2: both segments need the same fused-norm input and K");
   // one plan for the union of the tiles (the shared G sizes both segments' workgroups)
   const GemvsPlan pl = plan_gemvs(p.ntiles + p2.ntiles, p.nsb, p.M, EPI_STORE, true, true);
   if (pl.nsplit != 1 || pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs2: x k-range does not fit LDS");
   p.sb_per_split = p2.sb_per_split = pl.sb_per_split;
+#ifdef MIPIPE_TIMING_PROBES
+  p.probe = p2.probe = knob(KNOB_GEMVS_PROBE);
+#endif
   if (pt == P_Q4_K) {
     if (pt2 == P_Q6_K) gemvs2_g<P_Q4_K, P_Q6_K>(pl.G, p, p2, pl.lds, st);
     else gemvs2_g<P_Q4_K, P_Q8_0>(pl.G, p, p2, pl.lds, st);
@@ -517,117 +478,13 @@ void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st)
   }
 }
 
-// ---- chains
-namespace {
-
-template <class K>
-int chain_capacity(K kernel, size_t lds) {
-  // resident workgroups of this kernel over the whole device; the occupancy API can report one block
-  // per CU too many at some SGPR counts (MI355X_MICROARCH.md, occupancy row), so at most 2 per CU
-  // are counted, with a 10 % margin (a spin-waiting phase needs every workgroup resident)
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t pr;
-    if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return 0;
-    cus = pr.multiProcessorCount;
-  }
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel), mpk::GS_NT, lds) != hipSuccess)
-    return 0;
-  return (int)(0.9 * std::min(nb, 2) * cus);
-}
-
-template <class P0, class P1, class P2>
-bool chain_go(GemvsChainArgs a, size_t lds, hipStream_t st) {
-  auto k = &mpk::gemvs_chain_kernel<P0, P1, P2>;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               152 * 1024) == hipSuccess;
-  const int n = std::is_void<P2>::value ? 2 : 3;
-  if (!attr && lds > 60 * 1024) return false;
-  if (a.start[n] > chain_capacity(k, lds)) return false;
-  hipLaunchKernelGGL(k, dim3(a.start[n]), dim3(mpk::GS_NT), lds, st, a);
-  return true;
-}
-
-// phase shapes the chain supports: (type, epilogue, G) -> the instantiation (G of the GEMVs with
-// SWIGLU: 4 | 8; of the ATOMIC ones: 2 | 4)
-template <int PTd, int Go, int Gg, int Gd>
-bool chain3_d(GemvsChainArgs a, size_t lds, hipStream_t st) {
-  using O = mpk::GemvsPhase<P_Q4_K, EPI_ATOMIC, Go, false>;
-  using GU = mpk::GemvsPhase<P_Q4_K, EPI_SWIGLU, Gg, true>;
-  using DN = mpk::GemvsPhase<PTd, EPI_ATOMIC, Gd, false>;
-  return chain_go<O, GU, DN>(a, lds, st);
-}
-template <int PTd>
-bool chain3_g(int go, int gg, int gd, GemvsChainArgs a, size_t lds, hipStream_t st) {
-  const int code = (go == 4) * 4 + (gg == 8) * 2 + (gd == 4);
-  switch (code) {
-    case 0: return chain3_d<PTd, 2, 4, 2>(a, lds, st);
-    case 1: return chain3_d<PTd, 2, 4, 4>(a, lds, st);
-    case 2: return chain3_d<PTd, 2, 8, 2>(a, lds, st);
-    case 3: return chain3_d<PTd, 2, 8, 4>(a, lds, st);
-    case 4: return chain3_d<PTd, 4, 4, 2>(a, lds, st);
-    case 5: return chain3_d<PTd, 4, 4, 4>(a, lds, st);
-    case 6: return chain3_d<PTd, 4, 8, 2>(a, lds, st);
-    default: return chain3_d<PTd, 4, 8, 4>(a, lds, st);
-  }
-}
-
-}  // namespace
-
-bool launch_gemvs_chain(const GemvsChainPhase* ph, int n, int32_t* cnt, int32_t* err, hipStream_t st, int* wgs_out) {
-  if (n != 3 || !cnt || !err) return false;
-  // o (ATOMIC, Q4_K) -> gate/up (SWIGLU + norm, Q4_K) -> down (ATOMIC, Q4_K | Q6_K), one row
-  if (ph[0].epi != EPI_ATOMIC || ph[1].epi != EPI_SWIGLU || ph[2].epi != EPI_ATOMIC) return false;
-  if (ph[0].ptype != P_Q4_K || ph[1].ptype != P_Q4_K || (ph[2].ptype != P_Q4_K && ph[2].ptype != P_Q6_K)) return false;
-  for (int i = 0; i < 3; ++i)
-    if (ph[i].p.M != 1 || (i != 1 && (ph[i].p.Xf || !ph[i].p.X)) || ph[i].p.bias) return false;
-  if (!ph[1].p.Xf || (ph[1].p.d_norm & 7) || (ph[1].p.n_valid & 1)) return false;
-  GemvsChainArgs a{};
-  size_t lds = 0;
-  for (int i = 0; i < 3; ++i) {
-    a.p[i] = ph[i].p;
-    a.p[i].sb_per_split = a.p[i].nsb;   // no k-split over the grid: single-owner outputs
-    lds = std::max(lds, (size_t)a.p[i].nsb * 256 * 2);
-  }
-  if (lds > 150 * 1024) return false;
-  // G per phase from its plan, clamped to the instantiated values, then coarsened until the three
-  // phases fit the resident capacity (at most 2 workgroups per CU are assumed: 0.9 x 2 x CUs)
-  auto wgs = [&](int i, int g) { return (a.p[i].ntiles + g - 1) / g; };
-  int G[3];
-  G[0] = std::max(2, std::min(4, plan_gemvs(a.p[0].ntiles, a.p[0].nsb, 1, EPI_ATOMIC, false, true).G));
-  G[1] = std::max(4, std::min(8, plan_gemvs(a.p[1].ntiles, a.p[1].nsb, 1, EPI_SWIGLU, true, true).G));
-  G[2] = std::max(2, std::min(4, plan_gemvs(a.p[2].ntiles, a.p[2].nsb, 1, EPI_ATOMIC, false, true).G));
-  int dev = 0;
-  hipDeviceProp_t pr;
-  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) return false;
-  const int budget = (int)(0.9 * 2 * pr.multiProcessorCount);
-  const int gmax[3] = {4, 8, 4};
-  for (;;) {
-    const int tot = wgs(0, G[0]) + wgs(1, G[1]) + wgs(2, G[2]);
-    if (tot <= budget) break;
-    int best = -1;
-    for (int i = 0; i < 3; ++i)
-      if (G[i] < gmax[i] && (best < 0 || wgs(i, G[i]) > wgs(best, G[best]))) best = i;
-    if (best < 0) return false;
-    G[best] *= 2;
-  }
-  a.start[0] = 0;
-  for (int i = 0; i < 3; ++i) a.start[i + 1] = a.start[i] + wgs(i, G[i]);
-  a.cnt = cnt;
-  a.err = err;
-  if (wgs_out) *wgs_out = a.start[3];
-  return ph[2].ptype == P_Q6_K ? chain3_g<P_Q6_K>(G[0], G[1], G[2], a, lds, st)
-                               : chain3_g<P_Q4_K>(G[0], G[1], G[2], a, lds, st);
-}
-
 void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G, int force_split) {
   if (p.M < 1 || p.M > 4) throw std::runtime_error("launch_gemvs: M must be 1..4");
   if (p.Xf && (p.d_norm <= 0 || (p.d_norm & 7) || p.d_norm > p.nsb * 256))
     throw std::runtime_error("launch_gemvs: fused RMSNorm needs d_norm a multiple of 8 within the padded K");
   if (!p.Xf && !p.X) throw std::runtime_error("launch_gemvs: no input");
+  if (p.qa.pos && (epi != EPI_STORE || !p.Xf || p.qa.hd % 16 || p.qa.col0 % 16 || p.qa.hd > p.qa.Dp))
+    throw std::runtime_error("launch_gemvs: the q|k|v append epilogue needs STORE, the fused norm and 16-aligned heads");
   GemvsPlan pl = plan_gemvs(p.ntiles, p.nsb, p.M, epi, p.Xf != nullptr, deterministic);
   if (force_G) pl.G = force_G;
   if (force_split) {   // tests: an explicit k-split over grid.y
@@ -638,6 +495,10 @@ void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStrea
   if (pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs: x k-range does not fit LDS");
   if (epi != EPI_ATOMIC && pl.nsplit != 1) throw std::runtime_error("launch_gemvs: only ATOMIC splits K");
   p.sb_per_split = pl.sb_per_split;
+  p.rpf = knob(KNOB_GEMVS_RPF);
+#ifdef MIPIPE_TIMING_PROBES
+  p.probe = knob(KNOB_GEMVS_PROBE);
+#endif
   switch (ptype) {
     case P_Q4_K: gemvs_pt<P_Q4_K>(epi, p, pl, st); break;
     case P_Q5_K: gemvs_pt<P_Q5_K>(epi, p, pl, st); break;

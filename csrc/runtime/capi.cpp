@@ -9,7 +9,11 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <atomic>
+#include <mutex>
+#include <thread>
 
+#include "cpu_qdot.h"
 #include "engine.h"
 #include "probe.h"
 #include "model.h"
@@ -73,6 +77,22 @@ int mp_dequant_row(int type, const uint8_t* src, float* dst, int64_t K) {
   API_TRY
   dequant_row(type, src, dst, K);
   return 0;
+  API_CATCH(-1)
+}
+
+// CPU integer dot (cpu_qdot.cpp): y[n] = <row n of W (N rows of K weights of ggml type), q8(x)>, the
+// dispatched (AVX2 when present) and the scalar form; returns 1 if the type has an integer dot
+int mp_qdot_rows(int type, const uint8_t* W, int64_t N, int64_t K, const float* x, float* y, float* y_scalar) {
+  API_TRY
+  if (!qdot_supported(type)) return 0;
+  Q8Buf b;
+  quantize_q8_rows(x, (int)K, 1, K, b);
+  const size_t rb = row_bytes(type, K);
+  for (int64_t n = 0; n < N; ++n) {
+    y[n] = qdot_row(type, W + n * rb, q8_row(b, 0), K);
+    y_scalar[n] = qdot_row_scalar(type, W + n * rb, q8_row(b, 0), K);
+  }
+  return 1;
   API_CATCH(-1)
 }
 
@@ -387,32 +407,6 @@ int mp_op_gemvs(int ptype, int epi, const void* W, int ntiles, int nsb, const vo
   launch_gemvs(ptype, epi, p, deterministic != 0, (hipStream_t)stream, G, nsplit);
   HIP_OK(hipGetLastError());
   return 0;
-  API_CATCH(-1)
-}
-
-// chained o -> gate/up -> down of one row (launch_gemvs_chain): attn f16 [Ko_pad] -> x f32 [d] += o;
-// h f16 = SwiGLU(gate/up(rmsnorm(x) * gamma)); x += down(h).  cnt: 16 device ints (zeroed once;
-// [8] = the error flag).  Returns the workgroups launched, 0 when the chain does not apply.
-int mp_op_gemvs_chain3(int pt_o, const void* Wo, int nt_o, int nsb_o, const void* attn, int ld_attn, int pt_gu,
-                       const void* Wgu, int nt_gu, int nsb_gu, void* x, int d, const void* gamma, float eps, void* h,
-                       int ldh, int F, int pt_dn, const void* Wdn, int nt_dn, int nsb_dn, void* cnt, void* stream) {
-  API_TRY
-  GemvsChainPhase ph[3];
-  for (auto& q : ph) q.p = GemvParams{};
-  ph[0].ptype = pt_o; ph[0].epi = EPI_ATOMIC;
-  ph[0].p.W = (const uint8_t*)Wo; ph[0].p.ntiles = nt_o; ph[0].p.nsb = nsb_o; ph[0].p.X = (const f16*)attn;
-  ph[0].p.ldx = ld_attn; ph[0].p.M = 1; ph[0].p.Y = (float*)x; ph[0].p.ldy = d; ph[0].p.n_valid = d;
-  ph[1].ptype = pt_gu; ph[1].epi = EPI_SWIGLU;
-  ph[1].p.W = (const uint8_t*)Wgu; ph[1].p.ntiles = nt_gu; ph[1].p.nsb = nsb_gu; ph[1].p.M = 1;
-  ph[1].p.H = (f16*)h; ph[1].p.ldh = ldh; ph[1].p.n_valid = F;
-  ph[1].p.Xf = (const float*)x; ph[1].p.ldxf = d; ph[1].p.gamma = (const float*)gamma; ph[1].p.eps = eps; ph[1].p.d_norm = d;
-  ph[2].ptype = pt_dn; ph[2].epi = EPI_ATOMIC;
-  ph[2].p.W = (const uint8_t*)Wdn; ph[2].p.ntiles = nt_dn; ph[2].p.nsb = nsb_dn; ph[2].p.X = (const f16*)h;
-  ph[2].p.ldx = ldh; ph[2].p.M = 1; ph[2].p.Y = (float*)x; ph[2].p.ldy = d; ph[2].p.n_valid = d;
-  int wgs = 0;
-  if (!launch_gemvs_chain(ph, 3, (int32_t*)cnt, (int32_t*)cnt + 8, (hipStream_t)stream, &wgs)) return 0;
-  HIP_OK(hipGetLastError());
-  return wgs;
   API_CATCH(-1)
 }
 
@@ -774,6 +768,74 @@ int mp_rccl_unique_id(uint8_t* out128) {
 // RCCL transport self-test (ws = 1): a 1-rank communicator on `device` and the
 // engine's RcclLink looping every size in `sizes` back to itself (grouped ncclSend/ncclRecv on one
 // stream), `iters` times each, checking every byte.  Returns a JSON report.
+// LocalLink posted-queue self-test on one device: a sender thread cycles n_bufs buffers (message i
+// filled with the value i + 1, each buffer reused only after Link::wait_consumed of its previous
+// message) while a receiver thread takes the messages with recv_delay_us of host delay before each
+// (a slow receiver: the sender runs ahead until the kDepth queue pushes back).  Returns the number of
+// received words that do not hold their message's value (0: ordered, no buffer reused too early),
+// or -1 on an error.
+int mp_local_link_selftest(int device, int n_msgs, int64_t bytes, int n_bufs, int recv_delay_us) {
+  API_TRY
+  HIP_OK(hipSetDevice(device));
+  if (n_msgs <= 0 || n_bufs <= 0 || bytes < 4 || bytes % 4) throw std::runtime_error("selftest: bad arguments");
+  LocalLink link(device, device);
+  link.set_timeout(60);
+  std::vector<void*> bufs(n_bufs);
+  for (auto& b : bufs) HIP_OK(hipMalloc(&b, bytes));
+  void* rb = nullptr;
+  HIP_OK(hipMalloc(&rb, bytes));
+  hipStream_t ss, rs;
+  HIP_OK(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
+  std::atomic<int> bad{0};
+  std::string err;
+  std::mutex emu;
+  std::thread snd([&] {
+    try {
+      HIP_OK(hipSetDevice(device));
+      std::vector<uint64_t> seq(n_bufs, 0);
+      for (int i = 0; i < n_msgs; ++i) {
+        const int k = i % n_bufs;
+        link.wait_consumed(seq[k], ss);   // the buffer's previous message has left it
+        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)bufs[k], i + 1, bytes / 4, ss));
+        link.send(bufs[k], bytes, ss);
+        seq[k] = link.last_seq();
+      }
+      HIP_OK(hipStreamSynchronize(ss));
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> l(emu);
+      err = e.what();
+      link.abort();
+    }
+  });
+  std::thread rcv([&] {
+    try {
+      HIP_OK(hipSetDevice(device));
+      std::vector<int32_t> h(bytes / 4);
+      for (int i = 0; i < n_msgs; ++i) {
+        if (recv_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(recv_delay_us));
+        link.recv(rb, bytes, rs);
+        HIP_OK(hipMemcpyAsync(h.data(), rb, bytes, hipMemcpyDeviceToHost, rs));
+        HIP_OK(hipStreamSynchronize(rs));
+        for (int32_t v : h) bad += v != i + 1;
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> l(emu);
+      err = e.what();
+      link.abort();
+    }
+  });
+  snd.join();
+  rcv.join();
+  for (auto b : bufs) (void)hipFree(b);
+  (void)hipFree(rb);
+  (void)hipStreamDestroy(ss);
+  (void)hipStreamDestroy(rs);
+  if (!err.empty()) throw std::runtime_error("local link selftest: " + err);
+  return bad.load();
+  API_CATCH(-1)
+}
+
 const char* mp_rccl_selftest(int device, const int64_t* sizes, int n_sizes, int iters) {
   API_TRY
   HIP_OK(hipSetDevice(device));

@@ -262,6 +262,21 @@ MP_HOST_AVX2_CLONES static float dot8(const float* w, const float* x, int64_t K)
 
 void CpuStage::matmul(const CpuMat& W, const float* X, int ldx, int M, float* Y, int ldy, bool accumulate) {
   const int64_t K = W.K;
+  if (opt_.cpu_q8 && qdot_supported(W.type) && K % qdot_block(W.type) == 0) {
+    // the weights in their stored integer form against int8 activation blocks (cpu_qdot.cpp)
+    quantize_q8_rows(X, ldx, M, K, xq_);
+    pool_->parallel_for(W.N, [&](int64_t n0, int64_t n1) {
+      for (int64_t n = n0; n < n1; ++n) {
+        const uint8_t* wr = W.data + n * W.rb;
+        for (int m = 0; m < M; ++m) {
+          const float s = qdot_row(W.type, wr, q8_row(xq_, m), K);
+          float& y = Y[(size_t)m * ldy + n];
+          y = accumulate ? y + s : s;
+        }
+      }
+    }, 16);
+    return;
+  }
   pool_->parallel_for(W.N, [&](int64_t n0, int64_t n1) {
     std::vector<float> w((size_t)K);
     for (int64_t n = n0; n < n1; ++n) {

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "model.h"
+#include "cpu_qdot.h"
 #include "stage.h"
 #include "threadpool.h"
 
@@ -99,6 +100,7 @@ class CpuStage : public Stage {
   std::vector<float> logits_;
   // scratch
   std::vector<float> xn_, qkv_, att_, h_, gu_;
+  Q8Buf xq_;   // matmul: the activation rows as int8 blocks (cpu_q8)
   uint64_t step_ = 0;
   std::vector<std::vector<int32_t>> hist_;   // per slot: accepted tokens, most recent last
 };

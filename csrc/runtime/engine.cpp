@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -22,6 +23,28 @@
 #include "qtypes.h"
 
 namespace mp {
+
+namespace {
+// host memory a CPU stage's KV pool may plan with: the "host_mem_gib" option, else MemAvailable from
+// /proc/meminfo (physical pages as a fallback), instead of assuming a 64 GiB host
+double host_mem_bytes(const Json& j) {
+  const double opt = j.get_num("host_mem_gib", 0.0);
+  if (opt > 0) return opt * (1 << 30);
+  if (FILE* f = std::fopen("/proc/meminfo", "r")) {
+    char key[64];
+    long kb = 0;
+    while (std::fscanf(f, "%63s %ld kB\n", key, &kb) == 2) {
+      if (std::strcmp(key, "MemAvailable:") == 0) {
+        std::fclose(f);
+        return (double)kb * 1024.0;
+      }
+    }
+    std::fclose(f);
+  }
+  const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGE_SIZE);
+  return pages > 0 && psz > 0 ? (double)pages * (double)psz : 64.0 * (1 << 30);
+}
+}  // namespace
 
 namespace {
 
@@ -276,7 +299,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
       const double pt = (double)layers * 2.0 * cfg_.n_head_kv * cfg_.padded_head_dim() * (host ? 4.0 : kv_fp8 ? 1.0 : 2.0);
       const double reserve =
           dev_n[e.first] * (4.0 * (1 << 30) + (double)M_ * std::max(chunk_, B_) * cfg_.d_model * 4.0 * 4);
-      const double budget = frac * (host ? 64.0 * (1 << 30) : cap_bytes) - e.second - reserve;
+      const double budget = frac * (host ? host_mem_bytes(j) : cap_bytes) - e.second - reserve;
       // paged KV: the pool holds the LIVE tokens of all slots (not n_slots x max_ctx)
       const long c = budget > 0 ? (long)(budget / pt) : 0;
       if (c < ctx) { ctx = c; per_tok = pt; lmax = layers; }
@@ -360,6 +383,11 @@ Engine::Engine(const Json& j) : jcfg_(j) {
   so.use_graphs = j.get_bool("graphs", true);
   so.attn_split_len = j.get_int("attn_split_len", 0);   // 0 = auto
   so.threads = j.get_int("threads", 0);
+  {
+    const std::string ca = j.get_str("cpu_act", "q8");
+    if (ca != "q8" && ca != "f32") throw std::runtime_error("cpu_act must be q8 or f32");
+    so.cpu_q8 = ca == "q8";
+  }
   so.fused_attn = j.get_bool("fused_attn", true);
   so.attn_o_max_ctx = j.get_int("attn_o_max_ctx", 0);
   so.prefill_gemm = j.get_bool("prefill_gemm", true);
@@ -403,6 +431,7 @@ Engine::Engine(const Json& j) : jcfg_(j) {
     HIP_OK(hipStreamCreateWithFlags(&w->recv_st, hipStreamNonBlocking));
     w->comp_ev.resize(M_); w->sent_ev.resize(M_); w->recv_ev.resize(M_);
     w->sent_valid.assign(M_, false);
+    w->sent_seq.assign(M_, 0);
     for (int mb = 0; mb < M_; ++mb) {
       HIP_OK(hipEventCreateWithFlags(&w->comp_ev[mb], hipEventDisableTiming));
       HIP_OK(hipEventCreateWithFlags(&w->sent_ev[mb], hipEventDisableTiming));
@@ -742,8 +771,15 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
     w.tr_base_ms = now_ms();
   }
   const bool wire = act_dtype_ != ACT_F32;
+  // before a stream overwrites micro-batch mb's last sent buffer: its send has been issued (sent_ev)
+  // and its bytes have left the buffer (Link::wait_consumed: LocalLink's posted queue)
+  auto reuse_wait = [&](int mb, hipStream_t s) {
+    if (!w.sent_valid[mb]) return;
+    HIP_OK(hipStreamWaitEvent(s, w.sent_ev[mb], 0));
+    w.out->wait_consumed(w.sent_seq[mb], s);
+  };
   auto recv_into = [&](int mb, void* buf, size_t bytes) {
-    if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(w.recv_st, w.sent_ev[mb], 0));
+    reuse_wait(mb, w.recv_st);
     HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
     HIP_OK(hipStreamWaitEvent(w.recv_st, w.comp_ev[mb], 0));
     // 2-byte wire: receive into the staging buffer, widen to the f32 residual on the compute stream
@@ -761,6 +797,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
     span(w, w.send_st, 1, std::string(last ? "send tok" : "send act") + " mb" + std::to_string(mb),
          [&] { w.out->send(buf, bytes, w.send_st); });
     HIP_OK(hipEventRecord(w.sent_ev[mb], w.send_st));
+    w.sent_seq[mb] = w.out->last_seq();
     w.sent_valid[mb] = true;
   };
   // activations: narrowed to the wire format on the compute stream (the previous send of this
@@ -778,7 +815,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
       case Item::PREFILL: {
         const size_t bytes = (size_t)it.T * d4;
         if (!first) recv_into(mb, st.act(mb), bytes);
-        else if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
+        else reuse_wait(mb, cs);
         span(w, cs, 0, "prefill mb" + std::to_string(mb) + " T" + std::to_string(it.T),
              [&] { st.prefill(mb, it.segs, cs); });
         if (!last) send_act(mb, st.act(mb), bytes);
@@ -799,7 +836,7 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
       case Item::DECODE: {
         if (!first) recv_into(mb, st.act(mb), (size_t)B_ * d4);
         else if (S_ > 1) HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
-        if (w.sent_valid[mb]) HIP_OK(hipStreamWaitEvent(cs, w.sent_ev[mb], 0));
+        reuse_wait(mb, cs);
         span(w, cs, 0, "decode mb" + std::to_string(mb), [&] { st.decode(mb, cs); });
         if (last) {
           const size_t ev_i = (size_t)(it.round - rounds_done_) * M_ + mb;
@@ -1014,6 +1051,7 @@ void Engine::ring_bcast_from_last(std::vector<int32_t>& v) {
   if (last) {
     HIP_OK(hipMemcpy(bcast_dev_, v.data(), bytes, hipMemcpyHostToDevice));
     w.out->send(bcast_dev_, bytes, w.send_st);
+    w.out->wait_consumed(w.out->last_seq(), w.send_st);
     HIP_OK(hipStreamSynchronize(w.send_st));
   } else {
     w.in->recv(bcast_dev_, bytes, w.recv_st);
@@ -1021,6 +1059,7 @@ void Engine::ring_bcast_from_last(std::vector<int32_t>& v) {
     HIP_OK(hipMemcpy(v.data(), bcast_dev_, bytes, hipMemcpyDeviceToHost));
     if (fwd) {
       w.out->send(bcast_dev_, bytes, w.send_st);
+      w.out->wait_consumed(w.out->last_seq(), w.send_st);
       HIP_OK(hipStreamSynchronize(w.send_st));
     }
   }

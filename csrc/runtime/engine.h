@@ -123,6 +123,7 @@ class Engine {
     hipStream_t send_st = nullptr, recv_st = nullptr;
     std::vector<hipEvent_t> comp_ev, sent_ev, recv_ev;
     std::vector<bool> sent_valid;
+    std::vector<uint64_t> sent_seq;   // Link::last_seq() of each micro-batch's last send
     std::vector<hipEvent_t> tok_ev;   // last stage: per (round, mb) timing events
     std::vector<double> tok_t;        // CPU backend: host timestamps of the same
     std::vector<bool> ring_pending;   // CPU backend, first stage: ring token not yet received

@@ -60,9 +60,6 @@ HipStage::HipStage(const ModelConfig& cfg, const StageSpec& spec, const StageOpt
 HipStage::~HipStage() {
   (void)hipSetDevice(spec_.device);
   destroy_graphs();
-  if (pf_st_) (void)hipStreamDestroy(pf_st_);
-  if (pf_fork_) (void)hipEventDestroy(pf_fork_);
-  if (pf_join_) (void)hipEventDestroy(pf_join_);
   for (void* p : allocs_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -501,8 +498,6 @@ void HipStage::alloc_runtime() {
     ml_part_ = (float*)zalloc((size_t)n_split_ * B * Hq * 2 * 4);
   }
   attn_cnt_ = (int32_t*)zalloc((size_t)std::max(B, 16) * Hkv * 4);
-  chain_cnt_ = (int32_t*)zalloc(16 * 4);
-  pf_sink_ = (uint32_t*)zalloc(64 * 4);
   if (opt_.prefill_flash && opt_.max_ctx > 256) {   // prefill KV-split partials (attn_prefill.hip)
     pf_opart_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * Dp_ * 4);
     pf_ml_ = (float*)zalloc((size_t)kPrefillMaxSplit * opt_.prefill_chunk * Hq * 2 * 4);
@@ -513,11 +508,7 @@ void HipStage::alloc_runtime() {
     auto acc = [&](const PackedMat& m) {
       if (!m.d || is16(m.ptype)) return;
       for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
-        if (M > 4 && M <= 64 && knob(KNOB_GEMV_SKSTORE)) {   // the GEMV's partial stores (gemv)
-          const int ns = det_splits((int)m.dims.ntiles, (int)m.dims.nsb, M, EPI_ATOMIC);
-          if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
-        }
-        if (M <= (knob(KNOB_GEMM4_M64) ? 32 : 64)) continue;
+        if (M <= 64) continue;
         int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
         if (opt_.prefill_gemm_v == 4 || opt_.prefill_gemm_v == 0)
           ns = std::max(ns, gemm4_splits(m.ptype, (int)m.dims.ntiles, (int)m.dims.nsb, M));
@@ -764,11 +755,7 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     launch_gemm3(P_I8, epi, p, st, allow_split && !opt_.deterministic);
     return;
   }
-  // (opt-in, knob GEMM4_M64: 33-64 row micro-batches on gemm4's 64-row tiles, where the GEMV's MFMA
-  // time is exposed -- PERFORMANCE.md 'Why the 70B mb64 GEMV did not move further')
-  const bool g4m64 = M > 32 && M <= 64 && !extras && !is16(m.ptype) && knob(KNOB_GEMM4_M64) && opt_.prefill_gemm &&
-                     opt_.prefill_gemm_v == 0 && gemm4_supported(m.ptype);
-  if ((M > 64 || g4m64) && opt_.prefill_gemm && gv == 4 && gemm4_supported(m.ptype)) {
+  if (M > 64 && opt_.prefill_gemm && gv == 4 && gemm4_supported(m.ptype)) {
     // v4 GEMM (gemm4.hip: 32x32x16 MFMA): split-K shapes store per-split partials like v2 (into the
     // residual x: absorbed by the next RMSNorm), the rest run whole-K
     GemvParams p{};
@@ -827,21 +814,6 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     p.n_valid = n_valid;
     const int nsplit = allow_split ? gemv_auto_split(p.ntiles, p.nsb, p.M, epi) : 1;
     const int ns = det_splits(p.ntiles, p.nsb, p.M, epi, allow_split);
-    // split-K through per-split partial stores instead of float atomics (knob GEMV_SKSTORE; 5-64
-    // rows, one slice): the o / down partials go to the next RMSNorm of x (norm_x), the qkv ones
-    // through one reduction -- the same scheme as the M > 64 GEMMs
-    if (!opt_.deterministic && knob(KNOB_GEMV_SKSTORE) && opt_.gemm_splitk_store && sk_part_ && epi == EPI_ATOMIC &&
-        ns > 1 && M <= 64 && !extras && (size_t)ns * p.M * p.ntiles * 16 <= sk_part_n_) {
-      const int ldp = p.ntiles * 16;
-      const bool defer = Y == sk_defer_;
-      flush_sk(st);   // the scratch is about to be overwritten
-      GemvParams q = p;
-      q.Y = sk_part_; q.ldy = ldp; q.split_stride = (int64_t)p.M * ldp;
-      launch_gemv(m.ptype, EPI_STORE, q, ns, st);
-      if (defer) sk_pend_ = SkPending{Y, p.M, n_valid, ldy, ns, ldp, (int64_t)p.M * ldp};
-      else launch_splitk_reduce(sk_part_, ns, (int64_t)p.M * ldp, ldp, p.M, n_valid, p.Y, ldy, st);
-      continue;
-    }
     if (opt_.deterministic && epi == EPI_ATOMIC && ns > 1) {
       // split s stores its partial to det_part_[s]; then one fixed-order reduction adds them into Y
       const int ldp = p.ntiles * 16;
@@ -956,10 +928,20 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
   const LayerW& L = layers_[li];
   const int d = cfg_.d_model;
   if (small_path(M)) {
-    if (decode) prefetch_layer(li, st);
     // gemvs: RMSNorms fused into the qkv / gate-up GEMVs, complete outputs per workgroup (q|k|v
     // stored with its bias, o / down added into the residual by their single owner)
     const bool two = knob(KNOB_GEMVS2) != 0;
+    // decode: RoPE and the KV append in the qkv GEMV's epilogue (QkvAppend), so the attention starts
+    // from rotated q and a complete cache (no dependent position -> page -> append chain of its own)
+    const bool pre = decode && opt_.fused_attn && knob(KNOB_ATTN_PRE) && !opt_.deterministic &&
+                     !(opt_.attn_o_max_ctx > 0 && opt_.max_ctx <= opt_.attn_o_max_ctx) &&
+                     attn_decode_pre_ok(decode_attn_params(li, M, pos, slot, false));
+    QkvAppend qa{};
+    if (pre) {
+      qa.pos = pos; qa.slot0 = dec_slot0_; qa.block_table = block_table_; qa.max_pages = max_pages_;
+      qa.rope_cs = rope_cs_; qa.k_cache = kc_[li]; qa.v_cache = vc_[li];
+      qa.Hq = cfg_.n_head; qa.Hkv = cfg_.n_head_kv; qa.hd = cfg_.head_dim; qa.Dp = Dp_; qa.kv_fp8 = opt_.kv_fp8;
+    }
     const int first = L.qkv.size() == 2 && gemvs2_supported(L.qkv[1].m.ptype, L.qkv[0].m.ptype) ? 1 : 0;
     if (two && L.qkv.size() == 2 && gemvs2_supported(L.qkv[first].m.ptype, L.qkv[1 - first].m.ptype) &&
         L.qkv[0].m.dims.nsb == L.qkv[1].m.dims.nsb) {
@@ -972,17 +954,19 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
         q.ntiles = (int)sg.m.dims.ntiles; q.nsb = (int)sg.m.dims.nsb; q.n_valid = (int)sg.m.dims.N;
         q.bias = L.qkv_bias ? L.qkv_bias + sg.y_off : nullptr;
         q.Xf = x; q.ldxf = d; q.gamma = L.attn_norm; q.eps = cfg_.eps; q.d_norm = d;
+        if (pre) { q.qa = qa; q.qa.col0 = (int)sg.y_off; }
       }
       launch_gemvs2(L.qkv[first].m.ptype, L.qkv[1 - first].m.ptype, ps[0], ps[1], st);
     } else {
-      for (const MatSeg& s : L.qkv)
+      for (const MatSeg& s : L.qkv) {
+        QkvAppend q = qa;
+        q.col0 = (int)s.y_off;
         gemv_small(s.m, EPI_STORE, nullptr, 0, x, L.attn_norm, M, qkv_ + s.y_off, qkv_n_, nullptr, 0, (int)s.m.dims.N,
-                   L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st);
+                   L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st, pre ? &q : nullptr);
+      }
     }
     if (!(decode && attention_o(li, M, pos, slot, x, st))) {
-      attention(li, M, pos, kvlen, slot, decode, st, false);
-      // o -> gate/up -> down as one chained launch (knob GEMVS_CHAIN; falls back when unsupported)
-      if (knob(KNOB_GEMVS_CHAIN) && chain_layer(L, M, x, st)) return;
+      attention(li, M, pos, kvlen, slot, decode, st, false, pre);
       gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
     }
     if (L.moe) {
@@ -1083,21 +1067,27 @@ bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slo
   return true;
 }
 
-void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
-                         hipStream_t st, bool qkv_deferred) {
+// the fused decode attention's parameters for layer li (decode rows: slots dec_slot0_ + t)
+DecodeAttnParams HipStage::decode_attn_params(int li, int M, const int32_t* pos, const int32_t* slot,
+                                              bool qkv_deferred) const {
   const LayerW& L = layers_[li];
-  const int d = cfg_.d_model;
-  (void)d;
+  DecodeAttnParams dp{};
+  dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
+  dp.slot0 = dec_slot0_;
+  dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
+  dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
+  dp.kv_fp8 = opt_.kv_fp8;
+  dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
+  dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
+  if (qkv_deferred) { dp.ssq = ssq_; dp.eps = cfg_.eps; dp.d_model = cfg_.d_model; dp.bias = L.qkv_bias; }
+  return dp;
+}
+
+void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
+                         hipStream_t st, bool qkv_deferred, bool pre) {
   if (decode && opt_.fused_attn) {
-    DecodeAttnParams dp{};
-    dp.qkv = qkv_; dp.ldqkv = qkv_n_; dp.pos = pos; dp.slot = slot; dp.block_table = block_table_;
-    dp.slot0 = decode ? dec_slot0_ : -1;
-    dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
-    dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
-    dp.kv_fp8 = opt_.kv_fp8;
-    dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = opt_.attn_split_len; dp.n_split = n_split_;
-    dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
-    if (qkv_deferred) { dp.ssq = ssq_; dp.eps = cfg_.eps; dp.d_model = d; dp.bias = L.qkv_bias; }
+    DecodeAttnParams dp = decode_attn_params(li, M, pos, slot, qkv_deferred);
+    dp.pre = pre;
 #ifdef MIPIPE_TIMING_PROBES
     dp.probe = knob(KNOB_ATTN_PROBE);
 #endif
@@ -1178,29 +1168,11 @@ void HipStage::attention(int li, int M, const int32_t* pos, const int32_t* kvlen
   }
 }
 
-bool HipStage::chain_layer(const LayerW& L, int M, float* x, hipStream_t st) {
-  if (M != 1 || L.moe || !L.fused_gateup || opt_.deterministic || !chain_cnt_) return false;
-  const int d = cfg_.d_model;
-  GemvsChainPhase ph[3];
-  auto mat = [](GemvParams& p, const PackedMat& m) {
-    p.W = m.d; p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb;
-  };
-  ph[0] = GemvsChainPhase{L.wo.ptype, EPI_ATOMIC, GemvParams{}};
-  mat(ph[0].p, L.wo);
-  ph[0].p.X = attn_; ph[0].p.ldx = Ko_; ph[0].p.M = M; ph[0].p.Y = x; ph[0].p.ldy = d; ph[0].p.n_valid = d;
-  ph[1] = GemvsChainPhase{L.gateup.ptype, EPI_SWIGLU, GemvParams{}};
-  mat(ph[1].p, L.gateup);
-  ph[1].p.M = M; ph[1].p.H = h_; ph[1].p.ldh = Kff_; ph[1].p.n_valid = cfg_.d_ff;
-  ph[1].p.Xf = x; ph[1].p.ldxf = d; ph[1].p.gamma = L.ffn_norm; ph[1].p.eps = cfg_.eps; ph[1].p.d_norm = d;
-  ph[2] = GemvsChainPhase{L.down.ptype, EPI_ATOMIC, GemvParams{}};
-  mat(ph[2].p, L.down);
-  ph[2].p.X = h_; ph[2].p.ldx = Kff_; ph[2].p.M = M; ph[2].p.Y = x; ph[2].p.ldy = d; ph[2].p.n_valid = d;
-  return launch_gemvs_chain(ph, 3, chain_cnt_, chain_cnt_ + 8, st);
-}
-
 void HipStage::gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, const float* Xf, const float* gamma,
-                          int M, float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st) {
+                          int M, float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st,
+                          const QkvAppend* qa) {
   GemvParams p{};
+  if (qa) p.qa = *qa;
   p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
   p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid; p.bias = bias;
   if (Xf) { p.Xf = Xf; p.ldxf = cfg_.d_model; p.gamma = gamma; p.eps = cfg_.eps; p.d_norm = cfg_.d_model; }
@@ -1311,50 +1283,9 @@ void HipStage::decode_eager(int mb, hipStream_t st) {
   dec_slot0_ = slot_of(mb, 0);   // slot_[mb] holds slot_of(mb, b) = dec_slot0_ + b
   for (size_t li = 0; li < layers_.size(); ++li)
     layer_forward((int)li, B, x, pos_[mb], kvlen_[mb], slot_[mb], true, st);
-  prefetch_join(st);
   flush_sk(st);
   if (spec_.last()) head(mb, B, x, tok_[mb], (uint64_t)mb + 1, st);
   launch_advance(pos_[mb], kvlen_[mb], B, mb == 0 ? step_ : nullptr, st);
-}
-
-// The single stream's GEMVs are latency-bound except gate/up and down, and those read up to ~25 %
-// faster from the 256 MiB Infinity Cache (profiles/r2w_gemv_mall_hot_cold.txt): while qkv,
-// attention and o leave HBM idle, a side stream reads this layer's o / gate-up / down and the next
-// layer's qkv into the MALL.  Layers over 160 MB (70B: 0.43 GB) would evict themselves: no prefetch.
-// The side stream is forked per layer (an event on the compute stream) and joined once per decode
-// step (prefetch_join), so a captured graph holds it as a parallel branch.
-void HipStage::prefetch_layer(int li, hipStream_t st) {
-  const int grid = knob(KNOB_PREFETCH);
-  const LayerW& L = layers_[li];
-  if (grid <= 0 || L.moe || !L.fused_gateup || !pf_sink_) return;
-  PrefetchArgs a{};
-  auto add = [&](const PackedMat& m) {
-    if (m.d && a.n < 6) { a.p[a.n] = m.d; a.bytes[a.n] = m.bytes(); ++a.n; }
-  };
-  add(L.wo);
-  add(L.gateup);
-  add(L.down);
-  if (li + 1 < (int)layers_.size())
-    for (const MatSeg& sg : layers_[li + 1].qkv) add(sg.m);
-  uint64_t total = 0;
-  for (int i = 0; i < a.n; ++i) total += a.bytes[i];
-  if (total > ((uint64_t)160 << 20)) return;
-  if (!pf_st_) {
-    HIP_OK(hipStreamCreateWithFlags(&pf_st_, hipStreamNonBlocking));
-    HIP_OK(hipEventCreateWithFlags(&pf_fork_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&pf_join_, hipEventDisableTiming));
-  }
-  HIP_OK(hipEventRecord(pf_fork_, st));
-  HIP_OK(hipStreamWaitEvent(pf_st_, pf_fork_, 0));
-  launch_prefetch(a, grid, pf_sink_, pf_st_);
-  pf_open_ = true;
-}
-
-void HipStage::prefetch_join(hipStream_t st) {
-  if (!pf_open_) return;
-  HIP_OK(hipEventRecord(pf_join_, pf_st_));
-  HIP_OK(hipStreamWaitEvent(st, pf_join_, 0));
-  pf_open_ = false;
 }
 
 void HipStage::capture_graphs() {

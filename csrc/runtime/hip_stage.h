@@ -136,11 +136,13 @@ class HipStage : public Stage {
   const void* xq_src_ = nullptr; int xq_rows_ = 0;   // the f16 rows xq_ currently holds (set by norm_x / the quant)
   bool attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st);
   void attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
-                 hipStream_t st, bool qkv_deferred);
+                 hipStream_t st, bool qkv_deferred, bool pre = false);
+  DecodeAttnParams decode_attn_params(int li, int M, const int32_t* pos, const int32_t* slot, bool qkv_deferred) const;
   bool small_path(int M) const { return opt_.small_gemv && M <= 4; }
   // gemvs (M <= 4): Xf != nullptr fuses the RMSNorm of the f32 rows Xf with gamma
   void gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, const float* Xf, const float* gamma, int M,
-                  float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st);
+                  float* Y, int ldy, f16* H, int ldh, int n_valid, const float* bias, hipStream_t st,
+                  const QkvAppend* qa = nullptr);
   size_t kv_eb() const { return opt_.kv_fp8 ? 1 : 2; }   // bytes per cached K/V element
   int det_splits(int ntiles, int nsb, int M, int epi, bool allow_split = true) const;   // RMSNorm folded into the consuming GEMVs at this row count
   void flush_sk(hipStream_t st);
@@ -209,16 +211,6 @@ class HipStage : public Stage {
   float* sk_defer_ = nullptr;   // gemv(): ATOMIC GEMMs into this buffer defer their reduction
   float* o_part_ = nullptr; float* ml_part_ = nullptr; int n_split_ = 1;
   int32_t* attn_cnt_ = nullptr;   // fused decode attention: split arrival counters
-  int32_t* chain_cnt_ = nullptr;  // chained o -> gate/up -> down (launch_gemvs_chain): [0..3] counters, [8] error flag
-  bool chain_layer(const LayerW& L, int M, float* x, hipStream_t st);
-  // MALL prefetch (knob PREFETCH, single stream): a side stream forked at each layer's start reads
-  // that layer's o / gate-up / down and the next layer's qkv while qkv / attention / o run
-  hipStream_t pf_st_ = nullptr;
-  hipEvent_t pf_fork_ = nullptr, pf_join_ = nullptr;
-  uint32_t* pf_sink_ = nullptr;
-  bool pf_open_ = false;   // a fork not yet joined back into the compute stream
-  void prefetch_layer(int li, hipStream_t st);
-  void prefetch_join(hipStream_t st);
   // MoE scratch
   float* moe_logits_ = nullptr; int32_t* moe_counts_ = nullptr; int32_t* moe_lists_ = nullptr;
   float* moe_w_ = nullptr; f16* moe_h_ = nullptr;

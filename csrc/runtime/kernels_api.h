@@ -11,6 +11,21 @@ namespace mp {
 
 enum Epilogue : int { EPI_STORE = 0, EPI_ATOMIC = 1, EPI_SWIGLU = 2 };
 
+// Decode q|k|v epilogue of the small-M GEMV (gemvs, single stream): instead of storing raw q|k|v
+// for the attention to rotate and append, the GEMV applies RoPE to q (stored rotated, f32, into Y)
+// and to k, and appends k and v to the paged KV cache itself.  Its loads of pos, the block-table
+// entry and the cos/sin pair are issued at kernel start, under the weight stream, so the decode
+// attention that follows starts with only the block table and its K/V pages to wait for.
+struct QkvAppend {
+  const int32_t* pos = nullptr;    // [M]; nullptr: plain STORE epilogue
+  int slot0 = 0;                   // row m's slot is slot0 + m
+  const int32_t* block_table = nullptr; int max_pages = 0;
+  const float2* rope_cs = nullptr; // [max_pos][hd / 2] (cos, sin)
+  f16* k_cache = nullptr; f16* v_cache = nullptr;   // K [page][Hkv][64][Dp], V^T [page][Hkv][Dp][64]
+  int Hq = 0, Hkv = 0, hd = 0, Dp = 0, kv_fp8 = 0;
+  int col0 = 0;                    // q|k|v column of this GEMV's output column 0
+};
+
 struct GemvParams {
   const uint8_t* W;      // T16-packed weights
   const f16* X;          // activations [M][ldx] (K_pad columns, zero tail)
@@ -41,6 +56,9 @@ struct GemvParams {
   // P_I8 (launch_gemm3): X holds int8 rows (ldx in bytes), y = xscale[m] * wscale[n] * sum(xq * wq)
   const float* xscale = nullptr;
   const float* wscale = nullptr;
+  int rpf = 0;                   // gemvs ATOMIC, one split: residual loaded at kernel start (knob GEMVS_RPF)
+  QkvAppend qa;                  // gemvs STORE + fused norm: RoPE + KV append epilogue (qa.pos set)
+  int probe = 0;                 // timing probes only (knob GEMVS_PROBE, `make PROBES=1`)
 };
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st);
@@ -54,22 +72,6 @@ bool gemvs2_supported(int pt, int pt2);
 void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st);
 void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStream_t st, int force_G = 0,
                   int force_split = 0);
-// Chained single-stream GEMVs (gemvs.hip gemvs_chain_kernel): 2 or 3 consecutive gemvs launches as
-// ONE launch whose phases hand off through sc1 stores + agent counters, each phase's weights in
-// flight before it waits for the previous one.  Supported chain: [EPI_ATOMIC (Q4_K) ->] EPI_SWIGLU
-// (Q4_K, fused RMSNorm) -> EPI_ATOMIC (Q4_K | Q6_K), M == 1 -- the o -> gate/up -> down of a decode
-// layer.  cnt: 4 device ints, zero before the first launch (the kernel re-arms them); err: a device
-// int set to 1 if a poll gave up (bounded spin).  Returns false (nothing launched) when the shape is
-// not supported or the phases cannot all be resident at once.
-struct GemvsChainArgs {
-  GemvParams p[3];
-  int start[4];          // phase i owns blocks [start[i], start[i+1])
-  int32_t* cnt;
-  int32_t* err;
-};
-struct GemvsChainPhase { int ptype, epi; GemvParams p; };
-bool launch_gemvs_chain(const GemvsChainPhase* ph, int n, int32_t* cnt, int32_t* err, hipStream_t st,
-                        int* wgs_out = nullptr);
 void set_gemv_tpw(int tiles_per_wave);    // M > 32 tiles per wave: 0 = auto, 1, 2 (tuning knob)
 int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)
@@ -228,10 +230,13 @@ struct DecodeAttnParams {
   // * qkv + bias (bias optional, [q|k|v])
   const float* ssq = nullptr; float eps = 0.f; int d_model = 0; const float* bias = nullptr;
   int kv_fp8 = 0;                  // caches hold e4m3 bytes (kv_dtype "fp8")
+  int pre = 0;                     // q already rotated, new K / V already appended (gemvs QkvAppend)
   int probe = 0;                   // timing probes only (knob ATTN_PROBE): bit 0 skips the global V append,
                                    // bit 1 the K append (results wrong; never in production runs)
 };
 void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st);
+// the launch would take the one-split workgroup kernel that accepts pre-appended inputs (p.pre)
+bool attn_decode_pre_ok(const DecodeAttnParams& p);
 // Fused decode attention + output projection (single stream, M <= 4, one KV split): workgroup
 // (r, kvh) runs the attention of kv head kvh's query heads, then adds their split-K slice of W_o
 // (output tiles [r * 8, r * 8 + 8), k in the heads' dims) into Y with atomics.
@@ -272,14 +277,6 @@ struct PenaltyParams {
 void launch_penalize(const PenaltyParams& p, hipStream_t st);
 // append tokens[m] to row m's ring: hist[m][cnt[m] % last_n] = tokens[m]; ++cnt[m]
 void launch_hist_push(int32_t* hist, int32_t* cnt, int last_n, const int32_t* tokens, int M, hipStream_t st);
-
-// read up to 6 byte ranges into the Infinity Cache (MALL); sink: >= 64 device u32 (never read)
-struct PrefetchArgs {
-  const void* p[6];
-  uint64_t bytes[6];
-  int n;
-};
-void launch_prefetch(const PrefetchArgs& a, int grid, uint32_t* sink, hipStream_t st);
 
 // pos[i] += 1, kvlen[i] = pos[i] + 1 for i < M (graph-resident decode step advance)
 void launch_advance(int32_t* pos, int32_t* kvlen, int M, int32_t* step, hipStream_t st);

@@ -277,8 +277,10 @@ void Session::serve(const std::function<std::vector<Served>(int free)>& next) {
       std::vector<int32_t> pr = m->prompt;
       pr.insert(pr.end(), m->res.tokens.begin(), m->res.tokens.end());
       const int pages = pages_for((long)m->prompt.size(), m->s.req.n_predict);
+      // the pool test matches fresh admission (pages_for clamps to the pool and the request stops at
+      // "context" once its share fills): what it holds now plus its next token must fit the pool
       const bool ctx_ok = (int)pr.size() + 1 < max_ctx,
-                 pool_ok = pages_need((long)m->prompt.size(), m->s.req.n_predict) <= pool;
+                 pool_ok = ((long)pr.size() + 1 + 63) / 64 <= (long)pool;
       if ((int)prompts.size() < cap && ctx_ok && reserved + pages <= pool) {
         m->pages = pages;
         reserved += pages;

@@ -23,6 +23,8 @@ struct StageOptions {
   bool use_graphs = true;
   int attn_split_len = 0;   // decode flash-decoding split length (multiple of 128; 0 = auto)
   int threads = 0;          // CPU backend worker threads (0 = hardware concurrency)
+  bool cpu_q8 = true;       // CPU backend: quantized weights x int8 activation blocks (cpu_qdot.cpp); false: f32
+                            // dequant + f32 dot (exact to the fp32 oracle)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
   int attn_o_max_ctx = 0;     // single-stream decode: attention + o-projection in one launch up to this max_ctx (0 = off)
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs

@@ -39,15 +39,15 @@ LocalLink::LocalLink(int src_device, int dst_device) : src_dev_(src_device), dst
     (void)hipGetLastError();
   }
   HIP_OK(hipSetDevice(src_dev_));
-  HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  for (auto& e : ready_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_OK(hipSetDevice(dst_dev_));
-  HIP_OK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  for (auto& e : done_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_OK(hipSetDevice(cur));
 }
 
 LocalLink::~LocalLink() {
-  (void)hipEventDestroy(ready_);
-  (void)hipEventDestroy(done_);
+  for (auto e : ready_) (void)hipEventDestroy(e);
+  for (auto e : done_) (void)hipEventDestroy(e);
 }
 
 void LocalLink::abort() {
@@ -59,20 +59,26 @@ void LocalLink::abort() {
 void LocalLink::send(const void* buf, size_t bytes, hipStream_t st) {
   const auto to = std::chrono::milliseconds((long)(timeout_s * 1000));
   std::unique_lock<std::mutex> l(mu_);
+  if (!cv_.wait_for(l, to, [&] { return aborted_ || posted_ - taken_ < (uint64_t)kDepth; }))
+    throw std::runtime_error("LocalLink: send timed out (receiver stalled, queue full)");
   if (aborted_) throw std::runtime_error("LocalLink: aborted");
-  HIP_OK(hipEventRecord(ready_, st));
-  src_ = buf;
-  bytes_ = bytes;
-  const uint64_t me = ++posted_;
+  const int slot = (int)(posted_ % kDepth);   // its previous message was taken: its events are free
+  HIP_OK(hipEventRecord(ready_[slot], st));
+  src_[slot] = buf;
+  bytes_[slot] = bytes;
+  ++posted_;
   cv_.notify_all();
-  // the receiver enqueues its copy of THIS message (taken_ == me) before the sender goes on
-  if (!cv_.wait_for(l, to, [&] { return aborted_ || taken_ >= me; }))
-    throw std::runtime_error("LocalLink: send timed out (peer stalled)");
-  if (aborted_) throw std::runtime_error("LocalLink: aborted");
-  // the sender's stream (and so its sent_ev) orders after the copy: the buffer is reusable
-  HIP_OK(hipStreamWaitEvent(st, done_, 0));
   bytes_sent += bytes;
   ++msgs_sent;
+}
+
+void LocalLink::wait_consumed(uint64_t seq, hipStream_t st) {
+  if (seq == 0) return;
+  std::unique_lock<std::mutex> l(mu_);
+  if (!cv_.wait_for(l, std::chrono::milliseconds((long)(timeout_s * 1000)), [&] { return aborted_ || taken_ >= seq; }))
+    throw std::runtime_error("LocalLink: buffer reuse timed out (receiver stalled)");
+  if (aborted_) throw std::runtime_error("LocalLink: aborted");
+  HIP_OK(hipStreamWaitEvent(st, done_[(seq - 1) % kDepth], 0));
 }
 
 void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
@@ -81,10 +87,11 @@ void LocalLink::recv(void* buf, size_t bytes, hipStream_t st) {
                     [&] { return aborted_ || posted_ > taken_; }))
     throw std::runtime_error("LocalLink: recv timed out (peer stalled)");
   if (aborted_) throw std::runtime_error("LocalLink: aborted");
-  if (bytes_ != bytes) throw std::runtime_error("LocalLink: message size mismatch");
-  HIP_OK(hipStreamWaitEvent(st, ready_, 0));
-  HIP_OK(hipMemcpyAsync(buf, src_, bytes, hipMemcpyDefault, st));
-  HIP_OK(hipEventRecord(done_, st));
+  const int slot = (int)(taken_ % kDepth);
+  if (bytes_[slot] != bytes) throw std::runtime_error("LocalLink: message size mismatch");
+  HIP_OK(hipStreamWaitEvent(st, ready_[slot], 0));
+  HIP_OK(hipMemcpyAsync(buf, src_[slot], bytes, hipMemcpyDefault, st));
+  HIP_OK(hipEventRecord(done_[slot], st));
   ++taken_;
   cv_.notify_all();
 }

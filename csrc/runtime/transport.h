@@ -32,6 +32,13 @@ class Link {
   // ncclCommCount); 0 for transports without one
   virtual int comm_nranks() const { return 0; }
   virtual void abort() {}
+  // Buffer reuse for transports whose send() returns before the bytes have left the sender's buffer
+  // (LocalLink's posted queue): last_seq() numbers the latest send; wait_consumed(seq, st) makes
+  // stream st wait until message seq has been copied out, so st may overwrite its buffer.  For
+  // stream-ordered transports (RCCL) and copying ones (TCP, host) the send stream's own order
+  // already covers it: both are no-ops.
+  virtual uint64_t last_seq() const { return 0; }
+  virtual void wait_consumed(uint64_t seq, hipStream_t st) { (void)seq; (void)st; }
   // blocking waits give up after this long (a dead or stalled peer surfaces as an error)
   virtual void set_timeout(double s) { timeout_s = s; }
   double timeout_s = 600;
@@ -39,29 +46,35 @@ class Link {
 };
 
 // ---------------------------------------------------------------- LocalLink
-// A rendezvous: send() publishes (buffer, ready event) and blocks the sending HOST thread until
-// the receiver has enqueued its copy; it then makes the sender's stream wait for that copy, so
-// the engine's sent_ev (recorded after send) keeps the buffer alive exactly as long as needed.
-// Host threads only meet at enqueue points (the GPU work stays asynchronous), and every stage
-// issues its link operations in the global (round, micro-batch) order, so the ring cannot
-// deadlock on the rendezvous.  Both ends may be on the same device.
+// A posted queue of up to kDepth messages: send() records the message's ready event on the sender's
+// stream, posts (buffer, bytes) and returns at once (it blocks only while kDepth messages are still
+// untaken: back-pressure); recv() makes the receiver's stream wait for that ready event and copies
+// straight out of the sender's buffer (ONE device copy, peer read over xGMI between GPUs), recording
+// the message's done event.  The sender keeps its buffer until wait_consumed(seq, st) -- a host wait
+// for the receiver to have enqueued message seq (normally long done: the engine reuses a micro-
+// batch's buffer one round later) plus a stream wait on its done event.  Copies of one link run in
+// order on the receiver's stream, so a done event re-recorded by a later message still covers the
+// earlier copy.  Both ends may be on the same device (1-GPU rehearsal of PP = S).
 class LocalLink : public Link {
  public:
+  static constexpr int kDepth = 64;
   LocalLink(int src_device, int dst_device);
   ~LocalLink() override;
   void send(const void* buf, size_t bytes, hipStream_t st) override;
   void recv(void* buf, size_t bytes, hipStream_t st) override;
   const char* kind() const override { return "local"; }
   void abort() override;
+  uint64_t last_seq() const override { return posted_; }
+  void wait_consumed(uint64_t seq, hipStream_t st) override;
   bool peer() const { return src_dev_ != dst_dev_; }
 
  private:
   int src_dev_, dst_dev_;
-  hipEvent_t ready_ = nullptr;   // on the sender's device: the message's bytes are final
-  hipEvent_t done_ = nullptr;    // on the receiver's device: the copy has completed
-  const void* src_ = nullptr;
-  size_t bytes_ = 0;
-  uint64_t posted_ = 0, taken_ = 0;   // message counters (posted_ - taken_ <= 1)
+  hipEvent_t ready_[kDepth] = {};   // sender's device: message bytes final
+  hipEvent_t done_[kDepth] = {};    // receiver's device: message copied
+  const void* src_[kDepth] = {};
+  size_t bytes_[kDepth] = {};
+  uint64_t posted_ = 0, taken_ = 0;   // message counters (1-based sequence numbers)
   std::mutex mu_;
   std::condition_variable cv_;
   bool aborted_ = false;

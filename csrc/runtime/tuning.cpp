@@ -38,11 +38,13 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMVS_MINWG", 256, 1, 1 << 20, nullptr},
     {"GEMVS_G", 0, 0, 8, g_ok},
     {"GEMVS_SPLIT", 0, 0, 1 << 16, nullptr},
+    {"GEMVS_RPF", 1, 0, 1, nullptr},
     {"MOE_V", 2, 1, 2, nullptr},
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},
     {"ATTN_WAVE", 2, 0, 2, nullptr},
     {"ATTN_WAVE_MIN", 512, 1, 1 << 30, nullptr},   // r10ac: mb64 at 8 kv heads (512 items) +2.5-3 %, mb32 (256) -2.3 %
+    {"ATTN_PRE", 1, 0, 1, nullptr},
     {"GEMM4_NW", 0, 0, 8, nw4_ok},
     {"GEMM4_SPREAD", 0, 0, 2, nullptr},
     {"GEMM4_WNT", 0, 0, 2, nullptr},
@@ -50,11 +52,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
-    {"GEMVS_CHAIN", 0, 0, 1, nullptr},
-    {"GEMM4_M64", 0, 0, 1, nullptr},
-    {"GEMV_SKSTORE", 0, 0, 1, nullptr},
     {"GEMM4_TW4", 1, 0, 3, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
-    {"PREFETCH", 0, 0, 4096, nullptr},
 #ifdef MIPIPE_TIMING_PROBES
 #include "timing_probes.inc"
 #endif

@@ -22,11 +22,13 @@ enum Knob : int {
   KNOB_GEMVS_MINWG,         // gemvs: fewest workgroups before halving the tiles per workgroup
   KNOB_GEMVS_G,             // gemvs: force tiles per workgroup (0 auto, 1, 2, 4, 8)
   KNOB_GEMVS_SPLIT,         // gemvs: force the k-split over the grid (0 auto)
+  KNOB_GEMVS_RPF,           // gemvs: single-owner ATOMIC epilogue from a residual loaded at kernel start (0 / 1)
   KNOB_MOE_V,               // MoE GEMV version (1 | 2)
   KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)
   KNOB_ATTN_WAVE,           // decode attention: the wave-per-item kernel (0 off, 1 on, 2 auto)
   KNOB_ATTN_WAVE_MIN,       // auto: (token, kv head, split) items at or above which it is taken
+  KNOB_ATTN_PRE,            // single stream: RoPE + KV append in the qkv GEMV's epilogue (0 / 1)
   KNOB_GEMM4_NW,            // gemm4: compute waves per workgroup of unsplit launches (0 auto, 7, 8; 4 = 128-row
                             // tiles of 4 waves, two workgroups per CU, split-K included)
   KNOB_GEMM4_SPREAD,        // gemm4: LDS-DMA issue after the stage barrier (0 burst, 1 spread over MFMA steps, 2 spread + waves 4-7 two steps later)
@@ -35,20 +37,15 @@ enum Knob : int {
   KNOB_GEMM3_BM,            // gemm3: force rows per workgroup (0 auto, 128, 256); A/B runs only
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
-  KNOB_GEMVS_CHAIN,         // single stream: o -> gate/up -> down as one chained launch (0 / 1)
-  KNOB_GEMM4_M64,           // decode micro-batches of 33-64 rows on gemm4's 64-row tiles instead of the GEMV (0 / 1)
-  KNOB_GEMV_SKSTORE,        // decode GEMV at 5-64 rows: split-K partial stores + the next norm's reduction instead of
-                            // atomics (0 / 1; r10af: 8B mb64 +2 %, 70B mb16-32 -6-8 %)
   KNOB_GEMM4_TW4,           // gemm4 dense: 4 waves x 64 columns (two MFMAs per A fragment) instead of 8 x 32
                             // (0 off, 1 the 256-row tiles only, 2 also the 128-row tiles, 3 = 1 + the 128-row MoE tiles)
-  KNOB_PREFETCH,            // single stream: side-stream MALL prefetch of each layer's o / gate-up / down and the next
-                            // qkv, this many workgroups (0 = off)
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes that skip work (wrong results): only in a `make PROBES=1` build, never in the
   // default library, so no environment variable can corrupt a serving or bench run
   KNOB_GEMM3_PROBE,         // gemm3 timing probes (Q4_K SwiGLU 256x256 only; 0 = the real kernel)
   KNOB_ATTN_PROBE,          // decode attention timing probes (1: no V append, 2: no K append; 0 = real)
   KNOB_GEMM4_PROBE,         // gemm4 timing probes (Q4_K, dense): bit 0 no dequant, 1 no MFMA, 2 no LDS-DMA
+  KNOB_GEMVS_PROBE,         // gemvs timing probes: bit 0 no dequant / MFMA, 1 no x prologue, 2 plain epilogue store
 #endif
   KNOB_COUNT
 };

@@ -20,7 +20,8 @@ struct CliOptions {
   Json eng = Json::object();  // engine config
   std::string prompt = "Once upon a time";
   int n_predict = 200;        // reference: -n 200 (main.rs:44)
-  int ngl = 99;               // reference: -ngl 99 (main.rs:50); 0 = CPU backend; < n_layer: hybrid
+  int ngl = -1;               // -1 (no -ngl): every layer on the GPUs; reference -ngl 99 (main.rs:50) means the
+                              // same; 0 = CPU backend; 0 < N < n_layer: hybrid (the first n_layer - N on the CPU)
   bool verbose = false;
   bool echo_prompt = true;
   bool bench = false;
@@ -82,13 +83,14 @@ inline void print_common_usage(FILE* f) {
           "  --draft-max K             speculative decoding by prompt lookup: up to K drafted tokens per\n"
           "                            verify round (greedy; --lookup-ngram N, default 3)\n"
           "placement / pipeline:\n"
-          "  -ngl, --n-gpu-layers N    layers offloaded to the GPU stages (default 99 = all); 0 = CPU backend;\n"
+          "  -ngl, --n-gpu-layers N    layers offloaded to the GPU stages (default: all); 0 = CPU backend;\n"
           "                            0 < N < n_layer: the first n_layer - N layers run on a CPU stage in front\n"
           "  --stages N, --pp N        pipeline stages (one GPU each)\n"
           "  --devices 0,1,..          GPU of each stage (repeat a GPU to emulate PP on one device)\n"
           "  --micro-batches M         micro-batches in flight;  --mb-size B sequences per micro-batch\n"
           "  --split even|mem|cost     layer partitioner (default cost)\n"
           "  --link local|rccl|tcp     stage transport;  --prefill-chunk N;  --no-graphs;  --threads N\n"
+          "  --cpu-act q8|f32          CPU stages: integer dots on int8 activation blocks (default) or f32\n"
           "  --no-prefix-cache         prefill every request in full (no KV reuse of a common prefix)\n"
           "  --kv-pool TOKENS          paged KV pool per stage;  --kv-dtype f16|fp8 (-ctk/-ctv) KV cache element type\n"
           "  --int8-gemm               batches > 64 rows on the int8 MFMA (per-row int8 activations and weights:\n"
@@ -147,6 +149,7 @@ inline CliOptions parse_cli(int argc, char** argv,
     else if (a == "--draft-max" || a == "--draft") e["draft_max"] = std::atoi(val().c_str());   // prompt-lookup speculation
     else if (a == "--lookup-ngram") e["lookup_ngram"] = std::atoi(val().c_str());
     else if (a == "--threads" || a == "-t") e["threads"] = std::atoi(val().c_str());
+    else if (a == "--cpu-act") e["cpu_act"] = val();   // CPU stages: q8 (integer dots, default) | f32
     else if (a == "--world") world = std::atoi(val().c_str());
     else if (a == "--rank") rank = std::atoi(val().c_str());
     else if (a == "--next") next = val();
@@ -177,7 +180,7 @@ inline CliOptions parse_cli(int argc, char** argv,
   if (!synthetic.empty()) e["synthetic"] = synthetic_arch(synthetic);
   if (!e.has("gguf") && !e.has("synthetic")) throw std::runtime_error("need -m FILE or --synthetic NAME");
   if (o.ngl == 0) e["backend"] = "cpu";
-  else if (o.ngl > 0) e["gpu_layers"] = o.ngl;   // >= n_layer: every layer on the GPUs
+  else if (o.ngl > 0) e["gpu_layers"] = o.ngl;   // explicit -ngl only: >= n_layer puts every layer on the GPUs
   if (stages > 0) e["stages"] = stages;
   if (!devices.empty()) {
     Json d = Json::array();

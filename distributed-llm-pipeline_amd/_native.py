@@ -36,6 +36,7 @@ _SIGS = {
     "mp_pack_type": ([c_int], c_int),
     "mp_pack_t16": ([c_int, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int], c_int),
     "mp_dequant_row": ([c_int, c_void_p, c_void_p, c_int64], c_int),
+    "mp_qdot_rows": ([c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p], c_int),
     "mp_partition": ([c_void_p, c_int, c_double, c_double, c_void_p, c_int, c_int, c_void_p], c_int),
     "mp_gguf_open": ([c_char_p], c_void_p),
     "mp_gguf_close": ([c_void_p], None),
@@ -84,9 +85,6 @@ _SIGS = {
                           c_void_p, c_int64, c_void_p], c_int),
     "mp_op_gemvs": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                      c_int, c_void_p, c_int, c_void_p, c_float, c_int, c_void_p, c_int, c_int, c_int, c_void_p], c_int),
-    "mp_op_gemvs_chain3": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                            c_int, c_void_p, c_float, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                            c_void_p], c_int),
     "mp_op_penalize": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float, c_void_p], c_int),
     "mp_op_hist_push": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_sample": ([c_void_p, c_int, c_int, c_int, c_float, c_int, c_float, c_float, ctypes.c_uint64, c_void_p,
@@ -115,6 +113,7 @@ _SIGS = {
     "mp_engine_tokens": ([c_void_p, c_void_p, c_int, c_int], c_int),
     "mp_engine_logits": ([c_void_p, c_int, c_void_p, c_int], c_int),
     "mp_rccl_unique_id": ([c_void_p], c_int),
+    "mp_local_link_selftest": ([c_int, c_int, c_int64, c_int, c_int], c_int),
     "mp_rccl_selftest": ([c_int, c_void_p, c_int, c_int], c_char_p),
     "mp_rccl_loop_start": ([c_int, c_int64, c_int], c_int),
     "mp_rccl_loop_wait": ([], c_double),
@@ -123,6 +122,16 @@ _SIGS = {
     "mp_init_packed": ([c_void_p, ctypes.c_size_t, c_int, c_float, ctypes.c_uint64, c_void_p], c_int),
     "mp_tok_pretokenize": ([c_char_p, c_int], c_char_p),
 }
+
+
+def _lib_newer_than_sources() -> bool:
+    lib_t = os.path.getmtime(LIB_PATH)
+    for sub in ("csrc/kernels", "csrc/runtime"):
+        d = os.path.join(REPO_DIR, sub)
+        for f in os.listdir(d):
+            if f.endswith((".hip", ".cpp", ".h", ".inc")) and os.path.getmtime(os.path.join(d, f)) > lib_t:
+                return False
+    return os.path.getmtime(os.path.join(REPO_DIR, "Makefile")) <= lib_t
 
 
 def _make(*extra, quiet=True):
@@ -138,6 +147,10 @@ def build(force: bool = False, quiet: bool = True) -> str:
     tested against newer sources."""
     if not force and os.path.exists(LIB_PATH) and os.environ.get("MIPIPE_LIB"):
         return LIB_PATH   # an explicitly selected A/B build is used as is
+    if not force and os.path.exists(LIB_PATH) and _lib_newer_than_sources():
+        # the in-tree library is newer than every native source: current (also on a GPU box whose
+        # snapshot carries the library but not the object files make would otherwise look for)
+        return LIB_PATH
     if not force and os.path.exists(LIB_PATH):
         try:
             if _make("-q", "all", quiet=True).returncode == 0:

@@ -164,19 +164,6 @@ def gemm_splitk(w: PackedWeight, x: torch.Tensor, y: torch.Tensor, v: int = 4, m
                    "gemm_splitk")
 
 
-def gemvs_chain3(wo: PackedWeight, wgu: PackedWeight, wdn: PackedWeight, attn: torch.Tensor, x: torch.Tensor,
-                 gamma: torch.Tensor, eps: float, h: torch.Tensor, cnt: torch.Tensor) -> int:
-    """One decode row's o -> gate/up -> down as ONE chained launch (gemvs.hip gemvs_chain_kernel):
-    x += o(attn); h = SwiGLU(gate/up(rmsnorm(x) gamma)); x += down(h).  attn f16 [1][wo.k_pad], x f32
-    [1][d] (updated in place), h f16 [1][wdn.k_pad], cnt int32 [16] zeroed once ([8]: the poll
-    give-up flag).  Returns the workgroups launched (0: the chain does not apply)."""
-    d, F = x.shape[1], wgu.n // 2
-    return N.check(N.lib().mp_op_gemvs_chain3(wo.ptype, _ptr(wo.dev), wo.ntiles, wo.nsb, _ptr(attn), attn.stride(0),
-                                               wgu.ptype, _ptr(wgu.dev), wgu.ntiles, wgu.nsb, _ptr(x), d, _ptr(gamma),
-                                               eps, _ptr(h), h.stride(0), F, wdn.ptype, _ptr(wdn.dev), wdn.ntiles,
-                                               wdn.nsb, _ptr(cnt), _stream()), "gemvs_chain3")
-
-
 def moe_route(logits: torch.Tensor, k: int, list_cap: int | None = None):
     """Top-k routing of router logits [M][E] (f32, contiguous): returns (counts [E], lists [E][list_cap]
     of token-slot ids t * k + j, renormalised top-k weights [M * k])."""

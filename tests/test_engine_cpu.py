@@ -30,28 +30,35 @@ def free_port():
 @pytest.mark.parametrize("name,ftype", [("stories15m", "F32"), ("tiny-gqa", "Q8_0"), ("tiny-gqa", "Q4_K_M"),
                                         ("tiny-l3", "Q6_K"), ("tiny-moe", "Q5_K_M"), ("tiny-gqa", "BF16"),
                                         ("tiny-qwen2", "Q4_K_M")])
-def test_cpu_engine_matches_reference(native, model_dir, name, ftype):
+@pytest.mark.parametrize("act", ["f32", "q8"])
+def test_cpu_engine_matches_reference(native, model_dir, name, ftype, act):
+    """cpu_act f32 (dequantized weights, f32 dots): the fp32 oracle to 1e-8.  cpu_act q8 (the default:
+    integer dots against int8 activation blocks, cpu_qdot.cpp): within the int8 rounding of the
+    activations, and the oracle's greedy token wherever its top-2 margin is clear."""
     from mipipe.engine import Engine
     from mipipe.models.reference import RefLlama
     path, cfg = make_model(model_dir, name, ftype)
     ref = RefLlama.from_gguf(path)
     rng = np.random.default_rng(0)
     prompt = [int(t) for t in rng.integers(3, cfg.vocab, 21)]
-    with Engine(gguf=path, backend="cpu", max_ctx=128, prefill_chunk=16, threads=4) as eng:
+    tol = 1e-8 if act == "f32" else 2e-3
+    with Engine(gguf=path, backend="cpu", max_ctx=128, prefill_chunk=16, threads=4, cpu_act=act) as eng:
         eng.start([prompt])
         lg = eng.logits()[0]
         ref.reset()
         rl = ref.forward(prompt, 0)[-1].numpy()
-        assert nmse(lg, rl) < 1e-8, nmse(lg, rl)
+        assert nmse(lg, rl) < tol, nmse(lg, rl)
         pos = len(prompt)
         for step in range(4):
             tok = eng.tokens()[0][-1]
-            assert tok == int(rl.argmax()), step
+            top2 = np.sort(rl)[-2:]
+            if act == "f32" or top2[1] - top2[0] > 0.05 * (abs(top2).max() + 1):
+                assert tok == int(rl.argmax()), step
             eng.decode(1)
             lg = eng.logits()[0]
             rl = ref.forward([tok], pos)[-1].numpy()
             pos += 1
-            assert nmse(lg, rl) < 1e-8, (step, nmse(lg, rl))
+            assert nmse(lg, rl) < tol, (step, nmse(lg, rl))
 
 
 @pytest.mark.parametrize("stages,n_mb", [(2, 2), (3, 3), (4, 1)])
@@ -242,7 +249,7 @@ def test_cpu_repetition_penalties_match_reference(native, model_dir):
     ref = RefLlama.from_gguf(path)
     prompt = [5, 9, 5, 17, 30, 9]
     rep, fq, pr, last_n = 1.8, 0.3, 0.4, 8
-    with Engine(gguf=path, backend="cpu", max_ctx=64, repeat_penalty=rep, frequency_penalty=fq,
+    with Engine(gguf=path, backend="cpu", cpu_act="f32", max_ctx=64, repeat_penalty=rep, frequency_penalty=fq,
                 presence_penalty=pr, repeat_last_n=last_n) as eng:
         out, _ = eng.generate([prompt], 10)
     ref.reset()

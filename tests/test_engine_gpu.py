@@ -418,6 +418,36 @@ def test_fused_decode_attention_matches_unfused(cuda, native, model_dir, name):
     assert nmse(res[1][1], res[0][1]) < 1e-6
 
 
+@pytest.mark.parametrize("name,ftype,kv", [("tiny-gqa", "Q4_K_M", "f16"), ("tiny-qwen2", "Q8_0", "f16"),
+                                            ("stories15m", "Q8_0", "f16"), ("tiny-gqa", "Q4_K_M", "fp8")])
+@pytest.mark.parametrize("mb_size", [1, 3])
+def test_qkv_append_epilogue_matches_attention_append(cuda, native, model_dir, name, ftype, kv, mb_size):
+    """Knob ATTN_PRE: RoPE + the KV append in the qkv GEMV's epilogue (gemvs QkvAppend, also the
+    mixed-type gemvs2 launch of Q4_K_M and the q/k/v biases of qwen2) == the decode attention doing
+    them itself: same tokens, logits within rounding, f16 and fp8 KV, single stream and M = 3."""
+    from mipipe import _native as N
+    from mipipe.engine import Engine
+    path, cfg = make_model(model_dir, name, ftype)
+    rng = np.random.default_rng(11)
+    prompts = [[int(t) for t in rng.integers(3, cfg.vocab, n)] for n in (37, 70, 5)][:mb_size]
+    res = []
+    try:
+        for pre in (0, 1):
+            N.check(N.lib().mp_set_knob(b"ATTN_PRE", pre), "knob")
+            with Engine(gguf=path, max_ctx=256, mb_size=mb_size, prefill_chunk=16, kv_dtype=kv) as eng:
+                out, _ = eng.generate(prompts, 70)   # crosses a 64-token page for every prompt
+                res.append((out, eng.logits(rows=mb_size)))
+    finally:
+        N.lib().mp_reset_knob(b"ATTN_PRE")
+    if kv == "f16":
+        assert res[0][0] == res[1][0]
+        assert nmse(res[1][1], res[0][1]) < 1e-6, nmse(res[1][1], res[0][1])
+    else:   # e4m3 rounding of K amplifies f32 contraction-order differences into rare late near-tie flips
+        assert all(a[:16] == b[:16] for a, b in zip(res[0][0], res[1][0]))
+        if res[0][0] == res[1][0]:
+            assert nmse(res[1][1], res[0][1]) < 1e-3, nmse(res[1][1], res[0][1])
+
+
 def test_prefill_gemm_matches_gemv_path(cuda, native, model_dir):
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q4_K_M")
@@ -656,7 +686,7 @@ def test_bench_inprocess_same_device(cuda, native, gpus, link):
 
 
 def test_local_link_single_copy_cross_stage(cuda, native, model_dir):
-    """The rendezvous LocalLink (one device copy per message, receiver reads the sender's buffer):
+    """The posted-queue LocalLink (one device copy per message, receiver reads the sender's buffer):
     PP=3 on one GPU with 3 micro-batches and ring tokens generates what PP=1 generates."""
     from mipipe.engine import Engine
     path, cfg = make_model(model_dir, "tiny-gqa", "Q8_0")
@@ -670,6 +700,14 @@ def test_local_link_single_copy_cross_stage(cuda, native, model_dir):
         h = eng.health()
     assert out == ref
     assert all(s["link"] == "local" and s["msgs_sent"] > 0 for s in h["stages"])
+
+
+@pytest.mark.parametrize("n_msgs,n_bufs,delay_us", [(200, 2, 300), (300, 100, 50), (40, 1, 2000)])
+def test_local_link_posted_queue_delayed_receiver(cuda, native, n_msgs, n_bufs, delay_us):
+    """LocalLink's posted queue under a slow receiver: messages arrive in order with their own
+    bytes, senders cycling 1-100 buffers never overwrite one before its message has been copied
+    (wait_consumed), and more messages than the queue depth (64) push back instead of failing."""
+    assert native.mp_local_link_selftest(0, n_msgs, 1 << 16, n_bufs, delay_us) == 0
 
 
 @pytest.mark.parametrize("stages", [1, 2])

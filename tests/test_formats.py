@@ -133,3 +133,31 @@ def test_t16_gateup_interleave(native):
     for t in range(2 * F // 16):
         np.testing.assert_allclose(got[16 * t:16 * t + 8], deq[8 * t:8 * t + 8], rtol=1e-6)
         np.testing.assert_allclose(got[16 * t + 8:16 * t + 16], deq[F + 8 * t:F + 8 * t + 8], rtol=1e-6)
+
+
+@pytest.mark.parametrize("qt", [Q.Q8_0, Q.Q4_0, Q.Q4_K, Q.Q5_K, Q.Q6_K])
+def test_cpu_integer_dot_matches_dequant(native, qt):
+    """CPU stage integer dots (cpu_qdot.cpp): quantized weight rows x int8 activation blocks.  The
+    AVX2 form equals the scalar one (same integer sums, f32 order aside), and both stay within the
+    int8 rounding of x of the f32 dot of the dequantized row (numpy oracle)."""
+    import ctypes
+    rng = np.random.default_rng(31 + qt)
+    N, K = 24, 1024
+    w = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    b = np.concatenate([Q.quantize(w[n], qt) for n in range(N)])
+    wd = np.stack([Q.dequantize(Q.quantize(w[n], qt), qt) for n in range(N)])
+    x = rng.standard_normal(K).astype(np.float32)
+    x[::97] *= 20.0   # a few outliers per 32-block
+    y = np.zeros(N, np.float32)
+    ys = np.zeros(N, np.float32)
+    assert native.mp_qdot_rows(qt, b.ctypes.data, N, K, x.ctypes.data, y.ctypes.data, ys.ctypes.data) == 1
+    ref = wd.astype(np.float64) @ x.astype(np.float64)
+    np.testing.assert_allclose(y, ys, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    # exact up to f32 rounding against the dequantized row times the int8-rounded activations
+    xb = x.reshape(-1, 32).astype(np.float32)
+    d = np.abs(xb).max(1, keepdims=True) / np.float32(127)
+    x8 = (np.clip(np.rint(xb / np.where(d > 0, d, 1)), -127, 127) * d).reshape(-1)
+    ref8 = wd.astype(np.float64) @ x8.astype(np.float64)
+    np.testing.assert_allclose(y, ref8, rtol=2e-5, atol=2e-5 * np.abs(ref8).max())
+    rel = np.sqrt(((y - ref) ** 2).mean() / (ref ** 2).mean())
+    assert rel < 2e-2, rel   # the int8 rounding of x (outlier-heavy blocks)

@@ -271,29 +271,3 @@ def test_gemm4_splitk_qkv_width_three_splits(cuda, tuning, M):
     assert float(rows.max()) < 1e-5, f"worst row {int(rows.argmax())}: {float(rows.max()):.3e}"
 
 
-@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
-@pytest.mark.parametrize("M", [33, 48, 64])
-def test_gemm4_64_row_tiles(cuda, tuning, qt, M):
-    """Knob GEMM4_M64: 33-64 row micro-batches on 64-row tiles (two workgroups per CU), every
-    epilogue, split-K by atomics and by per-split partial stores, against the oracle."""
-    from mipipe import _native as N
-    from mipipe.ops.kernels import PackedWeight, gemm, gemm_splitk, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
-    N.check(N.lib().mp_set_knob(b"GEMM4_M64", 1), "knob")
-    try:
-        n, k = 640, 4096
-        raw, deq = _weights(qt, n, k, 60 + qt + M)
-        w = PackedWeight(raw, qt, n, k)
-        xh = _x(M, k, w.k_pad, M + 3)
-        ref = _ref(xh, k, deq, qt)
-        assert nmse(gemm(w, xh.cuda(), EPI_STORE, v=4).cpu(), ref) < 1e-5
-        base = torch.randn(M, n)
-        y = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4).cpu()
-        assert torch.isfinite(y).all() and nmse(y - base, ref) < 1e-5
-        h = gemm(w, xh.cuda(), EPI_SWIGLU, v=4)
-        gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
-        assert nmse(h.float().cpu(), torch.nn.functional.silu(ref[:, gi]) * ref[:, gi + 8]) < 1e-4
-        y2 = base.clone().cuda()
-        if gemm_splitk(w, xh.cuda(), y2, max_splits=64):
-            assert torch.isfinite(y2).all() and nmse(y2.cpu() - base, ref) < 1e-5
-    finally:
-        N.lib().mp_set_knob(b"GEMM4_M64", 0)
