@@ -90,7 +90,7 @@ int mp_qdot_rows(int type, const uint8_t* W, int64_t N, int64_t K, const float* 
   const size_t rb = row_bytes(type, K);
   for (int64_t n = 0; n < N; ++n) {
     y[n] = qdot_row(type, W + n * rb, q8_row(b, 0), K);
-    y_scalar[n] = qdot_row_scalar(type, W + n * rb, q8_row(b, 0), K);
+    if (y_scalar) y_scalar[n] = qdot_row_scalar(type, W + n * rb, q8_row(b, 0), K);
   }
   return 1;
   API_CATCH(-1)

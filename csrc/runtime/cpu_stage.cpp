@@ -9,6 +9,9 @@
 #include <stdexcept>
 #include <thread>
 
+#include <sched.h>
+#include <cstdio>
+
 #include "gguf.h"
 #include "hip_stage.h"   // SyntheticTypes
 #include "log.h"
@@ -83,9 +86,28 @@ inline uint64_t mix64(uint64_t x) {
 
 }  // namespace
 
+// CPUs this process may really use: the affinity mask and the cgroup quota (cpu.max), not the
+// machine's count (a GPU box's container sees every CPU of the host but gets a 16-CPU share); one
+// is left to the control plane (HTTP / session / link threads), since the pool's workers spin
+int default_cpu_threads() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = std::min(n, CPU_COUNT(&cs));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const long quota = std::atol(q);
+      if (quota > 0) n = std::min(n, (int)std::max(1L, (quota + period - 1) / period));
+    }
+    std::fclose(f);
+  }
+  return std::max(1, n > 3 ? n - 1 : n);
+}
+
 CpuStage::CpuStage(const ModelConfig& cfg, const StageSpec& spec, const StageOptions& opt)
     : cfg_(cfg), spec_(spec), opt_(opt) {
-  int nt = opt_.threads > 0 ? opt_.threads : (int)std::thread::hardware_concurrency();
+  int nt = opt_.threads > 0 ? opt_.threads : default_cpu_threads();
   pool_.reset(new ThreadPool(std::max(1, std::min(nt, 64))));
   layers_.resize(spec_.layer_end - spec_.layer_begin);
 }
