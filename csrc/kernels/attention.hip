@@ -742,7 +742,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 // here every wave has 32 KB of K / V in flight from its first chunk on.
 // Splits (few pairs, long contexts): partials + the last-arriving wave of the (token, kv head)
 // merges, with the same sc1 publish / counter / sc1 load hand-off as attn_decode_body.
-template <int DP, bool F8, bool FL = false, bool AL = false>
+template <int DP, bool F8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_decode_wave_kernel(const DecodeAttnParams p) {
   using KR = std::conditional_t<F8, u32x2, half8_t>;
   constexpr int KK = DP / 32, DT = DP / 16, EB = F8 ? 1 : 2;
@@ -770,51 +770,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int nch = (end - start + 31) / 32;
   const int krow0 = 8 * (col >> 2) + (col & 3);
 
-  // AL: the chunk loads as inline asm with this kernel's own counted vmcnt waits.  Left to the
-  // compiler, the two register sets' loads were scheduled so that each chunk's last PV MFMA waited
-  // for vmcnt(0): about one chunk in flight per wave instead of two (the loop was memory-latency
-  // bound: ~6.7 us per 32-key chunk at 2K contexts, r8o)
-  auto gload = [&](KR& dst, const uint8_t* a) {
-    if constexpr (AL) {
-      if constexpr (F8) asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(a) : "memory");
-      else asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(a) : "memory");
-    } else {
-      dst = *reinterpret_cast<const KR*>(a);
-    }
-  };
   auto load = [&](int ci, KR (&kf)[2][KK], KR (&vf)[DT]) {
     const int P0 = start + ci * 32;
     const int page = ld_bt(bt + (P0 >> 6));
     const int in_page = P0 & 63;
     const uint8_t* kbase = reinterpret_cast<const uint8_t*>(p.k_cache) + ((size_t)page * p.Hkv + kvh) * 64 * DP * EB;
     const uint8_t* vbase = reinterpret_cast<const uint8_t*>(p.v_cache) + ((size_t)page * p.Hkv + kvh) * DP * 64 * EB;
-    if constexpr (FL) {
-      // whole-line K loads (f16 pages): instruction (c, h, I|J) reads 8 keys x the 128-B line of dims
-      // 64h .. 64h+63; lanes m < 8 / m >= 8 carry fragments kk = 2h / 2h+1 of different keys, sorted
-      // into the MFMA fragments at use (fl_fix).  The fragment-shaped form reads 16 keys x 64 B per
-      // instruction (half lines, the other half by the next instruction)
-      const int m = col;
-      const int rI = m < 8 ? m : m - 8, rJ = m < 8 ? 8 + m : m;
-      const int kI = m < 8 ? 0 : 1, kJ = 1 - kI;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int keyI = in_page + 8 * (rI >> 2) + (rI & 3) + 4 * c, keyJ = in_page + 8 * (rJ >> 2) + (rJ & 3) + 4 * c;
-#pragma unroll
-        for (int hh = 0; hh < KK / 2; ++hh) {
-          gload(kf[c][2 * hh], kbase + ((size_t)keyI * DP + 32 * (2 * hh + kI) + 8 * q4) * EB);
-          gload(kf[c][2 * hh + 1], kbase + ((size_t)keyJ * DP + 32 * (2 * hh + kJ) + 8 * q4) * EB);
-        }
-      }
-    } else {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
-        gload(kf[c][kk], kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
-    }
+        kf[c][kk] = *reinterpret_cast<const KR*>(kbase + ((size_t)(in_page + krow0 + 4 * c) * DP + 32 * kk + 8 * q4) * EB);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
-      gload(vf[dt], vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
+      vf[dt] = *reinterpret_cast<const KR*>(vbase + ((size_t)(16 * dt + col) * 64 + in_page + 8 * q4) * EB);
   };
   KR kA[2][KK], vA[DT], kB[2][KK], vB[DT];
   load(0, kA, vA);   // in flight during the q build and the append
@@ -936,31 +905,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) o[dt] = mfma16x16x32(vf[dt], pf, o[dt]);
   };
-  // whole-line K loads: register pair (I, J) of (c, h) -> fragments kk = 2h (lanes m < 8 from I,
-  // m >= 8 from J) and 2h + 1 (the other register, rows rotated by 8 within each 16-lane row: DPP)
-  auto fl_fix = [&](KR (&kf)[2][KK]) {
-    if constexpr (FL && !F8) {
-      const bool lo = col < 8;
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int hh = 0; hh < KK / 2; ++hh) {
-          const u32x4 I = __builtin_bit_cast(u32x4, kf[c][2 * hh]), J = __builtin_bit_cast(u32x4, kf[c][2 * hh + 1]);
-          u32x4 f0, f1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            f0[e] = lo ? I[e] : J[e];
-            const uint32_t t = lo ? J[e] : I[e];
-            f1[e] = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x128, 0xF, 0xF, false);   // row_ror:8
-          }
-          kf[c][2 * hh] = __builtin_bit_cast(KR, f0);
-          kf[c][2 * hh + 1] = __builtin_bit_cast(KR, f1);
-        }
-    }
-  };
   // f16 pages: the loaded registers are used (and patched) in place; e4m3: converted at use
   auto step = [&](int ci, KR (&kraw)[2][KK], KR (&vraw)[DT]) {
-    fl_fix(kraw);
     if constexpr (F8) {
       half8_t kf[2][KK], vf[DT];
 #pragma unroll
@@ -974,22 +920,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       step_h(ci, kraw, vraw);
     }
   };
-  // two chunks in flight: chunk ci + 2 is loaded into the registers chunk ci frees.  AL: before a
-  // chunk's math, wait until only the other set's loads (issued after this chunk's) are in flight
-  constexpr int NL = 2 * KK + DT;   // load instructions per chunk
-  auto vm_wait = [&](int ci) {
-    if constexpr (AL) {
-      if (ci + 1 < nch) __builtin_amdgcn_s_waitcnt((NL & 15) | ((NL >> 4) << 14) | (7 << 4) | (15 << 8));
-      else __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
+  // two chunks in flight: chunk ci + 2 is loaded into the registers chunk ci frees
   for (int ci = 0; ci < nch;) {
-    vm_wait(ci);
     step(ci, kA, vA);
     if (ci + 2 < nch) load(ci + 2, kA, vA);
     if (++ci >= nch) break;
-    vm_wait(ci);
     step(ci, kB, vB);
     if (ci + 2 < nch) load(ci + 2, kB, vB);
     ++ci;
@@ -1081,7 +1016,7 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 //   3. split-K GEMV of the slice on MFMA (the decode GEMV's dequant), atomics into the residual:
 //      Hkv partial sums per output (not bitwise reproducible: the deterministic mode keeps the
 //      two-kernel path).
-template <int DP, bool F8, int PT, int TPW, int KS>
+template <int DP, bool F8, int PT, int TPW, int KS, bool PRE>
 __global__ __launch_bounds__(256) void attn_o_kernel(const DecodeAttnParams p, const AttnOParams o) {
   using D = Deq<PT>;
   constexpr int CB = D::CB, TB = KS * CB, WB = TPW * TB;
@@ -1102,7 +1037,7 @@ __global__ __launch_bounds__(256) void attn_o_kernel(const DecodeAttnParams p, c
   }
   const int M = p.M;
   for (int t = 0; t < M; ++t) {
-    attn_decode_body<DP, F8, true>(p, t, kvh, 0, &xo[t][0]);
+    attn_decode_body<DP, F8, true, 4, PRE>(p, t, kvh, 0, &xo[t][0]);
     __syncthreads();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1186,7 +1121,8 @@ bool attn_o_supported(const DecodeAttnParams& p, const AttnOParams& o) {
 template <bool F8, int PT>
 static void attn_o_go(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {
   const dim3 grid(o.ntiles / kAttnOTpw, p.Hkv);
-  hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2>), grid, dim3(256), 0, st, p, o);
+  if (p.pre) hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, true>), grid, dim3(256), 0, st, p, o);
+  else hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, false>), grid, dim3(256), 0, st, p, o);
 }
 
 void launch_attn_o(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {
@@ -1231,17 +1167,8 @@ void launch_attn_decode(const DecodeAttnParams& p, hipStream_t st) {
     const int items = p.M * p.Hkv * p.n_split;
     const dim3 grid((items + 3) / 4);
     if (p.Dp == 128) {
-      const bool al = knob(KNOB_ATTN_ASMLD) != 0;
-      if (p.kv_fp8) {
-        if (al) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true, false, true>), grid, dim3(256), 0, st, p);
-        else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
-      } else if (knob(KNOB_ATTN_KFL)) {
-        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, true>), grid, dim3(256), 0, st, p);
-      } else if (al) {
-        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false, false, true>), grid, dim3(256), 0, st, p);
-      } else {
-        hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
-      }
+      if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, true>), grid, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<128, false>), grid, dim3(256), 0, st, p);
     } else {
       if (p.kv_fp8) hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, true>), grid, dim3(256), 0, st, p);
       else hipLaunchKernelGGL((mpk::attn_decode_wave_kernel<64, false>), grid, dim3(256), 0, st, p);

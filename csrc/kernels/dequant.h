@@ -329,4 +329,149 @@ template <> struct Deq<P_BF16> {
   }
 };
 
+// ------------------------------------------------------------------ single-row dot forms (gemvs M = 1)
+// For ONE activation row the MFMA path wastes 15 of its 16 rows, and the dequant dominates the
+// kernel's VALU (profiles/r11d_gemvs_probe.txt: dequant + MFMA 1.2-4 us of a 5.7-16.7 us GEMV).
+// Here the exponent-magic pairs are used BIASED, straight as v_dot2_f32_f16 operands: a Q4_K pair
+// reads (1024 + q) or (64 + q) exactly, so sum (1024 + q_j) x_j = sum q_j x_j + 1024 sum x_j and the
+// bias term -- the same for every output column -- comes out of a per-(super-block, lane group)
+// table the workgroup builds once from its staged x (DotCorr).  Per 8 weights: one shift, 4
+// v_and_or, 4 v_dot2 (the MFMA form: shift, 4 v_and_or, 4 v_pk_add, 4 v_pk_fma, 2 MFMA); the scale
+// and min are applied once per sub-block in f32, and q enters the dot unrounded (the MFMA form
+// rounds each weight q S + M to f16).
+//   xq: the lane group's x of the super-block in LDS (fragment i = 4h + s at xq + 8 i: t16_xoff),
+//       read just before use (8 fragments held at once cost 32 VGPRs: occupancy 6 -> 4, r11f)
+//   c: the lane group's 4 correction floats (DotCorr<PT>::make)
+template <int PT> struct DotCorr;   // per (super-block, lane group g): 4 floats from that quarter's 64 x
+// a[i] = x_j0 + x_j1 + x_j4 + x_j5, b[i] = x_j2 + x_j3 + x_j6 + x_j7 of fragment i (the positions the
+// 1024- and 64-exponent magic words carry)
+template <> struct DotCorr<P_Q4_K> {   // (C_h0, C_h1, X_h0, X_h1): C = 1024 a + 64 b over the half, X = sum x
+  __device__ static __forceinline__ float4 make(const float (&a)[8], const float (&b)[8]) {
+    float c[2] = {0.f, 0.f}, x[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { c[i >> 2] += 1024.f * a[i] + 64.f * b[i]; x[i >> 2] += a[i] + b[i]; }
+    return make_float4(c[0], c[1], x[0], x[1]);
+  }
+};
+template <> struct DotCorr<P_Q5_K> : DotCorr<P_Q4_K> {};
+template <> struct DotCorr<P_Q6_K> {   // C per 16-wide sub-block (h, s >> 1): 1056 a + 96 b (zero point 32)
+  __device__ static __forceinline__ float4 make(const float (&a)[8], const float (&b)[8]) {
+    float c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i >> 1] += 1056.f * a[i] + 96.f * b[i];
+    return make_float4(c[0], c[1], c[2], c[3]);
+  }
+};
+template <> struct DotCorr<P_Q8_0> {   // C per 32-block h: 1152 (a + b) (bytes stored q + 128)
+  __device__ static __forceinline__ float4 make(const float (&a)[8], const float (&b)[8]) {
+    float c[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i >> 2] += 1152.f * (a[i] + b[i]);
+    return make_float4(c[0], c[1], 0.f, 0.f);
+  }
+};
+template <int PT> constexpr bool dot1_supported() {
+  return PT == P_Q4_K || PT == P_Q5_K || PT == P_Q6_K || PT == P_Q8_0;
+}
+
+__device__ __forceinline__ float d2(uint32_t w, uint32_t x, float acc) {
+  return __builtin_amdgcn_fdot2(as_h2(w), as_h2(x), acc, false);
+}
+
+// sum over the lane's 64 weights of W x for one super-block (Q4_K / Q5_K)
+__device__ __forceinline__ u32x4 xfrag(const f16* xq, int i) { return *reinterpret_cast<const u32x4*>(xq + 8 * i); }
+
+template <bool Q5, class Raw>
+__device__ __forceinline__ float dot1_q45k(const Raw& r, const f16* xq, const float4 c, int lane, const Consts& k) {
+  half2_t S2, M2;
+  kquarter_scales(r.hdr, lane, S2, M2);
+  float acc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u32x4 q = h == 0 ? r.q0 : r.q1;
+    uint32_t qh = 0;
+    if constexpr (Q5) qh = h == 0 ? r.qh0 : r.qh1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t w = q[s], t = w >> 8;
+      uint32_t h0 = k.mag_hi, h1 = k.mag_lo, h2 = k.mag_hi, h3 = k.mag_lo;
+      if constexpr (Q5) {
+        const uint32_t hb = (qh >> (8 * s)) & 0xFFu;
+        const uint32_t xx = hb | (hb << 12);
+        h0 = ((xx << 4) & 0x00100010u) | k.mag_hi; h1 = ((xx << 7) & 0x01000100u) | k.mag_lo;
+        h2 = ((xx << 2) & 0x00100010u) | k.mag_hi; h3 = ((xx << 5) & 0x01000100u) | k.mag_lo;
+      }
+      const u32x4 xv = xfrag(xq, 4 * h + s);
+      float a = acc[h];
+      a = d2(and_or(w, k.mlo, h0), xv.x, a);
+      a = d2(and_or(w, k.mhi, h1), xv.y, a);
+      a = d2(and_or(t, k.mlo, h2), xv.z, a);
+      a = d2(and_or(t, k.mhi, h3), xv.w, a);
+      acc[h] = a;
+    }
+  }
+  return (float)S2.x * (acc[0] - c.x) + (float)M2.x * c.z + (float)S2.y * (acc[1] - c.y) + (float)M2.y * c.w;
+}
+
+template <class Raw>
+__device__ __forceinline__ float dot1_q6k(const Raw& r, const f16* xq, const float4 c, int lane, const Consts& k) {
+  const float dh = (float)__builtin_bit_cast(f16, (uint16_t)r.d);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int H = 0; H < 2; ++H) {
+    const u32x4 q = H == 0 ? r.q0 : r.q1;
+    const u32x2 qh = H == 0 ? r.qh0 : r.qh1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t w = q[s], t = w >> 8;
+      const uint32_t h16 = (qh[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+      const uint32_t e = h16 | (h16 << 8);
+      const uint32_t h0 = ((e << 4) & 0x00300030u) | k.mag_hi, h1 = ((e << 6) & 0x03000300u) | k.mag_lo;
+      const uint32_t h2 = (e & 0x00300030u) | k.mag_hi, h3 = ((e << 2) & 0x03000300u) | k.mag_lo;
+      const u32x4 xv = xfrag(xq, 4 * H + s);
+      float a = acc[2 * H + (s >> 1)];
+      a = d2(and_or(w, k.mlo, h0), xv.x, a);
+      a = d2(and_or(w, k.mhi, h1), xv.y, a);
+      a = d2(and_or(t, k.mlo, h2), xv.z, a);
+      a = d2(and_or(t, k.mhi, h3), xv.w, a);
+      acc[2 * H + (s >> 1)] = a;
+    }
+  }
+  // int8 scales of the lane's 16-wide sub-blocks 4g + 2H + (s >> 1): bytes 0..3 of r.sc
+  const int32_t sc = (int32_t)r.sc;
+  const float s0 = (float)(int8_t)(sc & 0xFF), s1 = (float)(int8_t)((sc >> 8) & 0xFF);
+  const float s2 = (float)(int8_t)((sc >> 16) & 0xFF), s3 = (float)(int8_t)(sc >> 24);
+  return dh * (s0 * (acc[0] - c.x) + s1 * (acc[1] - c.y) + s2 * (acc[2] - c.z) + s3 * (acc[3] - c.w));
+}
+
+template <class Raw>
+__device__ __forceinline__ float dot1_q80(const Raw& r, const f16* xq, const float4 c, int lane) {
+  const half2_t S = as_h2(r.dd);   // d(2g), d(2g + 1)
+  float acc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int H = 0; H < 2; ++H) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const u32x4 src = H == 0 ? (s < 2 ? r.a0 : r.a1) : (s < 2 ? r.b0 : r.b1);
+      const uint32_t lo = src[2 * (s & 1)], hi = src[2 * (s & 1) + 1];
+      const u32x4 xv = xfrag(xq, 4 * H + s);
+      float a = acc[H];
+      a = d2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04010400u), xv.x, a);
+      a = d2(__builtin_amdgcn_perm(0x64646464u, lo, 0x04030402u), xv.y, a);
+      a = d2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04010400u), xv.z, a);
+      a = d2(__builtin_amdgcn_perm(0x64646464u, hi, 0x04030402u), xv.w, a);
+      acc[H] = a;
+    }
+  }
+  return (float)S.x * (acc[0] - c.x) + (float)S.y * (acc[1] - c.y);
+}
+
+template <int PT, class Raw>
+__device__ __forceinline__ float dot1(const Raw& r, const f16* xq, const float4 c, int lane, const Consts& k) {
+  if constexpr (PT == P_Q4_K) return dot1_q45k<false>(r, xq, c, lane, k);
+  else if constexpr (PT == P_Q5_K) return dot1_q45k<true>(r, xq, c, lane, k);
+  else if constexpr (PT == P_Q6_K) return dot1_q6k(r, xq, c, lane, k);
+  else return dot1_q80(r, xq, c, lane);
+}
+
 }  // namespace mpk

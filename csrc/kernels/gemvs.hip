@@ -45,8 +45,11 @@ constexpr int GS_NT = GS_NW * 64;
 constexpr int EPI_QKV = 3;   // STORE with the RoPE + KV-append epilogue (GemvParams::qa)
 
 // bx: this workgroup's tile-group index (blockIdx.x, or its offset inside a segment of gemvs2)
-template <int PT, int EPI, int G, bool NORM, int NSO = 0>
+// D1: one activation row on the v_dot2 form (dequant.h dot1): biased magic pairs against x, the bias
+// removed through a per-(super-block, lane group) correction table built from the staged x
+template <int PT, int EPI, int G, bool NORM, int NSO = 0, bool D1 = false>
 __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit, const int bx) {
+  static_assert(!D1 || dot1_supported<PT>(), "gemvs: no single-row dot form for this type");
   using D = Deq<PT>;
   constexpr int CB = D::CB;
   constexpr bool BF = PT == P_BF16;
@@ -208,15 +211,36 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
     }
   }
   __syncthreads();
+  // D1: the bias-correction table, 4 floats per (super-block, lane group) of the workgroup's range
+  float4* corr = reinterpret_cast<float4*>(xs + (size_t)M * krange);
+  if constexpr (D1) {
+    for (int e = tid; e < (sbB - sbA) * 4; e += GS_NT) {
+      const f16* q = xs + (e >> 2) * 256 + 64 * (e & 3);
+      float a[8], b[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const half8_t v = *reinterpret_cast<const half8_t*>(q + 8 * i);
+        a[i] = ((float)v[0] + (float)v[1]) + ((float)v[4] + (float)v[5]);
+        b[i] = ((float)v[2] + (float)v[3]) + ((float)v[6] + (float)v[7]);
+      }
+      corr[e] = DotCorr<PT>::make(a, b);
+    }
+    __syncthreads();
+  }
 
   // ---- weight stream: no barriers; slot s holds super-block wA + j + s
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float acc1 = 0.f;   // D1
   const Consts kc = make_consts();
   const f16* xrow = xs + (size_t)r * krange + t16_xoff(g, 0);   // valid for r < M only
   const bool xr_ok = r < M;
   auto step = [&](const int s, const int sbl) {   // sbl: super-block index relative to sbA
     if (probe & 1) {   // timing probe: consume the loads, no dequant / MFMA
       acc[0] += __uint_as_float(*reinterpret_cast<const uint32_t*>(&ring[s]) & 1u);
+      return;
+    }
+    if constexpr (D1) {
+      acc1 += dot1<PT>(ring[s], xs + sbl * 256 + t16_xoff(g, 0), corr[sbl * 4 + g], lane, kc);
       return;
     }
     half8_t b[4];
@@ -250,13 +274,21 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
 
   // ---- reduce the KSW k-slices of each tile, then the epilogue (one wave per tile)
   float v[4];
+  if constexpr (D1) {   // the 4 lane groups' k-quarters of column r, then row 0 of the MFMA layout
+    acc1 += __shfl_xor(acc1, 16);
+    acc1 += __shfl_xor(acc1, 32);
+    v[0] = acc1;
+    v[1] = v[2] = v[3] = 0.f;
+  }
   if constexpr (KSW == 1) {
+    if constexpr (!D1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = acc[i];
+      for (int i = 0; i < 4; ++i) v[i] = acc[i];
+    }
   } else {
     if (g == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[wave][i * 16 + r] = acc[i];
+      for (int i = 0; i < 4; ++i) red[wave][i * 16 + r] = D1 ? v[i] : acc[i];
     }
     __syncthreads();
     if (wave >= G) return;
@@ -264,7 +296,9 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   // epilogue wave e = gi' handles tile blockIdx.x * G + e; lane -> (row i = lane >> 4, column r)
   const int et = KSW == 1 ? tile : bx * G + wave;
   float val;
-  if constexpr (KSW == 1) {
+  if constexpr (KSW == 1 && D1) {
+    val = lane < 16 ? v[0] : 0.f;   // lane r of group 0: row 0, column r
+  } else if constexpr (KSW == 1) {
     // lane (g, r): rows 4g + i; only g = 0 is valid (M <= 4): move row i to lane 16 i + r
     const int i = lane >> 4;
     const float a0 = __shfl(v[0], r), a1 = __shfl(v[1], r), a2 = __shfl(v[2], r), a3 = __shfl(v[3], r);
@@ -328,18 +362,18 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
   }
 }
 
-template <int PT, int EPI, int G, bool NORM, int NSO = 0>
+template <int PT, int EPI, int G, bool NORM, int NSO = 0, bool D1 = false>
 __global__ __launch_bounds__(GS_NT) void gemvs_kernel(const GemvParams p, const int nsplit) {
-  gemvs_body<PT, EPI, G, NORM, NSO>(p, nsplit, blockIdx.x);
+  gemvs_body<PT, EPI, G, NORM, NSO, D1>(p, nsplit, blockIdx.x);
 }
 
 // two weight segments with different quant types over the same normed input in ONE launch (the
 // q+k and v projections of a mixed-type layer, e.g. Q4_K_M's Q6_K attn_v): workgroups [0, nwg1)
 // take segment 1, the rest segment 2.  STORE epilogue, RMSNorm fused, no k-split.
-template <int PT, int PT2, int G, int EPI = EPI_STORE>
+template <int PT, int PT2, int G, int EPI = EPI_STORE, bool D1 = false>
 __global__ __launch_bounds__(GS_NT) void gemvs2_kernel(const GemvParams p, const GemvParams p2, const int nwg1) {
-  if ((int)blockIdx.x < nwg1) gemvs_body<PT, EPI, G, true>(p, 1, blockIdx.x);
-  else gemvs_body<PT2, EPI, G, true>(p2, 1, blockIdx.x - nwg1);
+  if ((int)blockIdx.x < nwg1) gemvs_body<PT, EPI, G, true, 0, D1>(p, 1, blockIdx.x);
+  else gemvs_body<PT2, EPI, G, true, 0, D1>(p2, 1, blockIdx.x - nwg1);
 }
 
 }  // namespace mpk
@@ -376,26 +410,39 @@ GemvsPlan plan_gemvs(int ntiles, int nsb, int M, int epi, bool norm, bool determ
   return pl;
 }
 
-template <int PT, int EPI, int G, bool NORM, int NSO = 0>
+// dynamic LDS of the single-row dot form: the staged x plus its correction table (16 B per
+// super-block and lane group)
+static size_t d1_lds(const GemvsPlan& pl) { return pl.lds + (size_t)pl.sb_per_split * 64; }
+
+template <int PT, int EPI, int G, bool NORM, int NSO = 0, bool D1 = false>
 static void gemvs_go(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   static const bool attr = [] {   // dynamic LDS past the 64 KB default (gfx950: 160 KB per workgroup)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs_kernel<PT, EPI, G, NORM, NSO>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs_kernel<PT, EPI, G, NORM, NSO, D1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
   }();
-  if (!attr && pl.lds > 60 * 1024) throw std::runtime_error("gemvs: cannot raise the dynamic LDS limit");
-  hipLaunchKernelGGL((mpk::gemvs_kernel<PT, EPI, G, NORM, NSO>), dim3((p.ntiles + G - 1) / G, pl.nsplit),
-                     dim3(mpk::GS_NT), pl.lds, st, p, pl.nsplit);
+  const size_t lds = D1 ? d1_lds(pl) : pl.lds;
+  if (!attr && lds > 60 * 1024) throw std::runtime_error("gemvs: cannot raise the dynamic LDS limit");
+  hipLaunchKernelGGL((mpk::gemvs_kernel<PT, EPI, G, NORM, NSO, D1>), dim3((p.ntiles + G - 1) / G, pl.nsplit),
+                     dim3(mpk::GS_NT), lds, st, p, pl.nsplit);
 }
 
-template <int PT, int EPI, bool NORM, int NSO>
+template <int PT, int EPI, bool NORM, int NSO, bool D1 = false>
 static void gemvs_gn(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   switch (pl.G) {
-    case 1: return gemvs_go<PT, EPI, 1, NORM, NSO>(p, pl, st);
-    case 2: return gemvs_go<PT, EPI, 2, NORM, NSO>(p, pl, st);
-    case 4: return gemvs_go<PT, EPI, 4, NORM, NSO>(p, pl, st);
-    case 8: return gemvs_go<PT, EPI, 8, NORM, NSO>(p, pl, st);
+    case 1: return gemvs_go<PT, EPI, 1, NORM, NSO, D1>(p, pl, st);
+    case 2: return gemvs_go<PT, EPI, 2, NORM, NSO, D1>(p, pl, st);
+    case 4: return gemvs_go<PT, EPI, 4, NORM, NSO, D1>(p, pl, st);
+    case 8: return gemvs_go<PT, EPI, 8, NORM, NSO, D1>(p, pl, st);
     default: throw std::runtime_error("gemvs: G must be 1, 2, 4 or 8");
   }
+}
+
+// one row on the dot form (knob GEMVS_DOT): the quantized types that have one, default ring depth.
+// Q6_K only behind the fused norm (qkv, gate/up, LM head): its unnormed down projection measured
+// slower on the dot form (8B: 14.20 vs 13.59 us, 6 vs 7 waves per SIMD; profiles/r11f_*)
+static bool use_d1(int pt, const GemvParams& p) {
+  return p.M == 1 && knob(KNOB_GEMVS_DOT) != 0 &&
+         (pt == P_Q4_K || pt == P_Q5_K || pt == P_Q8_0 || (pt == P_Q6_K && p.Xf != nullptr));
 }
 
 template <int PT, int EPI, bool NORM>
@@ -405,6 +452,9 @@ static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   // 8B Q4_K_M mb1 NS 2 / 3 / 4 / 8 -> 548 / 541 / 524 / 441 tok/s, 70B Q4_K 105.4 / 106.6 / 104.4 / 91.1
   // (the knob only admits 2, 3 and 4; 16-bit weights always run the default depth)
   const int ns = knob(KNOB_GEMVS_NS);
+  if constexpr (mpk::dot1_supported<PT>()) {
+    if (use_d1(PT, p)) return gemvs_gn<PT, EPI, NORM, 2, true>(p, pl, st);
+  }
   if constexpr (!is16(PT)) {
     if (ns == 2) return gemvs_gn<PT, EPI, NORM, 2>(p, pl, st);
     if (ns == 3) return gemvs_gn<PT, EPI, NORM, 3>(p, pl, st);
@@ -424,20 +474,27 @@ static void gemvs_pt(int epi, const GemvParams& p, const GemvsPlan& pl, hipStrea
   }
 }
 
-template <int PT, int PT2, int G, int EPI>
+template <int PT, int PT2, int G, int EPI, bool D1>
 static void gemvs2_go_e(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
   static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs2_kernel<PT, PT2, G, EPI>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&mpk::gemvs2_kernel<PT, PT2, G, EPI, D1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024) == hipSuccess;
   }();
+  if (D1) lds += (size_t)p.sb_per_split * 64;   // the correction table
   if (!attr && lds > 60 * 1024) throw std::runtime_error("gemvs2: cannot raise the dynamic LDS limit");
   const int nwg1 = (p.ntiles + G - 1) / G, nwg2 = (p2.ntiles + G - 1) / G;
-  hipLaunchKernelGGL((mpk::gemvs2_kernel<PT, PT2, G, EPI>), dim3(nwg1 + nwg2), dim3(mpk::GS_NT), lds, st, p, p2, nwg1);
+  hipLaunchKernelGGL((mpk::gemvs2_kernel<PT, PT2, G, EPI, D1>), dim3(nwg1 + nwg2), dim3(mpk::GS_NT), lds, st, p, p2, nwg1);
 }
 template <int PT, int PT2, int G>
 static void gemvs2_go(const GemvParams& p, const GemvParams& p2, size_t lds, hipStream_t st) {
-  if (p.qa.pos) gemvs2_go_e<PT, PT2, G, mpk::EPI_QKV>(p, p2, lds, st);
-  else gemvs2_go_e<PT, PT2, G, EPI_STORE>(p, p2, lds, st);
+  const bool d1 = use_d1(PT, p) && use_d1(PT2, p2);
+  if (p.qa.pos) {
+    if (d1) gemvs2_go_e<PT, PT2, G, mpk::EPI_QKV, true>(p, p2, lds, st);
+    else gemvs2_go_e<PT, PT2, G, mpk::EPI_QKV, false>(p, p2, lds, st);
+  } else {
+    if (d1) gemvs2_go_e<PT, PT2, G, EPI_STORE, true>(p, p2, lds, st);
+    else gemvs2_go_e<PT, PT2, G, EPI_STORE, false>(p, p2, lds, st);
+  }
 }
 
 template <int PT, int PT2>
@@ -464,7 +521,8 @@ void launch_gemvs2(int pt, int pt2, GemvParams p, GemvParams p2, hipStream_t st)
     throw std::runtime_error("launch_gemvs2: both segments need the same fused-norm input and K");
   // one plan for the union of the tiles (the shared G sizes both segments' workgroups)
   const GemvsPlan pl = plan_gemvs(p.ntiles + p2.ntiles, p.nsb, p.M, EPI_STORE, true, true);
-  if (pl.nsplit != 1 || pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs2: x k-range does not fit LDS");
+  if (pl.nsplit != 1 || pl.lds + (size_t)pl.sb_per_split * 64 > 150 * 1024)
+    throw std::runtime_error("launch_gemvs2: x k-range does not fit LDS");
   p.sb_per_split = p2.sb_per_split = pl.sb_per_split;
 #ifdef MIPIPE_TIMING_PROBES
   p.probe = p2.probe = knob(KNOB_GEMVS_PROBE);
@@ -492,7 +550,7 @@ void launch_gemvs(int ptype, int epi, GemvParams p, bool deterministic, hipStrea
     pl.nsplit = (p.nsb + pl.sb_per_split - 1) / pl.sb_per_split;
     pl.lds = (size_t)p.M * pl.sb_per_split * 256 * 2;
   }
-  if (pl.lds > 150 * 1024) throw std::runtime_error("launch_gemvs: x k-range does not fit LDS");
+  if (pl.lds + (size_t)pl.sb_per_split * 64 > 150 * 1024) throw std::runtime_error("launch_gemvs: x k-range does not fit LDS");
   if (epi != EPI_ATOMIC && pl.nsplit != 1) throw std::runtime_error("launch_gemvs: only ATOMIC splits K");
   p.sb_per_split = pl.sb_per_split;
   p.rpf = knob(KNOB_GEMVS_RPF);

@@ -934,7 +934,6 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
     // decode: RoPE and the KV append in the qkv GEMV's epilogue (QkvAppend), so the attention starts
     // from rotated q and a complete cache (no dependent position -> page -> append chain of its own)
     const bool pre = decode && opt_.fused_attn && knob(KNOB_ATTN_PRE) && !opt_.deterministic &&
-                     !(opt_.attn_o_max_ctx > 0 && opt_.max_ctx <= opt_.attn_o_max_ctx) &&
                      attn_decode_pre_ok(decode_attn_params(li, M, pos, slot, false));
     QkvAppend qa{};
     if (pre) {
@@ -965,7 +964,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
                    L.qkv_bias ? L.qkv_bias + s.y_off : nullptr, st, pre ? &q : nullptr);
       }
     }
-    if (!(decode && attention_o(li, M, pos, slot, x, st))) {
+    if (!(decode && attention_o(li, M, pos, slot, x, st, pre))) {
       attention(li, M, pos, kvlen, slot, decode, st, false, pre);
       gemv_small(L.wo, EPI_ATOMIC, attn_, Ko_, nullptr, nullptr, M, x, d, nullptr, 0, d, nullptr, st);
     }
@@ -1046,7 +1045,7 @@ void HipStage::layer_forward(int li, int M, float* x, const int32_t* pos, const 
 // single-stream decode: attention + o-projection in one launch (attention.hip attn_o_kernel) while
 // the context is short enough for every workgroup of a kv head to compute that head's attention
 // itself; false: the caller runs the two-kernel path
-bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st) {
+bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st, bool pre) {
   const LayerW& L = layers_[li];
   if (!opt_.fused_attn || opt_.deterministic || opt_.attn_o_max_ctx <= 0 || opt_.max_ctx > opt_.attn_o_max_ctx)
     return false;
@@ -1056,6 +1055,7 @@ bool HipStage::attention_o(int li, int M, const int32_t* pos, const int32_t* slo
   dp.max_pages = max_pages_; dp.rope_cs = rope_cs_; dp.q_scale = 1.0f / std::sqrt((float)cfg_.head_dim);
   dp.k_cache = kc_[li]; dp.v_cache = vc_[li]; dp.M = M; dp.Hq = cfg_.n_head; dp.Hkv = cfg_.n_head_kv;
   dp.kv_fp8 = opt_.kv_fp8;
+  dp.pre = pre;   // q rotated and K / V appended by the qkv GEMV
   // one split over the whole context (every workgroup of a kv head runs that head's attention)
   dp.hd = cfg_.head_dim; dp.Dp = Dp_; dp.split_len = (int)round_up(opt_.max_ctx, 128); dp.n_split = 1;
   dp.o_part = o_part_; dp.ml_part = ml_part_; dp.counters = attn_cnt_; dp.out = attn_; dp.ldo = Ko_;
@@ -1176,7 +1176,8 @@ void HipStage::gemv_small(const PackedMat& m, int epi, const f16* X, int ldx, co
   p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
   p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid; p.bias = bias;
   if (Xf) { p.Xf = Xf; p.ldxf = cfg_.d_model; p.gamma = gamma; p.eps = cfg_.eps; p.d_norm = cfg_.d_model; }
-  if (!Xf && plan_gemvs(p.ntiles, p.nsb, M, epi, false, opt_.deterministic).lds > 150 * 1024) {
+  const GemvsPlan pl = plan_gemvs(p.ntiles, p.nsb, M, epi, false, opt_.deterministic);
+  if (!Xf && pl.lds + (size_t)pl.sb_per_split * 64 > 150 * 1024) {   // (+ the single-row form's table)
     // deterministic mode cannot split K over grid.y, so a wide K (70B down: 28672) with M >= 3
     // rows overflows LDS: take the v2 GEMV with its fixed-order split-K reduction instead
     gemv(m, epi, X, ldx, M, Y, ldy, H, ldh, n_valid, epi == EPI_ATOMIC, st);

@@ -134,7 +134,7 @@ class HipStage : public Stage {
   void build_i8_copies();
   int8_t* xq_ = nullptr; float* xqs_ = nullptr; int xq_ld_ = 0;   // int8_gemm: quantized activation rows
   const void* xq_src_ = nullptr; int xq_rows_ = 0;   // the f16 rows xq_ currently holds (set by norm_x / the quant)
-  bool attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st);
+  bool attention_o(int li, int M, const int32_t* pos, const int32_t* slot, float* x, hipStream_t st, bool pre = false);
   void attention(int li, int M, const int32_t* pos, const int32_t* kvlen, const int32_t* slot, bool decode,
                  hipStream_t st, bool qkv_deferred, bool pre = false);
   DecodeAttnParams decode_attn_params(int li, int M, const int32_t* pos, const int32_t* slot, bool qkv_deferred) const;

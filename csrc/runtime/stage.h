@@ -26,7 +26,7 @@ struct StageOptions {
   bool cpu_q8 = true;       // CPU backend: quantized weights x int8 activation blocks (cpu_qdot.cpp); false: f32
                             // dequant + f32 dot (exact to the fp32 oracle)
   bool fused_attn = true;   // decode: one fused RoPE + KV-append + attention + merge kernel
-  int attn_o_max_ctx = 0;     // single-stream decode: attention + o-projection in one launch up to this max_ctx (0 = off)
+  int attn_o_max_ctx = 512;   // single-stream decode: attention + o-projection in one launch up to this max_ctx (0 = off)
   bool prefill_gemm = true; // prompt chunks > 16 rows: MFMA dequant-GEMM instead of 16-row GEMVs
   bool int8_gemm = false;   // M > 64 GEMMs on v_mfma_i32_16x16x64_i8: per-row int8 activations x per-row int8
                             // re-quantized weights (+1 B/weight of HBM; reduced precision, opt-in)

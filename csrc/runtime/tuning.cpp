@@ -28,8 +28,6 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"ATTN_PF_MAXWG", 512, 0, 1 << 30, nullptr},   // r7v: mb256 np 61.3 vs PF 65.3 us/layer
     {"ATTN_WG_TARGET", 256, 1, 1 << 20, nullptr},
     {"ATTN_NW8_MAXWG", 0, 0, 1 << 20, nullptr},   // r8n: 8 waves 10.97 vs 10.03 us (8B mb1): off
-    {"ATTN_KFL", 0, 0, 1, nullptr},
-    {"ATTN_ASMLD", 0, 0, 1, nullptr},
     {"GEMM2_SPLIT_WG", 256, 1, 1 << 20, nullptr},
     {"GEMM2_TW1_BELOW", 128, 0, 1 << 20, nullptr},
     {"GEMVS_NS", 2, 2, 4, ns_ok},
@@ -39,6 +37,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMVS_G", 0, 0, 8, g_ok},
     {"GEMVS_SPLIT", 0, 0, 1 << 16, nullptr},
     {"GEMVS_RPF", 1, 0, 1, nullptr},
+    {"GEMVS_DOT", 1, 0, 1, nullptr},
     {"MOE_V", 2, 1, 2, nullptr},
     {"GEMV_NW", 8, 4, 8, nw_ok},
     {"GEMV2_TW", 0, 0, 2, nullptr},

@@ -12,8 +12,6 @@ enum Knob : int {
   KNOB_ATTN_PF_MAXWG = 0,   // decode attention: next-chunk prefetch variant while M * Hkv <= this
   KNOB_ATTN_WG_TARGET,      // decode attention: workgroup target of the automatic KV split
   KNOB_ATTN_NW8_MAXWG,      // decode attention: 8-wave workgroups while M * Hkv <= this (one split; 0 off)
-  KNOB_ATTN_KFL,            // wave decode attention: whole-line K loads + register sort (0 / 1; f16 pages, head_dim 128)
-  KNOB_ATTN_ASMLD,          // wave decode attention: chunk loads as inline asm with counted vmcnt waits (0 / 1; head_dim 128)
   KNOB_GEMM2_SPLIT_WG,      // gemm2: workgroup target of its split-K
   KNOB_GEMM2_TW1_BELOW,     // gemm2: one tile per wave below this many two-tile workgroups
   KNOB_GEMVS_NS,            // gemvs: weight super-blocks in flight per wave (2, 3 or 4)
@@ -23,6 +21,7 @@ enum Knob : int {
   KNOB_GEMVS_G,             // gemvs: force tiles per workgroup (0 auto, 1, 2, 4, 8)
   KNOB_GEMVS_SPLIT,         // gemvs: force the k-split over the grid (0 auto)
   KNOB_GEMVS_RPF,           // gemvs: single-owner ATOMIC epilogue from a residual loaded at kernel start (0 / 1)
+  KNOB_GEMVS_DOT,           // gemvs: one row on the v_dot2 form (Q4_K / Q5_K / Q6_K / Q8_0; 0 = MFMA form)
   KNOB_MOE_V,               // MoE GEMV version (1 | 2)
   KNOB_GEMV_NW,             // decode GEMV: waves per workgroup (4 | 8)
   KNOB_GEMV2_TW,            // decode GEMV: tiles per wave at M > 32 (0 auto, 1, 2)

@@ -103,14 +103,21 @@ def test_gemvs_swiglu_norm(cuda, native, qt, M):
 
 
 def test_gemvs_matches_rmsnorm_plus_gemv(cuda, native):
-    """Fused norm prologue == standalone rmsnorm kernel + v2 GEMV (same f16 rounding point)."""
+    """Fused norm prologue == standalone rmsnorm kernel + v2 GEMV (same f16 rounding point).  The
+    single-row dot form takes q unrounded (the MFMA forms round each weight to f16), so the
+    comparison runs the MFMA form (GEMVS_DOT 0); the dot form is checked against the oracle."""
+    from mipipe import _native as N
     from mipipe.ops.kernels import PackedWeight, gemv, gemv_small, rmsnorm, EPI_STORE
     n, k, M = 256, 4096, 1
     raw, deq = _weights(Q.Q4_K, n, k, 41)
     w = PackedWeight(raw, Q.Q4_K, n, k)
     xf = (torch.randn(M, k) * 2).cuda()
     gamma = (torch.rand(k) + 0.5).cuda()
-    y1 = gemv_small(w, EPI_STORE, xf=xf, gamma=gamma, eps=1e-6)
+    N.check(N.lib().mp_set_knob(b"GEMVS_DOT", 0), "knob")
+    try:
+        y1 = gemv_small(w, EPI_STORE, xf=xf, gamma=gamma, eps=1e-6)
+    finally:
+        N.lib().mp_reset_knob(b"GEMVS_DOT")
     y2 = gemv(w, rmsnorm(xf, gamma, 1e-6, w.k_pad), EPI_STORE)
     torch.testing.assert_close(y1, y2, rtol=1e-4, atol=1e-4 * float(y2.abs().max()))
 
@@ -176,3 +183,46 @@ def test_engine_small_gemv_matches_v2_path(cuda, native, model_dir, name, ftype)
     a, b = outs[True][0].astype(np.float64), outs[False][0].astype(np.float64)
     assert ((a - b) ** 2).sum() / (b ** 2).sum() < 1e-5
     assert outs[True][1] == outs[False][1]
+
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q5_K, Q.Q6_K, Q.Q8_0])
+@pytest.mark.parametrize("case", ["store_norm", "atomic_split", "swiglu", "long_k"])
+def test_gemvs_single_row_dot_form(cuda, native, qt, case):
+    """M = 1 on the v_dot2 form (knob GEMVS_DOT, dequant.h dot1: biased magic pairs, per-sub-block
+    bias correction from the staged x) against the fp32 oracle and against the MFMA form: every
+    epilogue, k split over the grid (atomics), ragged N / K and a 14336-wide K."""
+    from mipipe import _native as N
+    from mipipe.ops.kernels import PackedWeight, gemv_small, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
+    n, k = (200, 1792) if case != "long_k" else (72, 14336)
+    if case == "swiglu":
+        n = 144
+    raw, deq = _weights(qt, n, k, 41 + qt)
+    w = PackedWeight(raw, qt, n, k, gateup=case == "swiglu")
+    xf = torch.randn(1, k) * 3
+    gamma = torch.rand(k) + 0.5
+    xh = _xh(1, k, w.k_pad, 13)
+    base = torch.randn(1, n)
+    outs = []
+    try:
+        for dot in (1, 0):
+            N.check(N.lib().mp_set_knob(b"GEMVS_DOT", dot), "knob")
+            if case == "store_norm":
+                outs.append(gemv_small(w, EPI_STORE, xf=xf.cuda(), gamma=gamma.cuda(), eps=1e-5).cpu())
+            elif case in ("atomic_split", "long_k"):
+                outs.append(gemv_small(w, EPI_ATOMIC, x=xh.cuda(), y=base.clone().cuda(),
+                                       nsplit=3 if case == "atomic_split" else 0).cpu() - base)
+            else:
+                outs.append(gemv_small(w, EPI_SWIGLU, xf=xf.cuda(), gamma=gamma.cuda(), eps=1e-5).float().cpu())
+    finally:
+        N.lib().mp_reset_knob(b"GEMVS_DOT")
+    if case == "store_norm":
+        ref = _xn(xf, gamma, 1e-5) @ deq.T
+    elif case == "swiglu":
+        xn = _xn(xf, gamma, 1e-5)
+        F = n // 2
+        ref = torch.nn.functional.silu(xn @ deq[:F].T) * (xn @ deq[F:].T)
+    else:
+        ref = xh[:, :k].float() @ deq.T
+    assert torch.isfinite(outs[0]).all()
+    assert nmse(outs[0], ref) < 1e-5, nmse(outs[0], ref)
+    assert nmse(outs[0], outs[1]) < 1e-5
