@@ -87,10 +87,12 @@ def parse_set(items):
     return out
 
 
-def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, devices=(0,), dump_tokens=None):
+def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, devices=(0,), dump_tokens=None,
+        trace=None):
     """Start n_seq synthetic prompts, warm up, time exactly `steps` decode rounds; returns
     (ms, p50 ms, engine info) with ms and p50 the MAX over ranks.  dump_tokens: write the generated
-    tokens (where the last stage lives) to that JSON file, after the timed region."""
+    tokens (where the last stage lives) to that JSON file, after the timed region.  trace: after the
+    timed region, 5 more rounds with the engine's span trace on, written there (Chrome JSON)."""
     eng = eng_factory()
     try:
         g = torch.Generator().manual_seed(0)
@@ -121,6 +123,10 @@ def run(eng_factory, vocab, n_seq, prompt_len, steps, warmup, world, pg_cpu, dev
         if dump_tokens:
             with open(dump_tokens, "w") as f:
                 json.dump(eng.tokens(), f)
+        if trace:
+            eng.trace(True)
+            eng.decode(5)
+            eng.write_trace(trace)
         return float(vals[0]), float(vals[1]), info
     finally:
         eng.close()
@@ -153,6 +159,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="N = 1: skip the secondary configs")
     ap.add_argument("--dump-tokens", default=None, metavar="PATH",
                     help="write the headline run's generated tokens to PATH (JSON; A/B of e.g. the bf16 wire)")
+    ap.add_argument("--trace", default=None, metavar="PATH",
+                    help="after the timed region: 5 traced decode rounds of the headline run, Chrome JSON to PATH")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="extra engine option (A/B runs), e.g. --set fused_norm=false")
     args = ap.parse_args()
@@ -205,7 +213,8 @@ def main():
     ms, p50, info = run(factory(args.model, args.ftype, args.mb_size, n_mb), MODELS[args.model]["vocab"],
                         n_mb * args.mb_size, args.prompt_len, args.steps, args.warmup, world, pg_cpu,
                         sorted(set(devices)),
-                        dump_tokens=args.dump_tokens if rank == world - 1 else None)   # the last stage's rank
+                        dump_tokens=args.dump_tokens if rank == world - 1 else None,   # the last stage's rank
+                        trace=(args.trace if world == 1 else f"{args.trace}.rank{rank}") if args.trace else None)
     n_tok = args.steps * n_mb * args.mb_size * replicas
     value = n_tok / (ms / 1e3)
 

@@ -1016,35 +1016,49 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 //   3. split-K GEMV of the slice on MFMA (the decode GEMV's dequant), atomics into the residual:
 //      Hkv partial sums per output (not bitwise reproducible: the deterministic mode keeps the
 //      two-kernel path).
+//   Waves 0-3 run the attention, waves 4-7 issue the W_o DMA: the vector memory counter retires in
+//   issue order per wave, so when the attention waves issued the DMA too, their first K / V wait
+//   waited for the whole W_o slice (~37 KB per CU) behind it.  All 8 waves then take one output tile
+//   each.  The DMA waves match the attention body's barriers (PRE: one per token, else two) and the
+//   one after each token.
 template <int DP, bool F8, int PT, int TPW, int KS, bool PRE>
-__global__ __launch_bounds__(256) void attn_o_kernel(const DecodeAttnParams p, const AttnOParams o) {
+__global__ __launch_bounds__(512) void attn_o_kernel(const DecodeAttnParams p, const AttnOParams o) {
   using D = Deq<PT>;
   constexpr int CB = D::CB, TB = KS * CB, WB = TPW * TB;
   static_assert(TB % 16 == 0, "attn_o: 16-B DMA pieces");
+  static_assert(TPW <= 8, "attn_o: one output tile per wave");
   __shared__ __attribute__((aligned(16))) uint8_t wl[WB];
   __shared__ __attribute__((aligned(16))) f16 xo[4][KS * 256];
   const int r = blockIdx.x, kvh = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tile0 = r * TPW, sb0 = kvh * KS;
   constexpr int NI = (WB + 1023) / 1024;
-  for (int i = wave; i < NI; i += 4) {
-    const int off = i * 1024 + lane * 16;
-    if (off < WB) {
-      const int u = off / TB, rem = off - u * TB;
-      const int tile = min(tile0 + u, o.ntiles - 1);
-      glds16(o.W + ((size_t)tile * o.nsb + sb0) * CB + rem, wl + i * 1024);
-    }
-  }
   const int M = p.M;
-  for (int t = 0; t < M; ++t) {
-    attn_decode_body<DP, F8, true, 4, PRE>(p, t, kvh, 0, &xo[t][0]);
-    __syncthreads();
+  if (wave >= 4) {
+    for (int i = wave - 4; i < NI; i += 4) {
+      const int off = i * 1024 + lane * 16;
+      if (off < WB) {
+        const int u = off / TB, rem = off - u * TB;
+        const int tile = min(tile0 + u, o.ntiles - 1);
+        glds16(o.W + ((size_t)tile * o.nsb + sb0) * CB + rem, wl + i * 1024);
+      }
+    }
+    for (int t = 0; t < M; ++t) {
+      if constexpr (!PRE) __syncthreads();   // the body's append barrier (one split: it owns the position)
+      __syncthreads();                       // the body's wave merge
+      __syncthreads();                       // after the token
+    }
+  } else {
+    for (int t = 0; t < M; ++t) {
+      attn_decode_body<DP, F8, true, 4, PRE>(p, t, kvh, 0, &xo[t][0]);
+      __syncthreads();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const Consts kc = make_consts();
   const int g = lane >> 4, m = lane & 15;
-  for (int u = wave; u < TPW; u += 4) {
+  for (int u = wave; u < TPW; u += 8) {
     const int tile = tile0 + u;
     if (tile >= o.ntiles) break;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1121,8 +1135,8 @@ bool attn_o_supported(const DecodeAttnParams& p, const AttnOParams& o) {
 template <bool F8, int PT>
 static void attn_o_go(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {
   const dim3 grid(o.ntiles / kAttnOTpw, p.Hkv);
-  if (p.pre) hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, true>), grid, dim3(256), 0, st, p, o);
-  else hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, false>), grid, dim3(256), 0, st, p, o);
+  if (p.pre) hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, true>), grid, dim3(512), 0, st, p, o);
+  else hipLaunchKernelGGL((mpk::attn_o_kernel<128, F8, PT, kAttnOTpw, 2, false>), grid, dim3(512), 0, st, p, o);
 }
 
 void launch_attn_o(const DecodeAttnParams& p, const AttnOParams& o, hipStream_t st) {

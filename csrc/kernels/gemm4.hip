@@ -679,9 +679,19 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
 // CUs idle (8B gate/up at M = 256: 112 workgroups of 256 rows, 112 us, against 224 of 128 rows,
 // 78 us: profiles/r8a_gemm_microbench.txt).  16-bit weights: always 128, their raw stage images
 // leave no room for three 256-row x images in LDS
-static int g4_bm(int ptype, int M, int ntiles) {
+// 8 waves x 64 columns on 128-row tiles (GEMM4_TW4 4: every dense shape, 5: the whole-K SwiGLU
+// gate/up only, 6: the split-K shapes only): a 128 x 512 workgroup tile whose A fragments each feed
+// two MFMAs (half the A-fragment LDS reads per MFMA of the 8 x 32 form) at two waves per SIMD (128
+// accumulators + ~110 registers: 237 VGPRs, no spills)
+static bool g4_w8x64(int ptype, int epi) {
+  const int k = knob(KNOB_GEMM4_TW4);
+  return !is16(ptype) && (k == 4 || (k == 5 && epi == EPI_SWIGLU) || (k == 6 && epi != EPI_SWIGLU));
+}
+
+static int g4_bm(int ptype, int M, int ntiles, int epi = -1) {
   if (is16(ptype)) return 128;
   if (knob(KNOB_GEMM3_BM)) return knob(KNOB_GEMM3_BM);
+  if (epi >= 0 && g4_w8x64(ptype, epi)) return 128;
   if (M <= 128) return 128;
   const int cgs = (ntiles + 15) / 16;
   return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;
@@ -704,12 +714,28 @@ static int g4_nwv(int ntiles, int n_mb) {
   return util(7) > util(8) + 0.05 ? 7 : 8;
 }
 
+// T16 tiles per workgroup column group
+static int g4_tpc(int ptype, int bm, int epi) {
+  if (g4_w8x64(ptype, epi)) return 32;
+  return g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;
+}
+
 template <int PT, int EPI>
-static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st) {
-  const int bm = g4_bm(PT, p.M, p.ntiles);
+static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st, int epi_sel = EPI) {
+  const int bm = g4_bm(PT, p.M, p.ntiles, epi_sel);
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
+  } else if (g4_w8x64(PT, epi_sel)) {
+    // 7 waves (448 columns) when that fills more of the 256 CUs in whole rounds
+    const int n_mb = (p.M + 127) / 128;
+    auto util = [&](int nw) {
+      const long w = (long)(p.ntiles + 4 * nw - 1) / (4 * nw) * n_mb * nsplit;
+      return (double)w / (((w + 255) / 256) * 256);
+    };
+    const int nwk = knob(KNOB_GEMM4_NW);
+    if (nwk == 7 || (nwk == 0 && util(7) > util(8) + 0.05)) gemm4_go<PT, EPI, 128, false, 7, 4>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 128, false, 8, 4>(p, nsplit, st);
   } else if (((knob(KNOB_GEMM4_TW4) & 1) && bm == 256) || (knob(KNOB_GEMM4_TW4) == 2 && bm >= 128)) {
     // 4 waves of 64 columns (one per SIMD): every A fragment read from LDS feeds two MFMAs (half the
     // LDS A traffic of 8 waves x 32 columns); the same 256-column workgroup tile and grid
@@ -736,8 +762,9 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
   if constexpr (!mpk::g4_supported<PT>()) {
     return false;
   } else {
-    const int bm = g4_bm(PT, p.M, p.ntiles);
-    const int tpc = g4_per_cu(PT, bm) == 2 && bm == 128 ? 8 : 16;   // T16 tiles per column group
+    const int esel = scratch ? EPI_ATOMIC : epi;   // split-K partial stores: the accumulating shapes
+    const int bm = g4_bm(PT, p.M, p.ntiles, esel);
+    const int tpc = g4_tpc(PT, bm, esel);   // T16 tiles per column group
     const int wgs = (p.ntiles + tpc - 1) / tpc * ((p.M + bm - 1) / bm);
     const int n_stages = p.nsb * 4;
     int ns = 1;
@@ -749,7 +776,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
       if (ns < 2 || (size_t)ns * p.M * ldp > scratch_n) return false;
       p.Y = scratch; p.ldy = ldp; p.split_stride = (int64_t)p.M * ldp;
       *nsplit_out = ns;
-      gemm4_bm<PT, EPI_STORE>(p, ns, st);
+      gemm4_bm<PT, EPI_STORE>(p, ns, st, EPI_ATOMIC);
       return true;
     }
     if (epi == EPI_ATOMIC && allow_split)
@@ -778,8 +805,8 @@ static bool gemm4_dispatch(int ptype, int epi, const GemvParams& p, bool allow_s
 
 int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
   if (!gemm4_supported(ptype)) return 1;
-  const int bm = g4_bm(ptype, M, ntiles);
-  const int tpc = g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;
+  const int bm = g4_bm(ptype, M, ntiles, EPI_ATOMIC);
+  const int tpc = g4_tpc(ptype, bm, EPI_ATOMIC);
   const int wgs = (ntiles + tpc - 1) / tpc * ((M + bm - 1) / bm);
   const int n_stages = nsb * 4;
   int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(ptype, bm));

@@ -91,39 +91,71 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
     if (nsplit == 1 && p.rpf && wave < G && et0 < p.ntiles && (lane >> 4) < M && nc0 < p.n_valid)
       resid = p.Y[(size_t)(lane >> 4) * p.ldy + nc0];
   }
+  // Load order.  The vector memory counter retires in issue order, so a wave that waits for a load
+  // issued AFTER the weight ring waits for the ring too: the prologue's x (and the QKV epilogue's
+  // position) used to sit behind the first NS super-blocks of weights, and the pos -> page -> (cos,
+  // sin) chain behind them again -- the qkv GEMV ran ~2x its weight-stream floor.  Now the loads the
+  // prologue needs go FIRST (one-row fast paths: every load of the row in flight at once), the ring
+  // next, and the dependent epilogue loads after the prologue, all under the weight stream.
+  const int k0 = sbA * 256;
+  const bool fast_norm = NORM && !(probe & 2) && M == 1 && (p.d_norm >> 2) <= 4 * GS_NT;
+  const bool fast_x = !NORM && !(probe & 2) && M == 1 && (krange >> 3) <= 4 * GS_NT;
+  // fast_norm: the first 2 float4 per thread of the f32 row and gamma (rows up to 4096; a wider
+  // row's other half follows the ring: 4 early slots took the fused-norm kernels past their register
+  // budget -- gemvs2 130 VGPRs, one workgroup per CU instead of two, 10.6 -> 13.2 us)
+  float4 xv[2], xg[2];
+  u32x4 xh[4];           // fast_x: the f16 row's k-range, 8 per thread-chunk
+  if (fast_norm) {
+    const int d4 = p.d_norm >> 2, k1 = min(sbB * 256, p.d_norm);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + u * GS_NT;
+      const bool in = c < d4, mine = in && 4 * c >= k0 && 4 * c < k1;
+      xv[u] = in ? *reinterpret_cast<const float4*>(p.Xf + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      xg[u] = mine ? reinterpret_cast<const float4*>(p.gamma)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (fast_x) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * GS_NT;
+      xh[u] = c < (krange >> 3) ? *reinterpret_cast<const u32x4*>(p.X + (size_t)k0 + 8 * c) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  // QKV epilogue: the position first (its page and (cos, sin) follow the prologue)
+  int qa_pos = 0, qa_page = 0;
+  float2 qa_cs = make_float2(1.f, 0.f);
+  const int qa_m = lane >> 4, qa_c = p.qa.col0 + (bx * G + wave) * 16 + r;
+  const bool qa_live = EPI == EPI_QKV && wave < G && qa_m < M;
+  if constexpr (EPI == EPI_QKV) {
+    if (qa_live) qa_pos = p.qa.pos[qa_m];
+  }
+  __builtin_amdgcn_sched_barrier(0);   // keep the early loads ahead of the ring
   typename D::Raw ring[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) D::load(ring[s], BufSrc{wsrc, s * CB}, lane);   // past the range: zeros, no traffic
-  // QKV epilogue: position, cache page and this lane's (cos, sin), loaded under the weight stream
-  int qa_pos = 0, qa_page = 0;
-  float2 qa_cs = make_float2(1.f, 0.f);
-  if constexpr (EPI == EPI_QKV) {
-    const QkvAppend& q = p.qa;
-    const int m = lane >> 4, c = q.col0 + (bx * G + wave) * 16 + r;
-    if (wave < G && m < M) {
-      qa_pos = q.pos[m];
-      qa_page = q.block_table[(size_t)(q.slot0 + m) * q.max_pages + (qa_pos >> 6)];
-      if (c < (q.Hq + q.Hkv) * q.hd) qa_cs = q.rope_cs[(size_t)qa_pos * (q.hd >> 1) + ((c % q.hd) >> 1)];
-    }
-  }
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- prologue: x of rows [0, M), k in [sbA*256, sbB*256) -> LDS as f16
   if (probe & 2) {
   } else if constexpr (NORM) {
     const int d4 = p.d_norm >> 2;
-    const int k0 = sbA * 256, k1 = min(sbB * 256, p.d_norm);   // this workgroup's k-range (valid part)
-    if (M == 1 && d4 <= 4 * GS_NT) {
-      // one row of <= 8192: every float4 of the row loaded once, in one batch, and kept: the thread
-      // that reduced a chunk also stages it (no second pass over x)
-      float4 v[4], gm[4];
-      float ss = 0.f;
+    const int k1 = min(sbB * 256, p.d_norm);   // this workgroup's k-range (valid part)
+    if (fast_norm) {
+      // one row of <= 8192: every float4 of the row loaded once, in one batch ahead of the weight
+      // ring, and kept: the thread that reduced a chunk also stages it (no second pass over x)
+      float4 v[4] = {xv[0], xv[1], make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+      float4 gm[4] = {xg[0], xg[1], make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+      if (d4 > 2 * GS_NT) {   // uniform: only rows wider than 4096 issue (and wait for) the second half
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = tid + u * GS_NT;
-        const bool in = c < d4, mine = in && 4 * c >= k0 && 4 * c < k1;
-        v[u] = in ? *reinterpret_cast<const float4*>(p.Xf + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        gm[u] = mine ? reinterpret_cast<const float4*>(p.gamma)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int u = 2; u < 4; ++u) {
+          const int c = tid + u * GS_NT;
+          const bool in = c < d4, mine = in && 4 * c >= k0 && 4 * c < k1;
+          v[u] = in ? *reinterpret_cast<const float4*>(p.Xf + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          gm[u] = mine ? reinterpret_cast<const float4*>(p.gamma)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
+      float ss = 0.f;
 #pragma unroll
       for (int u = 0; u < 4; ++u) ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
       ss = wave_sum(ss);
@@ -191,6 +223,12 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
         *reinterpret_cast<u32x4*>(xs + (size_t)m * krange + kl) = o;
       }
     }
+  } else if (fast_x) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * GS_NT;
+      if (c < (krange >> 3)) *reinterpret_cast<u32x4*>(xs + 8 * c) = x8_from_h8<BF>(xh[u]);
+    }
   } else {
     // f16 activations [M][ldx] with a zero tail up to nsb * 256; loads batched by 4
     const int k8 = krange >> 3, tot = M * k8;
@@ -211,6 +249,13 @@ __device__ __forceinline__ void gemvs_body(const GemvParams& p, const int nsplit
     }
   }
   __syncthreads();
+  if constexpr (EPI == EPI_QKV) {   // the position has arrived with x: page and (cos, sin), consumed in the epilogue
+    const QkvAppend& q = p.qa;
+    if (qa_live) {
+      qa_page = q.block_table[(size_t)(q.slot0 + qa_m) * q.max_pages + (qa_pos >> 6)];
+      if (qa_c < (q.Hq + q.Hkv) * q.hd) qa_cs = q.rope_cs[(size_t)qa_pos * (q.hd >> 1) + ((qa_c % q.hd) >> 1)];
+    }
+  }
   // D1: the bias-correction table, 4 floats per (super-block, lane group) of the workgroup's range
   float4* corr = reinterpret_cast<float4*>(xs + (size_t)M * krange);
   if constexpr (D1) {

@@ -790,13 +790,19 @@ void Engine::run_items(Worker& w, const std::vector<Item>& items) {
     HIP_OK(hipStreamWaitEvent(cs, w.recv_ev[mb], 0));
     if (wire) launch_act_unpack(dst, static_cast<float*>(buf), (int64_t)(bytes / 4), act_dtype_, cs);
   };
+  // a LocalLink send only records the ready event (the receiver copies): on the compute stream
+  // itself, one cross-stream hop fewer per item than through the send stream (profiles/r12a trace)
+  const bool send_direct = w.out && std::strcmp(w.out->kind(), "local") == 0;
   auto send_from = [&](int mb, const void* buf, size_t bytes) {
     if (fault_hook(w, "send")) return;
-    HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
-    HIP_OK(hipStreamWaitEvent(w.send_st, w.comp_ev[mb], 0));
-    span(w, w.send_st, 1, std::string(last ? "send tok" : "send act") + " mb" + std::to_string(mb),
-         [&] { w.out->send(buf, bytes, w.send_st); });
-    HIP_OK(hipEventRecord(w.sent_ev[mb], w.send_st));
+    hipStream_t ss = send_direct ? cs : w.send_st;
+    if (!send_direct) {
+      HIP_OK(hipEventRecord(w.comp_ev[mb], cs));
+      HIP_OK(hipStreamWaitEvent(w.send_st, w.comp_ev[mb], 0));
+    }
+    span(w, ss, 1, std::string(last ? "send tok" : "send act") + " mb" + std::to_string(mb),
+         [&] { w.out->send(buf, bytes, ss); });
+    HIP_OK(hipEventRecord(w.sent_ev[mb], ss));
     w.sent_seq[mb] = w.out->last_seq();
     w.sent_valid[mb] = true;
   };

@@ -63,7 +63,12 @@ class ThreadPool {
     }
     if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
     run_part(0);
-    while (pending_.load(std::memory_order_acquire) != 0) MP_CPU_RELAX();
+    // spin for the stragglers, yielding once the wait gets long: on an oversubscribed host (several
+    // engines, or test workers, sharing the cores) a pure spin starves the very workers it waits for
+    for (int spins = 0; pending_.load(std::memory_order_acquire) != 0;) {
+      if (++spins < 4096) MP_CPU_RELAX();
+      else std::this_thread::yield();
+    }
     fn_ = nullptr;
   }
 
@@ -89,6 +94,7 @@ class ThreadPool {
             sleepers_.fetch_sub(1);
             break;
           }
+          std::this_thread::yield();   // let a descheduled caller or sibling run (oversubscribed host)
         }
       }
       seen = gen_.load(std::memory_order_acquire);

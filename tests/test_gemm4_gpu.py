@@ -174,18 +174,22 @@ def test_gemm4_seven_wave_tiles(cuda, native, qt, nw, M):
 
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
-@pytest.mark.parametrize("form", ["tw4", "nw4"])
+@pytest.mark.parametrize("form", ["tw4", "nw4", "w8x64", "w7x64"])
 @pytest.mark.parametrize("k", [2048, 2304])
 @pytest.mark.parametrize("M", [65, 256])
 def test_gemm4_four_wave_tiles(cuda, tuning, qt, form, k, M):
-    """The 4-wave forms on every tile: 64 columns per wave with the accumulators in AGPRs
-    (GEMM4_TW4=2; the AGPR -> VGPR epilogue copies once landed on in-flight LDS reads at the loop's
-    even exit) and 32 columns per wave at two workgroups per CU (GEMM4_NW=4).  An even (32) and an
-    odd (36) stage count, STORE / SwiGLU / split-K ATOMIC over a non-zero residual."""
+    """The 64-column and 4-wave forms on every tile: 4 waves x 64 columns with the accumulators in
+    AGPRs (GEMM4_TW4=2; the AGPR -> VGPR epilogue copies once landed on in-flight LDS reads at the
+    loop's even exit), 32 columns per wave at two workgroups per CU (GEMM4_NW=4), and 8 / 7 waves x
+    64 columns on 128-row tiles (GEMM4_TW4=4, GEMM4_NW=7 for the 448-column group: 40 tiles = one
+    full group plus a partial one).  An even (32) and an odd (36) stage count, STORE / SwiGLU /
+    split-K ATOMIC over a non-zero residual."""
     from mipipe import _native as N
     from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
-    name, val = (b"GEMM4_TW4", 2) if form == "tw4" else (b"GEMM4_NW", 4)
-    N.check(N.lib().mp_set_knob(name, val), "knob")
+    knobs = {"tw4": [(b"GEMM4_TW4", 2)], "nw4": [(b"GEMM4_NW", 4)], "w8x64": [(b"GEMM4_TW4", 4)],
+             "w7x64": [(b"GEMM4_TW4", 4), (b"GEMM4_NW", 7)]}[form]
+    for name, val in knobs:
+        N.check(N.lib().mp_set_knob(name, val), "knob")
     try:
         n = 640
         raw, deq = _weights(qt, n, k, 900 + qt + M + k)
@@ -203,7 +207,8 @@ def test_gemm4_four_wave_tiles(cuda, tuning, qt, form, k, M):
         y2 = gemm(w, xh.cuda(), EPI_ATOMIC, y=base.clone().cuda(), v=4)
         assert nmse(y2.cpu() - base, ref) < 1e-5
     finally:
-        N.lib().mp_reset_knob(name)
+        for name, _ in knobs:
+            N.lib().mp_reset_knob(name)
 
 
 def _ref_gpu(xh, k, deq, qt):
@@ -271,3 +276,39 @@ def test_gemm4_splitk_qkv_width_three_splits(cuda, tuning, M):
     assert float(rows.max()) < 1e-5, f"worst row {int(rows.argmax())}: {float(rows.max()):.3e}"
 
 
+
+@pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K])
+@pytest.mark.parametrize("ns_last", TAIL_SPLITS, ids=[f"ns{a}" for a, _ in TAIL_SPLITS])
+@pytest.mark.parametrize("M", [65, 256])
+def test_gemm4_w8x64_splitk_tails(cuda, tuning, qt, ns_last, M):
+    """The 8-wave x 64-column form (GEMM4_TW4=4) on the split-K partial stores with every
+    per-split stage count 1-5 and 43, over a NaN-filled scratch: finite, at the oracle, bitwise
+    equal run to run; and the whole-K SwiGLU at the 70B gate/up K."""
+    from mipipe import _native as N
+    from mipipe.ops.kernels import PackedWeight, gemm, gemm_splitk, EPI_SWIGLU
+    ns, _ = ns_last
+    N.check(N.lib().mp_set_knob(b"GEMM4_TW4", 4), "knob")
+    try:
+        tuning(0, 0, ns, 0)
+        n, k = 1024, 8192
+        raw, deq = _weights(qt, n, k, 1900 + qt)
+        w = PackedWeight(raw, qt, n, k)
+        xh = _x(M, k, w.k_pad, 27 + M)
+        ref = _ref_gpu(xh, k, deq, qt)
+        base = torch.randn(M, n)
+        outs = []
+        for _ in range(2):
+            y2 = base.clone().cuda()
+            assert gemm_splitk(w, xh.cuda(), y2, max_splits=ns) == ns
+            outs.append(y2.cpu())
+        assert torch.isfinite(outs[0]).all()
+        assert nmse(outs[0] - base, ref) < 1e-5
+        assert torch.equal(outs[0], outs[1])
+        if ns == 128:
+            tuning(0, 0, 0, 0)
+            h = gemm(w, xh.cuda(), EPI_SWIGLU, v=4)
+            gi = torch.tensor([16 * (o // 8) + (o % 8) for o in range(n // 2)])
+            href = torch.nn.functional.silu(ref[:, gi]) * ref[:, gi + 8]
+            assert torch.isfinite(h.float()).all() and nmse(h.float().cpu(), href) < 1e-4
+    finally:
+        N.lib().mp_reset_knob(b"GEMM4_TW4")
