@@ -68,6 +68,21 @@ static int gemv2_tw(int M, int epi, int ntiles = 1 << 30) {
 }
 
 int gemv_tiles_per_wave(int M, int epi) { return gemv2_tw(M, epi); }
+
+int gemv_auto_split(int ntiles, int nsb, int M, int epi) {
+  if (epi != EPI_ATOMIC) return 1;
+  const int tpw = gemv_tiles_per_wave(M, epi);
+  // wide row groups (M > 32) pay more per split (x re-staged per split, M atomics per output):
+  // 70B M=64 best at ~2048 tile-waves (qkv 31 -> 29 us, o 25.4 -> 22.1 us; r1g_gemv_tiles_per_wave_ab.txt)
+  const int target_waves = (M > 32 ? knob(KNOB_GEMV_SPLIT_WAVES) : 4096) / tpw;
+  const int waves = (ntiles + tpw - 1) / tpw;
+  int s = (target_waves + waves - 1) / waves;
+  // >= GEMV_SPLIT_MINSB (4) super-blocks per split, except for a handful of tiles (MoE router: one
+  // tile), where the serial super-block loop of a single workgroup would dominate
+  const int minsb = knob(KNOB_GEMV_SPLIT_MINSB);
+  const int smax = ntiles <= 4 ? nsb : (nsb / minsb > 1 ? nsb / minsb : 1);
+  return s < 1 ? 1 : (s > smax ? smax : s);
+}
 void set_gemv_tpw(int t) { set_knob("GEMV2_TW", (t == 1 || t == 2) ? t : 0); }
 
 void launch_gemv(int ptype, int epi, GemvParams p, int nsplit, hipStream_t st) {

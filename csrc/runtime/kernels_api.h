@@ -77,19 +77,10 @@ int gemv_tiles_per_wave(int M, int epi);
 // split-K factor giving ~target waves for an ATOMIC-epilogue GEMV (>= 4 super-blocks per split)
 // Cold-weight sweep on MI355X (tools/gemv_bench.py, 70B shapes): ~4096 tile-waves per launch
 // (e.g. Wo M=16: 4 tiles/wave x 8 splits = 14 us vs 20 us at 1 tile x 2 splits).
-inline int gemv_auto_split(int ntiles, int nsb, int M, int epi) {
-  if (epi != EPI_ATOMIC) return 1;
-  const int tpw = gemv_tiles_per_wave(M, epi);
-  // wide row groups (M > 32) pay more per split (x re-staged per split, M atomics per output):
-  // 70B M=64 best at ~2048 tile-waves (qkv 31 -> 29 us, o 25.4 -> 22.1 us; r1g_gemv_tiles_per_wave_ab.txt)
-  const int target_waves = (M > 32 ? 2048 : 4096) / tpw;
-  const int waves = (ntiles + tpw - 1) / tpw;
-  int s = (target_waves + waves - 1) / waves;
-  // >= 4 super-blocks per split, except for a handful of tiles (MoE router: one tile), where
-  // the serial super-block loop of a single workgroup would dominate
-  const int smax = ntiles <= 4 ? nsb : (nsb / 4 > 1 ? nsb / 4 : 1);
-  return s < 1 ? 1 : (s > smax ? smax : s);
-}
+// split-K factor of a decode GEMV launch (ATOMIC only): tile-waves over the whole grid against a
+// target (knob GEMV_SPLIT_WAVES for M > 32, 4096 below), at least GEMV_SPLIT_MINSB super-blocks per
+// split; implemented in gemv.hip
+int gemv_auto_split(int ntiles, int nsb, int M, int epi);
 void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, int ldo, hipStream_t st);
 
 // Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.

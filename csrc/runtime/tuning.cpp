@@ -52,6 +52,8 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
     {"GEMM4_TW4", 1, 0, 6, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
+    {"GEMV_SPLIT_WAVES", 2048, 64, 1 << 20, nullptr},
+    {"GEMV_SPLIT_MINSB", 4, 1, 64, nullptr},
 #ifdef MIPIPE_TIMING_PROBES
 #include "timing_probes.inc"
 #endif

@@ -37,7 +37,10 @@ enum Knob : int {
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
   KNOB_GEMM4_TW4,           // gemm4 dense: 4 waves x 64 columns (two MFMAs per A fragment) instead of 8 x 32
-                            // (0 off, 1 the 256-row tiles only, 2 also the 128-row tiles, 3 = 1 + the 128-row MoE tiles)
+                            // (0 off, 1 the 256-row tiles only, 2 also the 128-row tiles, 3 = 1 + the 128-row MoE tiles;
+                            // 8 / 7 waves x 64 columns on 128-row tiles: 4 every shape, 5 gate/up only, 6 split-K only)
+  KNOB_GEMV_SPLIT_WAVES,    // decode GEMV (M > 32): tile-wave target of the automatic split-K
+  KNOB_GEMV_SPLIT_MINSB,    // decode GEMV: fewest super-blocks per split
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes that skip work (wrong results): only in a `make PROBES=1` build, never in the
   // default library, so no environment variable can corrupt a serving or bench run
