@@ -50,11 +50,8 @@ __global__ __launch_bounds__(NW * 64) void gemv2_kernel(const GemvParams p) {
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
-  // prompt GEMM use (p.m_blocks > 1): blockIdx.x = tile group * m_blocks + row block, so the row
-  // blocks sharing a weight tile group are dispatched together (their weight reads after the first
-  // hit the memory-side cache)
-  const int mblk = p.m_blocks > 1 ? (int)blockIdx.x % p.m_blocks : 0;
-  const int bx = p.m_blocks > 1 ? (int)blockIdx.x / p.m_blocks : (int)blockIdx.x;
+  const int mblk = 0;   // one row block of <= 64 rows (the 128-row prompt GEMM form, gemm2, is retired: gemm4)
+  const int bx = (int)blockIdx.x;
   const int tile0 = (bx * NW + wave) * TW;
   const size_t r_off = (size_t)mblk * 16 * MT;   // first row of this workgroup
   const int sbA = blockIdx.y * p.sb_per_split;
@@ -307,92 +304,6 @@ void launch_gemv2(int ptype, int epi, const GemvParams& p, int nsplit, int nw, i
     case P_Q4_0: gemv2_pt<P_Q4_0>(epi, p, nsplit, nw, tw, st); break;
     case P_F16: gemv2_pt<P_F16>(epi, p, nsplit, nw, tw, st); break;
     case P_BF16: gemv2_pt<P_BF16>(epi, p, nsplit, nw, tw, st); break;
-  }
-}
-
-// split-K factor of a gemm2 launch that may split (two tiles per wave): narrow outputs (8B down /
-// qkv, 70B o / down: 16-32 tile groups) leave CUs idle, so K is split over workgroups as far as the
-// grid still runs in ONE round of one workgroup per CU (135 KB of LDS each) and >= 4 super-blocks
-// per split (M=512: 70B down 409 -> 261 us, o 136 -> 99, 8B down 206 -> 94; a second round cost
-// 70B qkv 142 -> 170)
-int gemm2_splits(int ntiles, int nsb, int M) {
-  const int groups = (ntiles + 15) / 16, m_blocks = (M + 127) / 128;
-  const int wgs = groups * m_blocks;
-  const int split_wg = knob(KNOB_GEMM2_SPLIT_WG);
-  int nsplit = wgs < split_wg ? std::min(split_wg / wgs, std::max(1, nsb / 4)) : 1;
-  const int per = (nsb + nsplit - 1) / nsplit;
-  return (nsb + per - 1) / per;
-}
-
-// force_split > 0: that many K splits whatever the epilogue (EPI_STORE into per-split partials,
-// p.split_stride apart: launch_gemm2_splitk)
-template <int PT, int EPI, int TW>
-static void gemm2_go(GemvParams p, bool allow_split, hipStream_t st, int force_split = 0) {
-  constexpr int NW = 8, MT = 8;
-  p.m_blocks = (p.M + 16 * MT - 1) / (16 * MT);
-  const int groups = (p.ntiles + NW * TW - 1) / (NW * TW);
-  const int wgs = groups * p.m_blocks;
-  int nsplit = force_split > 0 ? force_split : (EPI == EPI_ATOMIC && allow_split) ? gemm2_splits(p.ntiles, p.nsb, p.M) : 1;
-  p.sb_per_split = (p.nsb + nsplit - 1) / nsplit;
-  nsplit = (p.nsb + p.sb_per_split - 1) / p.sb_per_split;
-  hipLaunchKernelGGL((mpk::gemv2_kernel<PT, EPI, NW, 2, MT, TW, false>), dim3(wgs, nsplit), dim3(NW * 64), 0, st, p);
-}
-
-template <int PT, int TW>
-static void gemm2_cfg(int epi, const GemvParams& p, bool allow_split, hipStream_t st) {
-  switch (epi) {
-    case EPI_STORE: return gemm2_go<PT, EPI_STORE, TW>(p, allow_split, st);
-    case EPI_ATOMIC: return gemm2_go<PT, EPI_ATOMIC, TW>(p, allow_split, st);
-    case EPI_SWIGLU: return gemm2_go<PT, EPI_SWIGLU, TW>(p, allow_split, st);
-  }
-}
-
-template <int PT>
-static void gemm2_pt(int epi, const GemvParams& p, bool allow_split, hipStream_t st) {
-  // a grid of at most half as many two-tile workgroups as CUs that cannot split K (SWIGLU / STORE,
-  // or deterministic) takes one tile per wave: twice the workgroups for twice the A-fragment LDS
-  // reads.  Measured (r5m): 8B mb128 (gate/up 112 workgroups) 15.9k -> 17.3k tok/s, but 8B mb256
-  // and 70B mb128 (224 workgroups) lose 4-7 %, hence the threshold of 128
-  const int min_wg = knob(KNOB_GEMM2_TW1_BELOW);
-  const int wgs2 = (p.ntiles + 15) / 16 * ((p.M + 127) / 128);
-  const bool splits = epi == EPI_ATOMIC && allow_split;
-  if (!splits && wgs2 < min_wg) gemm2_cfg<PT, 1>(epi, p, allow_split, st);
-  else gemm2_cfg<PT, 2>(epi, p, allow_split, st);
-}
-
-// split-K without atomics: split s stores its partial tile to scratch + s * M * ldp, then one
-// reduction adds the nsplit partials (fixed order) into Y.  Returns false (nothing launched) when
-// the shape does not split or the scratch is too small; the caller then takes launch_gemm2.
-bool launch_gemm2_splitk(int ptype, GemvParams p, float* scratch, size_t scratch_n, hipStream_t st, bool reduce,
-                         int* nsplit_out) {
-  if (is16(ptype) || ptype == P_I8 || p.bias) return false;
-  const int ns = gemm2_splits(p.ntiles, p.nsb, p.M);
-  const int ldp = p.ntiles * 16;
-  if (ns < 2 || (size_t)ns * p.M * ldp > scratch_n) return false;
-  float* Y = p.Y;
-  const int ldy = p.ldy;
-  p.Y = scratch; p.ldy = ldp; p.split_stride = (int64_t)p.M * ldp;
-  switch (ptype) {
-    case P_Q4_K: gemm2_go<P_Q4_K, EPI_STORE, 2>(p, false, st, ns); break;
-    case P_Q5_K: gemm2_go<P_Q5_K, EPI_STORE, 2>(p, false, st, ns); break;
-    case P_Q6_K: gemm2_go<P_Q6_K, EPI_STORE, 2>(p, false, st, ns); break;
-    case P_Q8_0: gemm2_go<P_Q8_0, EPI_STORE, 2>(p, false, st, ns); break;
-    case P_Q4_0: gemm2_go<P_Q4_0, EPI_STORE, 2>(p, false, st, ns); break;
-    default: return false;
-  }
-  if (nsplit_out) *nsplit_out = ns;
-  if (reduce) launch_splitk_reduce(scratch, ns, (int64_t)p.M * ldp, ldp, p.M, p.n_valid, Y, ldy, st);
-  return true;
-}
-
-void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split) {
-  switch (ptype) {
-    case P_Q4_K: gemm2_pt<P_Q4_K>(epi, p, allow_split, st); break;
-    case P_Q5_K: gemm2_pt<P_Q5_K>(epi, p, allow_split, st); break;
-    case P_Q6_K: gemm2_pt<P_Q6_K>(epi, p, allow_split, st); break;
-    case P_Q8_0: gemm2_pt<P_Q8_0>(epi, p, allow_split, st); break;
-    case P_Q4_0: gemm2_pt<P_Q4_0>(epi, p, allow_split, st); break;
-    default: launch_gemm(ptype, epi, p, st); break;   // f16 weights: the 64 x 64 GEMM
   }
 }
 

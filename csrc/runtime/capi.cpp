@@ -177,33 +177,6 @@ int mp_op_gemm(int ptype, int epi, const void* W, int ntiles, int nsb, const voi
   API_CATCH(-1)
 }
 
-int mp_op_gemm2(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
-                int ldy, void* H, int ldh, int n_valid, void* stream) {
-  API_TRY
-  GemvParams p{};
-  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
-  p.H = (f16*)H; p.ldh = ldh; p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
-  launch_gemm2(ptype, epi, p, (hipStream_t)stream);
-  return 0;
-  API_CATCH(-1)
-}
-
-// gemm2 split-K through per-split partial stores + the fixed-order reduction into Y (the engine's
-// gemm_splitk_store path); returns 1 when launched, 0 when the shape does not split (nothing launched)
-int mp_op_gemm2_splitk(int ptype, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y, int ldy,
-                       int n_valid, void* scratch, long long scratch_floats, void* stream) {
-  API_TRY
-  GemvParams p{};
-  p.W = (const uint8_t*)W; p.X = (const f16*)X; p.ldx = ldx; p.M = M; p.Y = (float*)Y; p.ldy = ldy;
-  p.ntiles = ntiles; p.nsb = nsb; p.n_valid = n_valid;
-  const bool ok = launch_gemm2_splitk(ptype, p, (float*)scratch, (size_t)scratch_floats, (hipStream_t)stream);
-  HIP_OK(hipGetLastError());
-  return ok ? 1 : 0;
-  API_CATCH(-1)
-}
-
-int mp_gemm2_splits(int ntiles, int nsb, int M) { return gemm2_splits(ntiles, nsb, M); }
-
 int mp_op_gemm3(int ptype, int epi, const void* W, int ntiles, int nsb, const void* X, int ldx, int M, void* Y,
                 int ldy, void* H, int ldh, int n_valid, int allow_split, void* stream) {
   API_TRY

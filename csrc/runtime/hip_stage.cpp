@@ -509,9 +509,7 @@ void HipStage::alloc_runtime() {
       if (!m.d || is16(m.ptype)) return;
       for (int M : {opt_.mb_size, opt_.prefill_chunk}) {
         if (M <= 64) continue;
-        int ns = gemm2_splits((int)m.dims.ntiles, (int)m.dims.nsb, M);
-        if (opt_.prefill_gemm_v == 4 || opt_.prefill_gemm_v == 0)
-          ns = std::max(ns, gemm4_splits(m.ptype, (int)m.dims.ntiles, (int)m.dims.nsb, M));
+        const int ns = gemm4_splits(m.ptype, (int)m.dims.ntiles, (int)m.dims.nsb, M);
         if (ns > 1) need = std::max(need, (size_t)ns * M * m.dims.ntiles * 16);
       }
     };
@@ -736,10 +734,10 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
   // round 5: with the tail-stage hazard gone (tools/isa_lint.py) and the saddr DMA, gemm4 takes the
   // split-K shapes too: 70B mb256 a tie (5797 / 5786 vs 5800 / 5776), 8B mb256 30401 vs 29709
   // (profiles/r10d_splitk_ab_and_prof.txt)
-  const int gv = opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v : is16(m.ptype) ? 3 : 4;
+  // (round 6: the 128-row gemm2 form is retired; prefill_gemm_v = 2 takes gemm4)
+  const int gv = opt_.prefill_gemm_v == 2 ? 4 : opt_.prefill_gemm_v != 0 ? opt_.prefill_gemm_v : is16(m.ptype) ? 3 : 4;
   const bool wide_swiglu = epi == EPI_SWIGLU && m.dims.ntiles / 16 >= 192;
   const bool v3 = gv == 3;
-  const bool v2 = gv == 2 && !is16(m.ptype);
   if (M > 64 && opt_.prefill_gemm && m.i8 && xq_ && X) {
     // int8_gemm: x rows quantized per row, int8 MFMA against the re-quantized copy (gemm3<P_I8>)
     const int K = (int)m.dims.nsb * 256;
@@ -772,26 +770,12 @@ void HipStage::gemv(const PackedMat& m, int epi, const f16* X, int ldx, int M, f
     }
     return;
   }
-  if (M > 64 && opt_.prefill_gemm && (v3 || v2 || !wide_swiglu)) {
+  if (M > 64 && opt_.prefill_gemm && (v3 || !wide_swiglu)) {
     GemvParams p{};
     p.W = m.d; p.X = X; p.ldx = ldx; p.M = M; p.Y = Y; p.ldy = ldy; p.H = H; p.ldh = ldh;
     p.ntiles = (int)m.dims.ntiles; p.nsb = (int)m.dims.nsb; p.n_valid = n_valid;
     if (v3) launch_gemm3(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
-    else if (v2) {
-      // split-K partial stores + a fixed-order reduction (gemm_splitk_store; into the residual x it
-      // is deferred to the next RMSNorm, norm_x) or float atomics into Y
-      // (fixed-order: also the deterministic mode's split-K, which otherwise runs unsplit)
-      const bool sk = opt_.gemm_splitk_store && sk_part_ && epi == EPI_ATOMIC && allow_split;
-      const bool defer = sk && Y == sk_defer_;
-      if (sk) flush_sk(st);   // the scratch is about to be overwritten
-      int ns = 0;
-      if (sk && launch_gemm2_splitk(m.ptype, p, sk_part_, sk_part_n_, st, !defer, &ns)) {
-        if (defer) sk_pend_ = SkPending{Y, M, n_valid, ldy, ns, p.ntiles * 16, (int64_t)M * p.ntiles * 16};
-      } else {
-        launch_gemm2(m.ptype, epi, p, st, allow_split && !opt_.deterministic);
-      }
-    }
-    else launch_gemm(m.ptype, epi, p, st);
+    else launch_gemm(m.ptype, epi, p, st);   // the types gemm4 does not take (Q4_0), or prefill_gemm_v = 1
     return;
   }
   for (int r0 = 0; r0 < M; r0 += 64) {

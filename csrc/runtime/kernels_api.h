@@ -52,7 +52,7 @@ struct GemvParams {
   const float* bias = nullptr;   // [n] added once (split 0) to STORE / ATOMIC outputs
   float* zero = nullptr;         // side job after the GEMV: zero_n floats cleared
   int64_t zero_n = 0;
-  int m_blocks = 1;              // prompt GEMM (launch_gemm2): row blocks of 128 per weight tile group
+  int m_blocks = 1;              // (unused: the retired 128-row gemm2 form)
   // P_I8 (launch_gemm3): X holds int8 rows (ldx in bytes), y = xscale[m] * wscale[n] * sum(xq * wq)
   const float* xscale = nullptr;
   const float* wscale = nullptr;
@@ -85,19 +85,8 @@ void launch_unpack(int ptype, const uint8_t* W, int ntiles, int nsb, f16* out, i
 
 // Prefill GEMM (M > 16): Y[M][N] (+)= X[M][K] W^T, MFMA tiles with in-LDS dequant.
 void launch_gemm(int ptype, int epi, GemvParams p, hipStream_t st);
-// Prefill GEMM v2: the decode GEMV design widened to 128 rows per workgroup (8 MFMA row groups per
-// dequantized weight fragment, two 16-column tiles per wave, 256 columns x 128 rows per 8-wave
-// workgroup, whole K per workgroup); EPI_ATOMIC adds into Y (single writer per element)
-// (EPI_ATOMIC: split-K over workgroups when there are few output tiles, unless allow_split is false)
-// split-K factor gemm2 uses for a splittable (ATOMIC) launch of this shape
-int gemm2_splits(int ntiles, int nsb, int M);
-// gemm2 split-K through per-split partial stores + a fixed-order reduction into Y (no atomics);
-// false = not applicable (no split, 16-bit weights, scratch too small): nothing was launched
-// reduce = false: the partials are left in scratch ([nsplit][M][ntiles * 16], *nsplit_out splits)
-// for the consumer to absorb (launch_rmsnorm_acc)
-bool launch_gemm2_splitk(int ptype, GemvParams p, float* scratch, size_t scratch_n, hipStream_t st,
-                         bool reduce = true, int* nsplit_out = nullptr);
-void launch_gemm2(int ptype, int epi, GemvParams p, hipStream_t st, bool allow_split = true);
+// (The 128-row "gemm2" form of the decode GEMV, the quantized prompt GEMM of rounds 1-4, is retired:
+// gemm4 took every quantized shape in round 5; the last commit with it is d54fe81.)
 // Prompt / wide-decode GEMM v3 (gemm3.hip): BM x BN = {128, 256} x {128, 256} workgroup tiles, each
 // weight element dequantized once per workgroup into an f16 LDS image shared by its 8 waves,
 // X and the raw quants staged by global_load_lds, 16x16x32 f16 MFMA; EPI_ATOMIC splits K over

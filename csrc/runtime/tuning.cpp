@@ -29,7 +29,6 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"ATTN_WG_TARGET", 256, 1, 1 << 20, nullptr},
     {"ATTN_NW8_MAXWG", 0, 0, 1 << 20, nullptr},   // r8n: 8 waves 10.97 vs 10.03 us (8B mb1): off
     {"GEMM2_SPLIT_WG", 256, 1, 1 << 20, nullptr},
-    {"GEMM2_TW1_BELOW", 128, 0, 1 << 20, nullptr},
     {"GEMVS_NS", 2, 2, 4, ns_ok},
     {"GEMVS_S", 64, 1, 1 << 20, nullptr},
     {"GEMVS2", 1, 0, 1, nullptr},

@@ -12,8 +12,7 @@ enum Knob : int {
   KNOB_ATTN_PF_MAXWG = 0,   // decode attention: next-chunk prefetch variant while M * Hkv <= this
   KNOB_ATTN_WG_TARGET,      // decode attention: workgroup target of the automatic KV split
   KNOB_ATTN_NW8_MAXWG,      // decode attention: 8-wave workgroups while M * Hkv <= this (one split; 0 off)
-  KNOB_GEMM2_SPLIT_WG,      // gemm2: workgroup target of its split-K
-  KNOB_GEMM2_TW1_BELOW,     // gemm2: one tile per wave below this many two-tile workgroups
+  KNOB_GEMM2_SPLIT_WG,      // gemm3 / gemm4: workgroup target of the split-K (name kept from the retired gemm2)
   KNOB_GEMVS_NS,            // gemvs: weight super-blocks in flight per wave (2, 3 or 4)
   KNOB_GEMVS_S,             // gemvs: super-blocks per wave target of the work split
   KNOB_GEMVS2,              // gemvs: q+k | v of mixed-type layers in one launch (0 / 1)

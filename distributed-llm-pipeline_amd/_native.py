@@ -46,8 +46,6 @@ _SIGS = {
                     c_int, c_int, c_int, c_void_p], c_int),
     "mp_op_gemm": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                     c_int, c_int, c_void_p], c_int),
-    "mp_op_gemm2": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
-                    c_int, c_int, c_void_p], c_int),
     "mp_op_gemm3": ([c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                      c_int, c_int, c_int, c_void_p], c_int),
     "mp_set_gemm3_tuning": ([c_int, c_int, c_int, c_int], c_int),
@@ -60,9 +58,6 @@ _SIGS = {
     "mp_op_router_logits": ([c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p], c_int),
     "mp_op_gemm4_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                             ctypes.c_longlong, c_void_p], c_int),
-    "mp_op_gemm2_splitk": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
-                            ctypes.c_longlong, c_void_p], c_int),
-    "mp_gemm2_splits": ([c_int, c_int, c_int], c_int),
     "mp_op_quant_i8": ([c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p], c_int),
     "mp_op_gemm3_i8": ([c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                         c_void_p, c_void_p, c_int, c_void_p], c_int),

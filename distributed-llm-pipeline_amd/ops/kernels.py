@@ -127,8 +127,9 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
          n_valid: int | None = None, v: int = 3, allow_split: bool = True) -> torch.Tensor:
     """Prefill / wide-decode GEMM (any M): x f16 [M][K_pad]. Same outputs as gemv (ATOMIC adds).
     v=3: BM x BN in {128, 256}^2 workgroup tiles, weights dequantized once per workgroup into LDS
-    (launch_gemm3; ATOMIC may split K over workgroups unless allow_split is False); v=2: 128-row x
-    256-column tiles with per-wave register dequant (launch_gemm2); v=1: the 64 x 64 tile GEMM."""
+    (launch_gemm3; ATOMIC may split K over workgroups unless allow_split is False); v=4: the 32x32x16
+    MFMA GEMM (launch_gemm4); v=1: the 64 x 64 tile GEMM.  (v=2, the 128-row form of the decode GEMV,
+    is retired.)"""
     assert x.dtype == torch.float16 and x.shape[1] == w.k_pad and x.is_contiguous()
     M = x.shape[0]
     L = N.lib()
@@ -137,7 +138,8 @@ def gemm(w: PackedWeight, x: torch.Tensor, epi: int = EPI_STORE, y: torch.Tensor
     elif v == 4:
         fn = lambda *a: L.mp_op_gemm4(*a[:-1], int(allow_split), a[-1])
     else:
-        fn = L.mp_op_gemm2 if v == 2 else L.mp_op_gemm
+        assert v == 1, "gemm: v must be 1, 3 or 4 (the v=2 form is retired)"
+        fn = L.mp_op_gemm
     if epi == EPI_SWIGLU:
         F = w.n // 2
         h = torch.zeros(M, F, dtype=torch.float16, device=x.device) if y is None else y

@@ -26,7 +26,7 @@ def _run(syn, ftype, mb, stages=1, **kw):
 
 @pytest.mark.parametrize("mb", [1, 16, 64, 128, 256])
 def test_deterministic_bitwise_runs_and_pp2(cuda, native, mb):
-    """mb > 64 runs the decode projections on the GEMMs: the split-K ones (qkv / o / down, gemm2)
+    """mb > 64 runs the decode projections on the GEMMs: the split-K ones (qkv / o / down, gemm4)
     store per-split partials that a fixed-order reduction adds (`gemm_splitk_store`, the default);
     the whole-K ones (gate/up, the LM head, gemm4) have one writer per output element."""
     a, ta = _run(WIDE, "Q4_K", mb, deterministic=True)

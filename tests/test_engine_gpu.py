@@ -222,7 +222,7 @@ def test_microbatch_invariance(cuda, native, model_dir):
 @pytest.mark.parametrize("mb_size", [24, 40, 64, 96, 200])
 def test_wide_microbatch_matches_single(cuda, native, model_dir, mb_size):
     """Decode micro-batches above 16 rows: the GEMV with 2-4 MFMA row groups per weight fragment;
-    above 64 rows the decode projections and the LM head run on the GEMMs (gemm2 / gemm4).  Rows on
+    above 64 rows the decode projections and the LM head run on the GEMMs (gemm4).  Rows on
     both sides of every 64-row boundary and the last row are checked against the fp32 oracle: a
     single-block 64-thread position advance once froze rows >= 64 at their prompt position (found by
     the 70B-width test)."""

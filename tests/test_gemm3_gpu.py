@@ -1,7 +1,7 @@
 """GEMM v3 (csrc/kernels/gemm3.hip) against a plain PyTorch fp32 reference.
 
 The v3 GEMM runs the wide (> 64-row) decode micro-batches and prompt chunks of 16-bit weights
-(hip_stage.cpp HipStage::gemv picks it for F16 / BF16; quantized weights take gemm2 or gemm4), and
+(hip_stage.cpp HipStage::gemv picks it for F16 / BF16; quantized weights take gemm4), and
 every type through prefill_gemm_v=3.  Besides small shapes in every quant type, tile shape and
 epilogue, it is checked at the 70B widths (K = 8192 / 28672, split-K forced to 1, 4 and 8)."""
 import math

@@ -136,15 +136,15 @@ def test_gemm4_asymmetric_identity(cuda, tuning, bm):
 
 
 @pytest.mark.parametrize("M", [96, 256])
-def test_gemm4_matches_gemm2_q4k(cuda, native, M):
-    """Same packed Q4_K weights through the 32x32 GEMM and the 16x16 GEMM v2: equal up to f32
+def test_gemm4_matches_gemm3_q4k(cuda, native, M):
+    """Same packed Q4_K weights through the 32x32 GEMM and the 16x16 GEMM v3: equal up to f32
     summation order."""
     from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE
     n, k = 512, 4096
     raw, _ = _weights(Q.Q4_K, n, k, 5)
     w = PackedWeight(raw, Q.Q4_K, n, k)
     xh = _x(M, k, w.k_pad, 8).cuda()
-    assert nmse(gemm(w, xh, EPI_STORE, v=4).cpu(), gemm(w, xh, EPI_STORE, v=2).cpu()) < 1e-9
+    assert nmse(gemm(w, xh, EPI_STORE, v=4).cpu(), gemm(w, xh, EPI_STORE, v=3).cpu()) < 1e-8
 
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
