@@ -496,20 +496,13 @@ static void gemvs_g(const GemvParams& p, const GemvsPlan& pl, hipStream_t st) {
   // (NS 2: 80 VGPRs, 3 workgroups per CU; NS 4: 104 VGPRs, 2; NS 8: 3 waves/SIMD).  r5o / r5p:
   // 8B Q4_K_M mb1 NS 2 / 3 / 4 / 8 -> 548 / 541 / 524 / 441 tok/s, 70B Q4_K 105.4 / 106.6 / 104.4 / 91.1
   // (the knob only admits 2, 3 and 4; 16-bit weights always run the default depth)
-  int ns = knob(KNOB_GEMVS_NS);
-  // ... except where residency is not the limit: an unnormed residual GEMV (down, o) whose grid is
-  // one workgroup per CU or less keeps 4 super-blocks in flight per wave (twice the bytes in flight
-  // per CU: Little's law against the ~2 us HBM latency of a single round)
-  const bool one_round = !NORM && EPI == EPI_ATOMIC && ns == 2 && (long)(p.ntiles + pl.G - 1) / pl.G * pl.nsplit <= 256;
+  // (4 super-blocks in flight for the one-round residual GEMVs -- down, o: one workgroup per CU, so
+  // residency is not what limits them -- measured slower: Q6_K down 12.81 -> 14.96 us, Q4_K down
+  // 9.41 -> 9.58; profiles/r12g_prof_8b_mb1.txt)
+  const int ns = knob(KNOB_GEMVS_NS);
   if constexpr (mpk::dot1_supported<PT>()) {
-    if (use_d1(PT, p)) {
-      if constexpr (!NORM && EPI == EPI_ATOMIC) {
-        if (one_round) return gemvs_gn<PT, EPI, NORM, 4, true>(p, pl, st);
-      }
-      return gemvs_gn<PT, EPI, NORM, 2, true>(p, pl, st);
-    }
+    if (use_d1(PT, p)) return gemvs_gn<PT, EPI, NORM, 2, true>(p, pl, st);
   }
-  if (one_round) ns = 4;
   if constexpr (!is16(PT)) {
     if (ns == 2) return gemvs_gn<PT, EPI, NORM, 2>(p, pl, st);
     if (ns == 3) return gemvs_gn<PT, EPI, NORM, 3>(p, pl, st);

@@ -128,14 +128,20 @@ std::vector<GenResult> Session::run(std::vector<GenRequest>& reqs) {
   }
   eng_->start(prompts);
   const double t1 = now_ms();
-  if (n_max > 0)
-    for (size_t i = 0; i < reqs.size(); ++i) consume(i, eng_->tokens()[i].back(), 0);
+  // a middle rank of a multi-process pipeline sees no tokens (they travel the ring from the last
+  // stage to the first): nothing to consume there
+  if (n_max > 0) {
+    const auto toks = eng_->tokens();
+    for (size_t i = 0; i < reqs.size(); ++i)
+      if (i < toks.size() && !toks[i].empty()) consume(i, toks[i].back(), 0);
+  }
   int step = 1;
   auto any_active = [&] { return std::any_of(active.begin(), active.end(), [](bool b) { return b; }); };
   while (step < n_max && (!early_stop || any_active())) {
     eng_->decode_steps(1);
     const auto toks = eng_->tokens();
-    for (size_t i = 0; i < reqs.size(); ++i) consume(i, toks[i].back(), step);
+    for (size_t i = 0; i < reqs.size(); ++i)
+      if (i < toks.size() && !toks[i].empty()) consume(i, toks[i].back(), step);
     ++step;
   }
   const double t2 = now_ms();

@@ -27,6 +27,8 @@ struct CliOptions {
   bool bench = false;
   int bench_prompt = 128, bench_warmup = 3, bench_steps = 20;
   std::string trace;
+  std::string rpc;            // --rpc host:port,... (without --world): stage workers to attach to (rpc.h)
+  std::string master;         // --master HOST: this process's address as the workers see it (rpc.h)
   std::map<std::string, std::string> extra;   // tool-specific flags (--port, --static, ...)
 };
 
@@ -99,7 +101,8 @@ inline void print_common_usage(FILE* f) {
           "  --next HOST --master HOST --base-port P   TCP ring neighbours (prima.cpp style)\n"
           "  --gpu-mem GiB [--force]   per-GPU memory budget (caps auto KV; fail if a stage exceeds it)\n"
           "  --prefetch                madvise(WILLNEED) the GGUF ranges this process uploads\n"
-          "  --rpc host:port,...       accepted for llama-cli parity: hosts of the stage processes\n"
+          "  --rpc host:port,...       stage workers (mi-cli --rpc-server PORT) to attach to; with --world: the\n"
+          "                            hosts of the stage processes; no worker answering: one local stage per entry\n"
           "logging:\n"
           "  --verbose, --log-file FILE, --trace FILE (Chrome trace of the pipeline)\n");
 }
@@ -205,9 +208,12 @@ inline CliOptions parse_cli(int argc, char** argv,
     e["hosts"] = hosts;
     if (!next.empty()) e["next_host"] = next;
   } else if (!rpc.empty() && stages == 0) {
-    // llama-cli --rpc lists remote workers; here every stage is a local GPU: one stage per entry
+    // llama-cli --rpc lists remote workers (rpc.h attaches to them when they answer); without
+    // workers every stage is a local GPU: one stage per entry
     e["stages"] = (int)split_list(rpc).size();
+    o.rpc = rpc;
   }
+  o.master = master;
   return o;
 }
 

@@ -6,6 +6,7 @@
 //   mi-cli --synthetic llama3-70b --ftype Q4_K --bench --mb-size 16
 //   mi-cli -m m.gguf --world 2 --rank 0 --next 10.0.0.2      (one process per stage, TCP ring)
 //   mi-cli -m m.gguf --daemon      (JSON-lines server on stdin/stdout for the orchestrator)
+//   mi-cli --rpc-server 50052      (long-lived stage worker; a client attaches with --rpc host:port,..)
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -14,6 +15,7 @@
 #include "cli_common.h"
 #include "engine.h"
 #include "log.h"
+#include "rpc.h"
 #include "session.h"
 
 using namespace mp;
@@ -27,7 +29,9 @@ static void usage() {
           "  --daemon                  read {\"prompt\":..,\"n_predict\":..} lines on stdin, answer with JSON lines\n"
           "  --no-display-prompt       do not echo the prompt\n"
           "  --state-save DIR          after generating, checkpoint the KV shards + sequences to DIR\n"
-          "  --state-load DIR          resume a checkpoint: continue its sequence for -n more tokens\n");
+          "  --state-load DIR          resume a checkpoint: continue its sequence for -n more tokens\n"
+          "  --rpc-server PORT [-m LOCAL.gguf] [--device D] [--rpc-jobs N]\n"
+          "                            stage worker (llama.cpp rpc-server role): serve --rpc clients, N jobs (0 = forever)\n");
 }
 
 static int run_daemon(Session& s) {
@@ -69,7 +73,37 @@ static int run_daemon(Session& s) {
   return 0;
 }
 
+// mi-cli --rpc-server PORT [-m LOCAL.gguf] [--device D] [--rpc-jobs N] [--verbose]
+static int rpc_server_main(int argc, char** argv) {
+  int port = 0, device = -1, jobs = 0;
+  std::string gguf;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) throw std::runtime_error("missing value for " + a);
+      return argv[++i];
+    };
+    if (a == "--rpc-server") port = std::atoi(val().c_str());
+    else if (a == "-m" || a == "--model") gguf = val();
+    else if (a == "--device") device = std::atoi(val().c_str());
+    else if (a == "--rpc-jobs") jobs = std::atoi(val().c_str());
+    else if (a == "--verbose") log_set_level(LOG_DEBUG);
+    else throw std::runtime_error("--rpc-server: unknown flag " + a);
+  }
+  if (port <= 0) throw std::runtime_error("--rpc-server needs a port");
+  return run_rpc_server(port, gguf, device, jobs);
+}
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::strcmp(argv[i], "--rpc-server") == 0) {
+      try {
+        return rpc_server_main(argc, argv);
+      } catch (const std::exception& e) {
+        MP_LOGE("mi-cli: %s", e.what());
+        return 2;
+      }
+    }
   bool daemon = false;
   std::string state_save, state_load;
   CliOptions o;
@@ -92,6 +126,9 @@ int main(int argc, char** argv) {
       const int need = o.bench_prompt + o.bench_warmup + o.bench_steps + 8;
       if (o.eng.get_int("max_ctx", 2048) < need) o.eng["max_ctx"] = need;
     }
+    RpcClient rpc;
+    const bool attached = !o.bench && !daemon && state_load.empty() && !o.rpc.empty() &&
+                          rpc_attach(o.rpc, o.eng, o.prompt, o.n_predict, o.master.empty() ? "127.0.0.1" : o.master, rpc);
     Engine eng(o.eng);
     if (!o.trace.empty()) eng.enable_trace(true);
     if (o.bench) {
@@ -146,6 +183,7 @@ int main(int argc, char** argv) {
     }
     if (!state_save.empty()) eng.save_state(state_save);
     if (!o.trace.empty()) eng.write_trace(o.trace);
+    if (attached) rpc_collect(rpc);
   } catch (const std::exception& e) {
     MP_LOGE("mi-cli: error: %s", e.what());
     return 1;

@@ -1,0 +1,157 @@
+// Long-lived stage workers a client attaches to by host:port -- the role of llama.cpp's `rpc-server`
+// in the reference (`orchestrator/src/main.rs:47-48`: `--rpc 127.0.0.1:50052,127.0.0.1:50053`).
+//
+//   worker:  mi-cli --rpc-server 50052 [-m LOCAL.gguf] [--device D]      (stays up across clients)
+//   client:  mi-cli -m m.gguf --rpc 127.0.0.1:50052,127.0.0.1:50053 -p "..." -n 200
+//
+// The client is the LAST rank of a (#workers + 1)-stage pipeline -- the LM head and the sampler, so
+// the text streams out where the user is (a Session emits on the stage that owns the head); worker
+// i is rank i (worker 0: the embedding and the first layers).  Per generation the client opens one control connection per
+// worker and sends one job: the engine config with the worker's rank, the ring's hosts and ports,
+// the prompt and n_predict.  The data plane is the engine's TCP ring of the multi-process mode
+// (`--world/--rank`, engine.cpp "tcp" links: the receiver of link l listens on base_port + l), so a
+// worker is exactly a `--world/--rank` process whose arguments arrive over the socket.  The worker
+// answers with one JSON result and waits for the next client.
+//
+// Unlike llama.cpp's rpc-server, weights are not shipped over the socket: each worker loads the
+// GGUF from its own disk (the client's path, or the worker's -m), mmap'd and packed into its HBM.
+// If the first worker does not answer, the client falls back to local stages, one per --rpc entry
+// (the reference's command line then still runs on one box).
+#pragma once
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.h"
+#include "json.h"
+#include "log.h"
+#include "session.h"
+#include "transport.h"
+
+namespace mp {
+
+// one length-prefixed JSON message on a control link
+inline void rpc_send_json(Link& l, const Json& j) {
+  const std::string s = j.dump();
+  const uint64_t n = s.size();
+  l.send(&n, 8, nullptr);
+  l.send(s.data(), s.size(), nullptr);
+}
+inline Json rpc_recv_json(Link& l) {
+  uint64_t n = 0;
+  l.recv(&n, 8, nullptr);
+  if (n > (64u << 20)) throw std::runtime_error("rpc: oversized control message");
+  std::string s(n, '\0');
+  l.recv(&s[0], n, nullptr);
+  return Json::parse(s);
+}
+
+// worker loop: one job per accepted control connection; max_jobs 0 = forever
+inline int run_rpc_server(int port, const std::string& local_gguf, int device, int max_jobs) {
+  MP_LOGI("rpc worker listening on port %d", port);
+  for (int done = 0; max_jobs <= 0 || done < max_jobs; ++done) {
+    std::unique_ptr<TcpLink> ctl = TcpLink::make_receiver(port, 1e9);
+    Json res = Json::object();
+    try {
+      Json job = rpc_recv_json(*ctl);
+      Json cfg = job["engine"];
+      if (!local_gguf.empty()) cfg["gguf"] = local_gguf;
+      cfg["device"] = device >= 0 ? device : 0;   // the worker's GPU (HIP_VISIBLE_DEVICES or --device)
+      MP_LOGI("rpc job: rank %d of %d, %s", cfg.get_int("rank", -1), cfg.get_int("world", 0),
+              cfg.get_str("gguf", cfg.has("synthetic") ? "synthetic" : "?").c_str());
+      Engine eng(cfg);
+      Session s(eng, cfg.get_str("gguf", ""));
+      std::vector<GenRequest> reqs(1);
+      reqs[0].prompt = job.get_str("prompt", "");
+      reqs[0].n_predict = job.get_int("n_predict", 200);
+      reqs[0].on_piece = [](const std::string&) { return true; };
+      auto r = s.run(reqs)[0];
+      res["ok"] = true;
+      res["rank"] = cfg.get_int("rank", -1);
+      res["stages"] = eng.info()["stages"];
+      res["n_gen"] = r.n_gen;
+    } catch (const std::exception& e) {
+      MP_LOGE("rpc job failed: %s", e.what());
+      res["ok"] = false;
+      res["error"] = std::string(e.what());
+    }
+    try {
+      rpc_send_json(*ctl, res);
+    } catch (const std::exception& e) {
+      MP_LOGE("rpc: client gone before the result: %s", e.what());
+    }
+  }
+  return 0;
+}
+
+struct RpcClient {
+  std::vector<std::unique_ptr<TcpLink>> ctl;   // one control connection per worker (rank i)
+};
+
+// Attach to the workers listed by --rpc (host:port,...): on success `eng_cfg` becomes the last rank
+// of the ring and every worker has its job; false (nothing sent) when the first worker does not answer.
+inline bool rpc_attach(const std::string& rpc, Json& eng_cfg, const std::string& prompt, int n_predict,
+                       const std::string& self_host, RpcClient& cl, double connect_timeout = 0.5) {
+  std::vector<std::string> ent;
+  for (size_t a = 0; a <= rpc.size();) {
+    const size_t b = rpc.find(',', a);
+    const std::string e = rpc.substr(a, b == std::string::npos ? std::string::npos : b - a);
+    if (!e.empty()) ent.push_back(e);
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  if (ent.empty()) return false;
+  std::vector<std::string> hosts;
+  std::vector<int> ports;
+  for (auto& e : ent) {
+    const auto c = e.rfind(':');
+    if (c == std::string::npos) throw std::runtime_error("--rpc entries are host:port (got " + e + ")");
+    hosts.push_back(e.substr(0, c));
+    ports.push_back(std::atoi(e.c_str() + c + 1));
+  }
+  for (size_t i = 0; i < hosts.size(); ++i) {
+    try {
+      cl.ctl.push_back(TcpLink::make_sender(hosts[i], ports[i], i == 0 ? connect_timeout : 30.0));
+    } catch (const std::exception& e) {
+      if (i == 0) {
+        MP_LOGI("rpc: no worker at %s:%d (%s): local stages, one per --rpc entry", hosts[0].c_str(), ports[0], e.what());
+        return false;
+      }
+      throw;
+    }
+  }
+  const int world = 1 + (int)hosts.size();
+  Json h = Json::array();
+  for (auto& x : hosts) h.push(x);
+  h.push(self_host);
+  eng_cfg["mode"] = "mp";
+  eng_cfg["world"] = world;
+  eng_cfg["link"] = "tcp";
+  eng_cfg["hosts"] = h;
+  eng_cfg.erase("stages");
+  eng_cfg.erase("devices");
+  for (int r = 0; r + 1 < world; ++r) {
+    Json job = Json::object();
+    Json c = eng_cfg;
+    c["rank"] = r;
+    job["engine"] = c;
+    job["prompt"] = prompt;
+    job["n_predict"] = n_predict;
+    rpc_send_json(*cl.ctl[r], job);
+  }
+  eng_cfg["rank"] = world - 1;
+  MP_LOGI("rpc: %d worker(s) attached, ring of %d stages", world - 1, world);
+  return true;
+}
+
+// the workers' results (after the client's own generation)
+inline void rpc_collect(RpcClient& cl) {
+  for (size_t i = 0; i < cl.ctl.size(); ++i) {
+    const Json r = rpc_recv_json(*cl.ctl[i]);
+    if (!r.get_bool("ok", false)) throw std::runtime_error("rpc worker " + std::to_string(i) + ": " + r.get_str("error", "?"));
+    MP_LOGI("rpc worker %zu done: %s", i, r.dump().c_str());
+  }
+}
+
+}  // namespace mp

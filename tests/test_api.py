@@ -498,3 +498,55 @@ def test_cli_gpu_mem_force_prefetch(native_bins, tiny_gguf):
     assert "proceeding" in r.stderr and "prefetch: madvise" in r.stderr
     r = subprocess.run(base[:-2] + ["--gpu-mem", "64"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_rpc_workers_attach_by_host_port(native_bins, tiny_gguf):
+    """The reference's worker layout (`--rpc 127.0.0.1:50052,127.0.0.1:50053`, main.rs:47-48): two
+    long-lived `mi-cli --rpc-server PORT` workers; a client attaches by host:port, the three
+    processes form a TCP pipeline ring (workers: the first stages, client: the head and sampler)
+    and the client's text equals the single-process greedy text -- twice, so the workers stay up
+    across clients.  CPU backend (-ngl 0)."""
+    prompt, n = "The pipeline sends activations", "12"
+    mi = os.path.join(BIN, "mi-cli")
+    local = subprocess.run([mi, "-m", tiny_gguf, "-p", prompt, "-n", n, "-c", "256", "-ngl", "0", "--stages", "3"],
+                           capture_output=True, text=True, timeout=120)
+    assert local.returncode == 0, local.stderr
+    ports = [_free_port(), _free_port()]
+    workers = [subprocess.Popen([mi, "--rpc-server", str(p), "--rpc-jobs", "2"], stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE, text=True) for p in ports]
+    try:
+        rpc = ",".join(f"127.0.0.1:{p}" for p in ports)
+        for _ in range(2):
+            base = _free_port()
+            cli = subprocess.run([mi, "-m", tiny_gguf, "-p", prompt, "-n", n, "-c", "256", "-ngl", "0", "--rpc", rpc,
+                                  "--base-port", str(base)], capture_output=True, text=True, timeout=180)
+            assert cli.returncode == 0, cli.stderr
+            assert "2 worker(s) attached, ring of 3 stages" in cli.stderr
+            assert "rpc worker 1 done" in cli.stderr
+            assert local.stdout.rstrip("\n") and cli.stdout.rstrip("\n").startswith(local.stdout.rstrip("\n"))
+        for w in workers:
+            assert w.wait(timeout=60) == 0
+            assert "rpc job: rank" in w.stderr.read()
+    finally:
+        for w in workers:
+            if w.poll() is None:
+                w.kill()
+
+
+def test_rpc_without_workers_runs_local_stages(native_bins, tiny_gguf):
+    """No worker listening: --rpc keeps its one-box meaning (one local stage per entry)."""
+    mi = os.path.join(BIN, "mi-cli")
+    p = _free_port()
+    cli = subprocess.run([mi, "-m", tiny_gguf, "-p", "Hello", "-n", "4", "-c", "256", "-ngl", "0",
+                          "--rpc", f"127.0.0.1:{p},127.0.0.1:{p}"], capture_output=True, text=True, timeout=120)
+    assert cli.returncode == 0, cli.stderr
+    assert "local stages, one per --rpc entry" in cli.stderr
