@@ -18,7 +18,13 @@
 // If the first worker does not answer, the client falls back to local stages, one per --rpc entry
 // (the reference's command line then still runs on one box).
 #pragma once
-#include <memory>
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -27,34 +33,105 @@
 #include "json.h"
 #include "log.h"
 #include "session.h"
-#include "transport.h"
 
 namespace mp {
 
-// one length-prefixed JSON message on a control link
-inline void rpc_send_json(Link& l, const Json& j) {
-  const std::string s = j.dump();
-  const uint64_t n = s.size();
-  l.send(&n, 8, nullptr);
-  l.send(s.data(), s.size(), nullptr);
+// Control connections: plain POSIX sockets carrying length-prefixed JSON (8-byte length, then the
+// text).  The worker keeps ONE listening socket for its whole life, so a client that arrives while
+// the previous job is still answering waits in the accept backlog instead of being refused.
+struct RpcConn {
+  int fd = -1;
+  RpcConn() = default;
+  explicit RpcConn(int f) : fd(f) {}
+  RpcConn(const RpcConn&) = delete;
+  RpcConn& operator=(const RpcConn&) = delete;
+  RpcConn(RpcConn&& o) noexcept : fd(o.fd) { o.fd = -1; }
+  ~RpcConn() {
+    if (fd >= 0) ::close(fd);
+  }
+  void write_all(const void* p, size_t n) const {
+    const char* c = static_cast<const char*>(p);
+    while (n) {
+      const ssize_t w = ::send(fd, c, n, MSG_NOSIGNAL);
+      if (w <= 0) throw std::runtime_error("rpc: connection lost (send)");
+      c += w;
+      n -= (size_t)w;
+    }
+  }
+  void read_all(void* p, size_t n) const {
+    char* c = static_cast<char*>(p);
+    while (n) {
+      const ssize_t r = ::recv(fd, c, n, 0);
+      if (r <= 0) throw std::runtime_error("rpc: connection lost (recv)");
+      c += r;
+      n -= (size_t)r;
+    }
+  }
+  void send_json(const Json& j) const {
+    const std::string s = j.dump();
+    const uint64_t n = s.size();
+    write_all(&n, 8);
+    write_all(s.data(), s.size());
+  }
+  Json recv_json() const {
+    uint64_t n = 0;
+    read_all(&n, 8);
+    if (n > (64u << 20)) throw std::runtime_error("rpc: oversized control message");
+    std::string s(n, '\0');
+    read_all(&s[0], n);
+    return Json::parse(s);
+  }
+};
+
+inline int rpc_listen(int port) {
+  const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_ANY);
+  a.sin_port = htons((uint16_t)port);
+  if (ls < 0 || ::bind(ls, (sockaddr*)&a, sizeof(a)) != 0 || ::listen(ls, 16) != 0) {
+    if (ls >= 0) ::close(ls);
+    throw std::runtime_error("rpc: cannot listen on port " + std::to_string(port));
+  }
+  return ls;
 }
-inline Json rpc_recv_json(Link& l) {
-  uint64_t n = 0;
-  l.recv(&n, 8, nullptr);
-  if (n > (64u << 20)) throw std::runtime_error("rpc: oversized control message");
-  std::string s(n, '\0');
-  l.recv(&s[0], n, nullptr);
-  return Json::parse(s);
+
+// connect with retries until timeout_s (a worker may still be starting)
+inline RpcConn rpc_connect(const std::string& host, int port, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) == 0 && res) {
+      const int fd = ::socket(res->ai_family, res->ai_socktype, 0);
+      const bool ok = fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0;
+      freeaddrinfo(res);
+      if (ok) return RpcConn(fd);
+      if (fd >= 0) ::close(fd);
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      throw std::runtime_error("rpc: no worker at " + host + ":" + std::to_string(port));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
 }
 
 // worker loop: one job per accepted control connection; max_jobs 0 = forever
 inline int run_rpc_server(int port, const std::string& local_gguf, int device, int max_jobs) {
+  const int ls = rpc_listen(port);
   MP_LOGI("rpc worker listening on port %d", port);
   for (int done = 0; max_jobs <= 0 || done < max_jobs; ++done) {
-    std::unique_ptr<TcpLink> ctl = TcpLink::make_receiver(port, 1e9);
+    const int fd = ::accept(ls, nullptr, nullptr);
+    if (fd < 0) {
+      ::close(ls);
+      throw std::runtime_error("rpc: accept failed");
+    }
+    RpcConn ctl(fd);
     Json res = Json::object();
     try {
-      Json job = rpc_recv_json(*ctl);
+      Json job = ctl.recv_json();
       Json cfg = job["engine"];
       if (!local_gguf.empty()) cfg["gguf"] = local_gguf;
       cfg["device"] = device >= 0 ? device : 0;   // the worker's GPU (HIP_VISIBLE_DEVICES or --device)
@@ -77,16 +154,17 @@ inline int run_rpc_server(int port, const std::string& local_gguf, int device, i
       res["error"] = std::string(e.what());
     }
     try {
-      rpc_send_json(*ctl, res);
+      ctl.send_json(res);
     } catch (const std::exception& e) {
       MP_LOGE("rpc: client gone before the result: %s", e.what());
     }
   }
+  ::close(ls);
   return 0;
 }
 
 struct RpcClient {
-  std::vector<std::unique_ptr<TcpLink>> ctl;   // one control connection per worker (rank i)
+  std::vector<RpcConn> ctl;   // one control connection per worker (rank i)
 };
 
 // Attach to the workers listed by --rpc (host:port,...): on success `eng_cfg` becomes the last rank
@@ -112,7 +190,7 @@ inline bool rpc_attach(const std::string& rpc, Json& eng_cfg, const std::string&
   }
   for (size_t i = 0; i < hosts.size(); ++i) {
     try {
-      cl.ctl.push_back(TcpLink::make_sender(hosts[i], ports[i], i == 0 ? connect_timeout : 30.0));
+      cl.ctl.push_back(rpc_connect(hosts[i], ports[i], i == 0 ? connect_timeout : 30.0));
     } catch (const std::exception& e) {
       if (i == 0) {
         MP_LOGI("rpc: no worker at %s:%d (%s): local stages, one per --rpc entry", hosts[0].c_str(), ports[0], e.what());
@@ -130,6 +208,10 @@ inline bool rpc_attach(const std::string& rpc, Json& eng_cfg, const std::string&
   eng_cfg["link"] = "tcp";
   eng_cfg["hosts"] = h;
   eng_cfg.erase("stages");
+  // this process's GPU: the first --devices entry, else 0 (the workers pick their own)
+  int dev = 0;
+  if (eng_cfg.has("devices") && eng_cfg["devices"].is_arr() && !eng_cfg["devices"].arr().empty())
+    dev = (int)eng_cfg["devices"].arr()[0].num();
   eng_cfg.erase("devices");
   for (int r = 0; r + 1 < world; ++r) {
     Json job = Json::object();
@@ -138,9 +220,10 @@ inline bool rpc_attach(const std::string& rpc, Json& eng_cfg, const std::string&
     job["engine"] = c;
     job["prompt"] = prompt;
     job["n_predict"] = n_predict;
-    rpc_send_json(*cl.ctl[r], job);
+    cl.ctl[r].send_json(job);
   }
   eng_cfg["rank"] = world - 1;
+  eng_cfg["device"] = dev;
   MP_LOGI("rpc: %d worker(s) attached, ring of %d stages", world - 1, world);
   return true;
 }
@@ -148,7 +231,7 @@ inline bool rpc_attach(const std::string& rpc, Json& eng_cfg, const std::string&
 // the workers' results (after the client's own generation)
 inline void rpc_collect(RpcClient& cl) {
   for (size_t i = 0; i < cl.ctl.size(); ++i) {
-    const Json r = rpc_recv_json(*cl.ctl[i]);
+    const Json r = cl.ctl[i].recv_json();
     if (!r.get_bool("ok", false)) throw std::runtime_error("rpc worker " + std::to_string(i) + ": " + r.get_str("error", "?"));
     MP_LOGI("rpc worker %zu done: %s", i, r.dump().c_str());
   }

@@ -550,3 +550,30 @@ def test_rpc_without_workers_runs_local_stages(native_bins, tiny_gguf):
                           "--rpc", f"127.0.0.1:{p},127.0.0.1:{p}"], capture_output=True, text=True, timeout=120)
     assert cli.returncode == 0, cli.stderr
     assert "local stages, one per --rpc entry" in cli.stderr
+
+
+@pytest.mark.gpu
+def test_rpc_workers_hip_stages(native_bins, tiny_gguf):
+    """The --rpc worker ring on HIP stages: two workers and the client share GPU 0 (each process
+    its own HIP stage, TCP links); the client's text equals the single-process GPU text."""
+    prompt, n = "The pipeline sends activations", "12"
+    mi = os.path.join(BIN, "mi-cli")
+    local = subprocess.run([mi, "-m", tiny_gguf, "-p", prompt, "-n", n, "-c", "256", "--stages", "3", "--devices", "0"],
+                           capture_output=True, text=True, timeout=180)
+    assert local.returncode == 0, local.stderr
+    ports = [_free_port(), _free_port()]
+    workers = [subprocess.Popen([mi, "--rpc-server", str(p), "--rpc-jobs", "1", "--device", "0"], stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE, text=True) for p in ports]
+    try:
+        cli = subprocess.run([mi, "-m", tiny_gguf, "-p", prompt, "-n", n, "-c", "256", "--devices", "0",
+                              "--rpc", ",".join(f"127.0.0.1:{p}" for p in ports), "--base-port", str(_free_port())],
+                             capture_output=True, text=True, timeout=180)
+        assert cli.returncode == 0, cli.stderr
+        assert "ring of 3 stages" in cli.stderr
+        assert local.stdout.rstrip("\n") and cli.stdout.rstrip("\n").startswith(local.stdout.rstrip("\n"))
+        for w in workers:
+            assert w.wait(timeout=60) == 0
+    finally:
+        for w in workers:
+            if w.poll() is None:
+                w.kill()
