@@ -340,7 +340,7 @@ template <int PT, int EPI>
 static void gemm3_shape(GemvParams p, bool allow_split, hipStream_t st) {
   // BM: 128 rows when one 128-row block holds M; BN: 256 columns (2 tiles per wave) unless that
   // leaves fewer than half the CUs with a workgroup and the epilogue cannot split K
-  const int bm = knob(KNOB_GEMM3_BM) ? knob(KNOB_GEMM3_BM) : (p.M <= 128 ? 128 : 256);
+  const int bm = knob(KNOB_GEMM3_BM) == 128 || knob(KNOB_GEMM3_BM) == 256 ? knob(KNOB_GEMM3_BM) : (p.M <= 128 ? 128 : 256);   // (96: gemm4 only)
   const int wg256 = (p.ntiles + 15) / 16 * ((p.M + bm - 1) / bm);
   const bool splits = EPI == EPI_ATOMIC && allow_split;
   // split-K (ATOMIC) shapes: 128 columns (r6e, M = 256: 70B qkv 104 -> 77 us, o 101 -> 74, down

@@ -699,7 +699,7 @@ static int g4_bm(int ptype, int M, int ntiles, int epi = -1) {
 
 // workgroups resident per CU: 2 for the 64-row tiles and for 4-wave 128-row tiles (GEMM4_NW=4)
 static int g4_per_cu(int ptype, int bm) {
-  return bm == 64 || (bm == 128 && !is16(ptype) && knob(KNOB_GEMM4_NW) == 4) ? 2 : 1;
+  return bm == 64 || bm == 96 || (bm == 128 && !is16(ptype) && knob(KNOB_GEMM4_NW) == 4) ? 2 : 1;
 }
 
 // compute waves per workgroup for an unsplit launch: 7 (224 columns) when that fills more of the
@@ -717,7 +717,7 @@ static int g4_nwv(int ntiles, int n_mb) {
 // T16 tiles per workgroup column group
 static int g4_tpc(int ptype, int bm, int epi) {
   if (g4_w8x64(ptype, epi)) return 32;
-  return g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;
+  return g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;   // (bm 96: 8 waves x 32 columns, 16 tiles)
 }
 
 template <int PT, int EPI>
@@ -741,6 +741,9 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st, int epi_sel = EPI
     // LDS A traffic of 8 waves x 32 columns); the same 256-column workgroup tile and grid
     if (bm == 128) gemm4_go<PT, EPI, 128, false, 4, 4>(p, nsplit, st);
     else gemm4_go<PT, EPI, 256, false, 4, 4>(p, nsplit, st);
+  } else if (bm == 96) {   // (GEMM3_BM=96, A/B) ~72 KB of LDS: two 8-wave workgroups per CU
+    if (nw7) gemm4_go<PT, EPI, 96, false, 7>(p, nsplit, st);
+    else gemm4_go<PT, EPI, 96>(p, nsplit, st);
   } else if (bm == 64) {   // 60 KB of LDS: two workgroups per CU
     if (nw7) gemm4_go<PT, EPI, 64, false, 7>(p, nsplit, st);
     else gemm4_go<PT, EPI, 64>(p, nsplit, st);
@@ -845,7 +848,7 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
   if constexpr (is16(PT)) {
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E * ((avg + 127) / 128), q.nsb * 4) : 1;
     gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
-  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64)) {   // opt-in: measured slower (r8i)
+  } else if (avg <= 64 && knob(KNOB_GEMM4_MOE64) == 1) {   // opt-in: measured slower (r8i)
     // (64-row tiles with 64 columns per wave, TW = 4, measured 33 % slower still: twice the Q4_K
     // dequant per live MFMA, VALU-bound; profiles/r10c_moe_tile64x64.txt)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot ? g4_splits(n_cg * q.E, q.nsb * 4) : 1;
@@ -854,7 +857,11 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
     // the down projection unsplit: Mixtral at 256 tokens 10225-10246 vs 10091-10093 tok/s with the
     // 2 K splits that fill the 256 CUs (half the float atomics into the residual; r9i)
     const int ns = EPI == EPI_ATOMIC && !q.Yslot && knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : 1;
-    if (knob(KNOB_GEMM4_TW4) == 3) gemm4_go<PT, EPI, 128, true, 4, 4>(p, ns, st, mo, q.E);   // 4 waves x 64 columns
+    // GEMM4_MOE64 = 2: 96-row expert tiles (three 32-row fragments) at <= 80 mean rows per expert:
+    // Mixtral's ~64 routed rows per expert at 256 tokens fill 2 of 3 fragments instead of 2 of 4,
+    // and an expert rarely needs a second row block (which re-streams its weights)
+    if (knob(KNOB_GEMM4_MOE64) == 2 && avg <= 80) gemm4_go<PT, EPI, 96, true>(p, ns, st, mo, q.E);
+    else if (knob(KNOB_GEMM4_TW4) == 3) gemm4_go<PT, EPI, 128, true, 4, 4>(p, ns, st, mo, q.E);   // 4 waves x 64 columns
     else if (knob(KNOB_GEMM4_NW) == 7) gemm4_go<PT, EPI, 128, true, 7>(p, ns, st, mo, q.E);   // 224-column tiles
     else gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);
   } else {

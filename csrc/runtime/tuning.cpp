@@ -21,7 +21,7 @@ struct KnobDef {
 bool ns_ok(int v) { return v == 2 || v == 3 || v == 4; }
 bool nw_ok(int v) { return v == 4 || v == 8; }
 bool g_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; }
-bool bm_ok(int v) { return v == 0 || v == 128 || v == 256; }
+bool bm_ok(int v) { return v == 0 || v == 96 || v == 128 || v == 256; }
 bool nw4_ok(int v) { return v == 0 || v == 4 || v == 7 || v == 8; }
 
 const KnobDef kDefs[KNOB_COUNT] = {
@@ -46,7 +46,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM4_NW", 0, 0, 8, nw4_ok},
     {"GEMM4_SPREAD", 0, 0, 2, nullptr},
     {"GEMM4_WNT", 0, 0, 2, nullptr},
-    {"GEMM4_MOE64", 0, 0, 1, nullptr},
+    {"GEMM4_MOE64", 2, 0, 2, nullptr},   // 1: 64-row expert tiles (r8i: slower); 2: 96-row tiles at <= 80 rows per expert (r12i: Mixtral mb256 10262 -> 13662)
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},

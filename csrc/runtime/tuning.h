@@ -31,8 +31,9 @@ enum Knob : int {
                             // tiles of 4 waves, two workgroups per CU, split-K included)
   KNOB_GEMM4_SPREAD,        // gemm4: LDS-DMA issue after the stage barrier (0 burst, 1 spread over MFMA steps, 2 spread + waves 4-7 two steps later)
   KNOB_GEMM4_WNT,           // gemm4: non-temporal LDS-DMA of the weights (0 auto: one row block per column group, 1 on, 2 off)
-  KNOB_GEMM4_MOE64,         // gemm4 MoE mode: 64-row tiles when the mean rows per expert <= 64 (0 / 1)
-  KNOB_GEMM3_BM,            // gemm3: force rows per workgroup (0 auto, 128, 256); A/B runs only
+  KNOB_GEMM4_MOE64,         // gemm4 MoE mode: 1 = 64-row tiles at <= 64 mean rows per expert, 2 (default) = 96-row
+                            // tiles at <= 80 (two workgroups per CU), 0 = 128-row tiles
+  KNOB_GEMM3_BM,            // gemm3 / gemm4: force rows per workgroup (0 auto, 128, 256; 96 gemm4 only); A/B runs only
   KNOB_GEMM3_BN,            // gemm3: force columns per workgroup (0 auto, 128, 256)
   KNOB_GEMM3_SPLIT,         // gemm3: force the split-K factor (0 auto)
   KNOB_GEMM4_TW4,           // gemm4 dense: 4 waves x 64 columns (two MFMAs per A fragment) instead of 8 x 32

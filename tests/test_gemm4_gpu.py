@@ -52,11 +52,12 @@ def tuning(native):
 
 
 @pytest.mark.parametrize("qt", TYPES)
-@pytest.mark.parametrize("bm", [0, 128, 256])
+@pytest.mark.parametrize("bm", [0, 96, 128, 256])
 @pytest.mark.parametrize("M", [65, 200, 300])
 def test_gemm4_tiles(cuda, tuning, qt, bm, M):
     """STORE / ATOMIC (auto split) / SwiGLU on 13 tiles (a partial 256-column group), 5
-    super-blocks (20 stages), partial row blocks, for every row tile."""
+    super-blocks (20 stages), partial row blocks, for every row tile (96: three 32-row fragments,
+    two workgroups per CU; 16-bit weights keep 128)."""
     from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
     tuning(bm, 0, 0, 0)
     n, k = 208, 1280

@@ -5,8 +5,8 @@ The weights are random GGUF blocks (Q4_K gate/up, Q6_K down, as in Mixtral Q4_K_
 engine's packer; the oracle dequantizes them with the unpack kernel (itself checked against the
 numpy dequantizer in test_kernels_gpu.py) and runs fp32 matmuls per routed expert.  M covers a
 65-token call (16 rows per expert), the 256-sequence decode micro-batch (64 rows per expert) and a
-512-token prompt chunk (128 per expert), with the default 128-row tiles and the opt-in 64-row ones
-(knob GEMM4_MOE64)."""
+512-token prompt chunk (128 per expert), with the default 128-row tiles and the opt-in 64- and 96-row
+ones (knob GEMM4_MOE64 1 / 2), plus a skewed routing."""
 import numpy as np
 import pytest
 import torch
@@ -53,7 +53,7 @@ def experts(native):
     return gu, dn, gu_all, dn_all
 
 
-@pytest.fixture(params=[0, 1], ids=["tile128", "tile64"])
+@pytest.fixture(params=[0, 1, 2], ids=["tile128", "tile64", "tile96"])
 def moe64(request, native):
     from mipipe import _native as N
     N.check(N.lib().mp_set_knob(b"GEMM4_MOE64", request.param), "knob")
@@ -61,12 +61,19 @@ def moe64(request, native):
     N.lib().mp_set_knob(b"GEMM4_MOE64", 0)
 
 
-@pytest.mark.parametrize("M", [65, 256, 512])
+@pytest.mark.parametrize("M", [65, 256, 512, "256skew"])
 def test_moe_grouped_gemm_mixtral_widths(cuda, experts, moe64, M):
+    """("256skew": expert 0 favoured, so it gets several row blocks of any tile height, e.g. three
+    of the 96-row tiles, while the others run short ones.)"""
     from mipipe.ops.kernels import moe_route, moe_gemm, EPI_SWIGLU, EPI_ATOMIC
     gu, dn, gu_all, dn_all = experts
-    g = torch.Generator().manual_seed(M)
-    logits = torch.randn(M, E, generator=g).cuda()
+    skew = M == "256skew"
+    M = 256 if skew else M
+    g = torch.Generator().manual_seed(M + skew)
+    logits = torch.randn(M, E, generator=g)
+    if skew:
+        logits[:, 0] += 2.5
+    logits = logits.cuda()
     counts, lists, weights = moe_route(logits, K_TOP)
     x = torch.randn(M, gu[0].k_pad, generator=g).half().cuda()
     h = torch.zeros(M * K_TOP, dn[0].k_pad, dtype=torch.float16, device="cuda")
