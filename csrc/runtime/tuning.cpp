@@ -50,7 +50,7 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
-    {"GEMM4_TW4", 1, 0, 6, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
+    {"GEMM4_TW4", 1, 0, 8, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
     {"GEMV_SPLIT_WAVES", 2048, 64, 1 << 20, nullptr},
     {"GEMV_SPLIT_MINSB", 4, 1, 64, nullptr},
 #ifdef MIPIPE_TIMING_PROBES
