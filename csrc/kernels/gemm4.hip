@@ -277,8 +277,7 @@ struct G4Geom {
   static constexpr int A_INSTR = (NP + NWV - 1) / NWV;        // per wave (uniform: vmcnt accounting)
 };
 
-// FL (compile-time flags): bit 6: two workgroups per CU (registers capped at 128 per lane; with
-// the 128-row 7-wave tile's 81408 B of LDS); bits 0-1 LDS-DMA spread mode, bit 2 non-temporal weights; bits 3-5 timing
+// FL (compile-time flags): bits 0-1 LDS-DMA spread mode, bit 2 non-temporal weights; bits 3-5 timing
 // probes (probe builds only, wrong results): 3 raw bits as B fragments (no dequant VALU), 4 no MFMAs
 // (operands kept live), 5 no LDS-DMA (the stage images keep stale bytes).  Compile-time
 // because every weight DMA of a stage branched on them at run time: the 2-stage loop body of the MoE
@@ -288,7 +287,7 @@ struct G4Geom {
 // share every A fragment; the 64-row MoE tile, where 32-column waves left half the MFMAs of a
 // 128-row tile on padding rows)
 template <int PT, int EPI, int BM, bool MOE, int NWV = 8, int FL = 0, int TW = 2>
-__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 && TW == 2 ? 2 : (FL & 64) ? 4 : 1))) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
+__global__ __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NWV == 4 && TW == 2 ? 2 : 1))) void gemm4_kernel(const GemvParams p, const int n_mb, const int st_per_split,
                                                     const int n_stages, const G4Moe mo) {
   static_assert(TW == 2 || TW == 4, "gemm4: 2 or 4 tiles per wave");
   constexpr int NPR = TW / 2;   // 32-column pairs per wave
@@ -620,7 +619,7 @@ static int g4_splits(int wgs, int n_stages, int per_cu = 1) {
   return std::max(1, std::min(target / wgs, n_stages / 16));
 }
 
-template <int PT, int EPI, int BM, bool MOE = false, int NWV = 8, int TW = 2, int FX = 0>
+template <int PT, int EPI, int BM, bool MOE = false, int NWV = 8, int TW = 2>
 static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe& mo = mpk::G4Moe{}, int E = 1) {
   const int n_cg = (p.ntiles + TW * NWV - 1) / (TW * NWV);
   const int n_mb = (p.M + BM - 1) / BM;   // MoE: p.M = the most rows one expert can get
@@ -640,7 +639,7 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
   const int wk = knob(KNOB_GEMM4_WNT);
   const bool wnt = wk == 1 || (wk == 0 && (MOE || n_mb == 1));
   const dim3 grid(n_cg * n_mb, nsplit, E), block(64 * NWV);
-#define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, (F) | FX, TW>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
+#define G4_LAUNCH(F) hipLaunchKernelGGL((mpk::gemm4_kernel<PT, EPI, BM, MOE, NWV, F, TW>), grid, block, 0, st, p, n_mb, per, n_stages, mo)
 #ifdef MIPIPE_TIMING_PROBES
   // timing probes (knob GEMM4_PROBE): Q4_K dense gate/up (SwiGLU, 256 rows) and split-K stores
   if constexpr (PT == P_Q4_K && ((!MOE && ((EPI == EPI_SWIGLU && BM == 256) || (EPI == EPI_STORE && BM == 128))) ||
@@ -684,14 +683,9 @@ static void gemm4_go(GemvParams p, int nsplit, hipStream_t st, const mpk::G4Moe&
 // gate/up only, 6: the split-K shapes only): a 128 x 512 workgroup tile whose A fragments each feed
 // two MFMAs (half the A-fragment LDS reads per MFMA of the 8 x 32 form) at two waves per SIMD (128
 // accumulators + ~110 registers: 237 VGPRs, no spills)
-// 7-wave 128-row tiles at two workgroups per CU (GEMM4_TW4 7: the whole-K SwiGLU gate/up, 8: every
-// dense shape; 81408 B of LDS and <= 128 registers each, so two share a CU and hide each other's
-// stage barriers and DMA waits -- the 96-row MoE tile's lever, r12i)
-static bool g4_two_per_cu(int ptype, int epi) {
-  const int k = knob(KNOB_GEMM4_TW4);
-  return !is16(ptype) && (k == 8 || (k == 7 && epi == EPI_SWIGLU));
-}
-
+// (A 7-wave 128-row tile at two workgroups per CU -- 81408 B of LDS fits, but the 128-register
+// cap it needs spilled VGPRs that hold in-flight asm LDS reads: tools/isa_lint.py, 82 findings.
+// Not shipped; the 96-row MoE tile reaches two per CU within its registers, r12i.)
 static bool g4_w8x64(int ptype, int epi) {
   const int k = knob(KNOB_GEMM4_TW4);
   return !is16(ptype) && (k == 4 || (k == 5 && epi == EPI_SWIGLU) || (k == 6 && epi != EPI_SWIGLU));
@@ -700,7 +694,7 @@ static bool g4_w8x64(int ptype, int epi) {
 static int g4_bm(int ptype, int M, int ntiles, int epi = -1) {
   if (is16(ptype)) return 128;
   if (knob(KNOB_GEMM3_BM)) return knob(KNOB_GEMM3_BM);
-  if (epi >= 0 && (g4_w8x64(ptype, epi) || g4_two_per_cu(ptype, epi))) return 128;
+  if (epi >= 0 && g4_w8x64(ptype, epi)) return 128;
   if (M <= 128) return 128;
   const int cgs = (ntiles + 15) / 16;
   return cgs * ((M + 255) / 256) < 192 && cgs * ((M + 127) / 128) <= 512 ? 128 : 256;
@@ -726,7 +720,6 @@ static int g4_nwv(int ntiles, int n_mb) {
 // T16 tiles per workgroup column group
 static int g4_tpc(int ptype, int bm, int epi) {
   if (g4_w8x64(ptype, epi)) return 32;
-  if (g4_two_per_cu(ptype, epi)) return 14;
   return g4_per_cu(ptype, bm) == 2 && bm == 128 ? 8 : 16;   // (bm 96: 8 waves x 32 columns, 16 tiles)
 }
 
@@ -736,10 +729,6 @@ static void gemm4_bm(GemvParams p, int nsplit, hipStream_t st, int epi_sel = EPI
   const bool nw7 = nsplit == 1 && g4_nwv(p.ntiles, (p.M + bm - 1) / bm) == 7;
   if constexpr (is16(PT)) {
     gemm4_go<PT, EPI, 128>(p, nsplit, st);
-  } else if (mpk::G4Geom<PT, 128, 7, 2>::NB * mpk::G4Geom<PT, 128, 7, 2>::STAGE <= 80 * 1024 && g4_two_per_cu(PT, epi_sel)) {
-    // (the types whose 7-wave 128-row stage ring fits half the CU's LDS: Q4_K 81408 B)
-    if constexpr (mpk::G4Geom<PT, 128, 7, 2>::NB * mpk::G4Geom<PT, 128, 7, 2>::STAGE <= 80 * 1024)
-      gemm4_go<PT, EPI, 128, false, 7, 2, 64>(p, nsplit, st);
   } else if (g4_w8x64(PT, epi_sel)) {
     // 7 waves (448 columns) when that fills more of the 256 CUs in whole rounds
     const int n_mb = (p.M + 127) / 128;
@@ -786,7 +775,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
     const int n_stages = p.nsb * 4;
     int ns = 1;
     if (scratch) {   // split-K partial stores: split s writes scratch + s * M * ldp
-      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_two_per_cu(PT, esel) ? 2 : g4_per_cu(PT, bm));
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(PT, bm));
       const int per = (n_stages + ns - 1) / ns;
       ns = (n_stages + per - 1) / per;
       const int ldp = p.ntiles * 16;
@@ -797,7 +786,7 @@ static bool gemm4_pt(int epi, GemvParams p, bool allow_split, hipStream_t st, fl
       return true;
     }
     if (epi == EPI_ATOMIC && allow_split)
-      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_two_per_cu(PT, esel) ? 2 : g4_per_cu(PT, bm));
+      ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(PT, bm));
     switch (epi) {
       case EPI_STORE: gemm4_bm<PT, EPI_STORE>(p, 1, st); break;
       case EPI_ATOMIC: gemm4_bm<PT, EPI_ATOMIC>(p, ns, st); break;
@@ -826,7 +815,7 @@ int gemm4_splits(int ptype, int ntiles, int nsb, int M) {
   const int tpc = g4_tpc(ptype, bm, EPI_ATOMIC);
   const int wgs = (ntiles + tpc - 1) / tpc * ((M + bm - 1) / bm);
   const int n_stages = nsb * 4;
-  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_two_per_cu(ptype, EPI_ATOMIC) ? 2 : g4_per_cu(ptype, bm));
+  int ns = knob(KNOB_GEMM3_SPLIT) > 0 ? knob(KNOB_GEMM3_SPLIT) : g4_splits(wgs, n_stages, g4_per_cu(ptype, bm));
   ns = std::max(1, std::min(ns, n_stages));
   const int per = (n_stages + ns - 1) / ns;
   return (n_stages + per - 1) / per;
@@ -874,7 +863,13 @@ static void moe4_go(const MoeGemvParams& q, hipStream_t st) {
     // GEMM4_MOE64 = 2: 96-row expert tiles (three 32-row fragments) at <= 80 mean rows per expert:
     // Mixtral's ~64 routed rows per expert at 256 tokens fill 2 of 3 fragments instead of 2 of 4,
     // and an expert rarely needs a second row block (which re-streams its weights)
-    if (knob(KNOB_GEMM4_MOE64) == 2 && avg <= 80) gemm4_go<PT, EPI, 96, true>(p, ns, st, mo, q.E);
+    // and the down projection split 4 ways over K (float atomics into the token rows, which the two
+    // slots of a token share anyway): its ~16 column groups x 8 experts are ~128 live workgroups on
+    // 256 CUs.  Mixtral mb256 13495 -> 14546 tok/s with GEMM3_SPLIT=4 (r12m); GEMM4_MOE64=3: unsplit
+    if (knob(KNOB_GEMM4_MOE64) >= 2 && avg <= 80) {
+      const int ns96 = EPI == EPI_ATOMIC && !q.Yslot && knob(KNOB_GEMM3_SPLIT) == 0 && knob(KNOB_GEMM4_MOE64) == 2 ? 4 : ns;
+      gemm4_go<PT, EPI, 96, true>(p, ns96, st, mo, q.E);
+    }
     else if (knob(KNOB_GEMM4_TW4) == 3) gemm4_go<PT, EPI, 128, true, 4, 4>(p, ns, st, mo, q.E);   // 4 waves x 64 columns
     else if (knob(KNOB_GEMM4_NW) == 7) gemm4_go<PT, EPI, 128, true, 7>(p, ns, st, mo, q.E);   // 224-column tiles
     else gemm4_go<PT, EPI, 128, true>(p, ns, st, mo, q.E);

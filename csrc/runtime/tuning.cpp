@@ -46,11 +46,11 @@ const KnobDef kDefs[KNOB_COUNT] = {
     {"GEMM4_NW", 0, 0, 8, nw4_ok},
     {"GEMM4_SPREAD", 0, 0, 2, nullptr},
     {"GEMM4_WNT", 0, 0, 2, nullptr},
-    {"GEMM4_MOE64", 2, 0, 2, nullptr},   // 1: 64-row expert tiles (r8i: slower); 2: 96-row tiles at <= 80 rows per expert (r12i: Mixtral mb256 10262 -> 13662)
+    {"GEMM4_MOE64", 2, 0, 3, nullptr},   // 1: 64-row expert tiles (r8i: slower); 2: 96-row tiles at <= 80 rows per expert (r12i: Mixtral mb256 10262 -> 13662), down split 4 over K; 3: the same unsplit
     {"GEMM3_BM", 0, 0, 256, bm_ok},
     {"GEMM3_BN", 0, 0, 256, bm_ok},
     {"GEMM3_SPLIT", 0, 0, 1 << 10, nullptr},
-    {"GEMM4_TW4", 1, 0, 8, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
+    {"GEMM4_TW4", 1, 0, 6, nullptr},   // r10u: 70B mb256 5756 -> 5792 (gate/up only); all tiles: 5570 (r10t)
     {"GEMV_SPLIT_WAVES", 2048, 64, 1 << 20, nullptr},
     {"GEMV_SPLIT_MINSB", 4, 1, 64, nullptr},
 #ifdef MIPIPE_TIMING_PROBES

@@ -175,7 +175,7 @@ def test_gemm4_seven_wave_tiles(cuda, native, qt, nw, M):
 
 
 @pytest.mark.parametrize("qt", [Q.Q4_K, Q.Q6_K, Q.Q8_0])
-@pytest.mark.parametrize("form", ["tw4", "nw4", "w8x64", "w7x64", "two_per_cu"])
+@pytest.mark.parametrize("form", ["tw4", "nw4", "w8x64", "w7x64"])
 @pytest.mark.parametrize("k", [2048, 2304])
 @pytest.mark.parametrize("M", [65, 256])
 def test_gemm4_four_wave_tiles(cuda, tuning, qt, form, k, M):
@@ -183,13 +183,12 @@ def test_gemm4_four_wave_tiles(cuda, tuning, qt, form, k, M):
     AGPRs (GEMM4_TW4=2; the AGPR -> VGPR epilogue copies once landed on in-flight LDS reads at the
     loop's even exit), 32 columns per wave at two workgroups per CU (GEMM4_NW=4), and 8 / 7 waves x
     64 columns on 128-row tiles (GEMM4_TW4=4, GEMM4_NW=7 for the 448-column group: 40 tiles = one
-    full group plus a partial one), and the 7-wave 128-row tile at two workgroups per CU
-    (GEMM4_TW4=8: registers capped at 128; Q4_K only, the other types take the plain tile).  An even (32) and an odd (36) stage count, STORE / SwiGLU /
+    full group plus a partial one).  An even (32) and an odd (36) stage count, STORE / SwiGLU /
     split-K ATOMIC over a non-zero residual."""
     from mipipe import _native as N
     from mipipe.ops.kernels import PackedWeight, gemm, EPI_STORE, EPI_ATOMIC, EPI_SWIGLU
     knobs = {"tw4": [(b"GEMM4_TW4", 2)], "nw4": [(b"GEMM4_NW", 4)], "w8x64": [(b"GEMM4_TW4", 4)],
-             "w7x64": [(b"GEMM4_TW4", 4), (b"GEMM4_NW", 7)], "two_per_cu": [(b"GEMM4_TW4", 8)]}[form]
+             "w7x64": [(b"GEMM4_TW4", 4), (b"GEMM4_NW", 7)]}[form]
     for name, val in knobs:
         N.check(N.lib().mp_set_knob(name, val), "knob")
     try:
